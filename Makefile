@@ -1,0 +1,27 @@
+# Builds the gfx950 HIP library behind the C ABI in include/binquant_amd.h.
+# The .so is written in-tree (binquant_amd/lib/) so it travels to the GPU box.
+HIPCC     ?= /opt/rocm/bin/hipcc
+ARCH      ?= gfx950
+HIPFLAGS  ?= -O3 --offload-arch=$(ARCH) -ffp-contract=off -fPIC -std=c++17 \
+             -Iinclude -Ibinquant_amd/csrc -Wall -Wno-unused-function
+SRCS      := $(wildcard binquant_amd/csrc/*.hip)
+OBJS      := $(patsubst binquant_amd/csrc/%.hip,build/%.o,$(SRCS))
+LIB       := binquant_amd/lib/libbinquant_amd.so
+
+all: $(LIB)
+
+build/%.o: binquant_amd/csrc/%.hip binquant_amd/csrc/bq_device.h include/binquant_amd.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p binquant_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+resource-usage: $(SRCS)
+	@for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "remark" ; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean resource-usage

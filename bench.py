@@ -1,0 +1,289 @@
+"""Benchmark: symbol-candles/s for the full 14-column indicator set on MI355X.
+
+Workload per GPU (weak scaling): the C4 shard of BASELINE.json configs[3] —
+12 500 symbols x 10 000 candles of synthetic fp64 OHLCV resident in HBM; at 8
+GPUs that is the 100k x 10k configuration. One step = one bq_enrich launch
+over the rank's shard (reads 5 inputs, writes 14 columns). Ranks share no data
+(symbols are independent); the only collective is the MAX of the timings.
+
+Also reported (same JSON line):
+  roofline     — algorithmic bytes (152 B/candle) / mean kernel time (HIP
+                 events on the launch stream) vs 8 TB/s HBM peak; traffic from
+                 the committed rocprofv3 PMC summary when present;
+  cpu_baseline — the oracle's pandas per-symbol path (the reference call
+                 pattern) on the host cores, rank 0 at N=1, time-bounded sample;
+  tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
+                 latency p50/p99;
+  breadth      — C5 leg (market features + breadth partials + RCCL all-reduce).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from binquant_amd import engine  # noqa: E402
+from binquant_amd._lib import ENRICH_COLUMNS  # noqa: E402
+from binquant_amd.synth import device_panel  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_CANDLE = 8 * (5 + len(ENRICH_COLUMNS))   # 5 inputs read + 14 columns written = 152 B
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--symbols", type=int, default=12_500, help="symbols per GPU")
+    ap.add_argument("--candles", type=int, default=10_000)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tick-symbols", type=int, default=10_000)
+    ap.add_argument("--ticks", type=int, default=2000)
+    ap.add_argument("--no-tick", action="store_true")
+    ap.add_argument("--no-breadth", action="store_true")
+    ap.add_argument("--breadth-steps", type=int, default=5)
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _cpu_worker(args):
+    """One host process: reference call pattern (one pandas frame per symbol,
+    oracle.indicators_ref.indicators_enrichment) until the time budget ends."""
+    seed, T, budget = args
+    import pandas as pd
+
+    from binquant_amd.synth import numpy_symbol
+    from oracle import indicators_ref as ref
+
+    done, spent, s = 0, 0.0, 0
+    while spent < budget:
+        sym = numpy_symbol(T, seed * 100_000 + s, scale=100.0)
+        df = pd.DataFrame(sym)
+        t0 = time.perf_counter()
+        ref.indicators_enrichment(df)
+        spent += time.perf_counter() - t0
+        done += T
+        s += 1
+    return done, spent, s
+
+
+def cpu_baseline(args, T):
+    import multiprocessing as mp
+
+    workers = max(1, args.cpu_workers)
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(i, T, args.cpu_seconds) for i in range(workers)])
+    wall = time.perf_counter() - t0
+    candles = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)
+    syms = sum(r[2] for r in res)
+    return {
+        "value": candles / busy,
+        "unit": "symbol-candles/s",
+        "cores": workers,
+        "kind": "port",
+        "sample": f"{syms} symbols x {T} candles, pandas per-symbol indicators_enrichment "
+        f"(oracle restatement), {workers} processes, ~{args.cpu_seconds:.0f}s each (wall {wall:.1f}s)",
+    }
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def bench_tick(args, dev):
+    S = args.tick_symbols
+    hist = device_panel(S, 400, device=dev, seed=7)
+    st = engine.TickState(S)
+    st.seed(hist["open"], hist["high"], hist["low"], hist["close"], hist["volume"])
+    rng = np.random.default_rng(0)
+    host_in = torch.empty((5, S), dtype=torch.float64).pin_memory()
+    dev_in = torch.empty((5, S), dtype=torch.float64, device=dev)
+    outs = {k: torch.empty(S, dtype=torch.float64, device=dev) for k in ENRICH_COLUMNS}
+    host_out = torch.empty((len(ENRICH_COLUMNS), S), dtype=torch.float64).pin_memory()
+    dev_out = torch.empty((len(ENRICH_COLUMNS), S), dtype=torch.float64, device=dev)
+    outs = {k: dev_out[i] for i, k in enumerate(ENRICH_COLUMNS)}
+    last = hist["close"][:, -1].cpu().numpy()
+    lat = []
+    n = args.ticks
+    for i in range(n + 50):
+        c = last * np.exp(rng.normal(0, 0.002, S))
+        o = last
+        hi = np.maximum(o, c) * 1.001
+        lo = np.minimum(o, c) * 0.999
+        v = rng.lognormal(3, 1, S)
+        host_in.numpy()[:] = np.stack([o, hi, lo, c, v])
+        last = c
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev_in.copy_(host_in, non_blocking=True)
+        st.tick([dev_in[j] for j in range(5)], out=outs)
+        host_out.copy_(dev_out, non_blocking=True)
+        torch.cuda.synchronize()
+        if i >= 50:
+            lat.append(time.perf_counter() - t0)
+    lat = np.array(lat) * 1e3
+    return {
+        "symbols": S,
+        "ticks": n,
+        "p50_ms": float(np.percentile(lat, 50)),
+        "p99_ms": float(np.percentile(lat, 99)),
+        "max_ms": float(lat.max()),
+        "includes": "H2D 5xS fp64 (pinned) + bq_tick + D2H 14xS fp64, synchronized",
+    }
+
+
+def bench_breadth(args, panel, world, dev):
+    """C5 leg: features -> partials -> RCCL all-reduce(sum) of [T x 10]."""
+    h, l, c = panel["high"], panel["low"], panel["close"]
+    S, T = c.shape
+    feats = engine.market_features(h, l, c, max_bars=400)
+    part = engine.breadth_partial(c, feats)
+    steps = max(1, args.breadth_steps)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        engine.market_features(h, l, c, max_bars=400, out=feats)
+        engine.breadth_partial(c, feats, out=part)
+        if world > 1:
+            dist.all_reduce(part)
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world) / steps
+    return {
+        "value": S * T * world / dt,
+        "unit": "symbol-candles/s",
+        "ms_per_step": dt * 1e3,
+        "workload": f"{S} symbols x {T} candles per GPU, max_bars 400, features + partials"
+        + (" + RCCL all_reduce [T x 10] fp64" if world > 1 else ""),
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    S, T = args.symbols, args.candles
+    panel = device_panel(S, T, device=dev, seed=1234 + rank)
+    out = {k: torch.empty((S, T), dtype=torch.float64, device=dev) for k in ENRICH_COLUMNS}
+    stream = torch.cuda.current_stream()
+
+    def step():
+        engine.enrich(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"], out=out)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    barrier(world)
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    wall = max_over_ranks(wall, world)
+    kern_ms = max_over_ranks(kern_ms, world)
+    ms_per_step = wall / args.steps * 1e3
+    value = S * T * world / (wall / args.steps)
+    bytes_launch = S * T * BYTES_PER_CANDLE
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = pmc_traffic("enrich_kernel")
+
+    result = {
+        "metric": "symbol-candles/s for full indicator set (14 fp64 columns)",
+        "value": value,
+        "unit": "symbol-candles/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY §8d random-walk klines generated in HBM)",
+        "config": {
+            "workload": f"C4 shard: {S} symbols x {T} candles per GPU ({S * world} x {T} total)",
+            "symbols_per_gpu": S,
+            "candles": T,
+            "columns": list(ENRICH_COLUMNS),
+            "parallelism": f"symbol-sharded x{world}, no data-path collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "enrich_kernel",
+            "kernel_ms": kern_ms,
+            "algorithmic_bytes_per_candle": BYTES_PER_CANDLE,
+        },
+    }
+    del out
+    if not args.no_breadth:
+        result["breadth"] = bench_breadth(args, panel, world, dev)
+    del panel
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_tick:
+        result["tick"] = bench_tick(args, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args, T)
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

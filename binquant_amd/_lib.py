@@ -1,0 +1,154 @@
+"""ctypes binding of the gfx950 HIP library (``include/binquant_amd.h``).
+
+The library is built in-tree by ``make`` (or ``__graft_entry__.build()``) into
+``binquant_amd/lib/libbinquant_amd.so``. There is no CPU fallback: if the
+library is missing, or a call returns a non-zero status, this module raises.
+
+torch is imported first so that the HIP runtime torch ships
+(``libamdhip64.so.7``) is the one the loader binds our library to; device
+pointers and streams are then shared with torch's allocator and streams.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (binds libamdhip64.so.7 before our library loads)
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libbinquant_amd.so"
+
+BQ_OK = 0
+BQ_EINVAL = -1
+BQ_EHIP = -2
+BQ_ESTATE = -4
+
+ENRICH_COLUMNS = (
+    "ma_7",
+    "ma_25",
+    "ma_100",
+    "macd",
+    "macd_signal",
+    "rsi",
+    "bb_upper",
+    "bb_mid",
+    "bb_lower",
+    "ATR",
+    "twap",
+    "ema20",
+    "ema50",
+    "mfi",
+)
+INPUT_FIELDS = ("open", "high", "low", "close", "volume")
+FEATURE_COLUMNS = ("return_pct", "ema20", "ema50", "trend_score", "atr_pct", "bb_width")
+PARTIAL_COLUMNS = (
+    "count",
+    "advancers",
+    "decliners",
+    "above_ema20",
+    "above_ema50",
+    "sum_return",
+    "sum_trend",
+    "sum_atr_pct",
+    "sum_bb_width",
+    "reserved",
+)
+MAX_WINDOW = 126
+
+
+class BqParams(ctypes.Structure):
+    """Mirror of ``bq_params`` (include/binquant_amd.h)."""
+
+    _fields_ = [
+        ("ma_periods", ctypes.c_int32 * 3),
+        ("macd_fast", ctypes.c_int32),
+        ("macd_slow", ctypes.c_int32),
+        ("macd_signal", ctypes.c_int32),
+        ("rsi_window", ctypes.c_int32),
+        ("bb_window", ctypes.c_int32),
+        ("bb_ddof", ctypes.c_int32),
+        ("atr_window", ctypes.c_int32),
+        ("twap_window", ctypes.c_int32),
+        ("ema_spans", ctypes.c_int32 * 2),
+        ("mfi_window", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("bb_k", ctypes.c_double),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); every symbol declared in include/binquant_amd.h
+SIGNATURES: dict[str, tuple] = {
+    "bq_default_params": (None, [ctypes.POINTER(BqParams)]),
+    "bq_version": (ctypes.c_char_p, []),
+    "bq_device_arch": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    "bq_enrich": (
+        ctypes.c_int,
+        [_PP, _I64, _I64, _I64, ctypes.POINTER(BqParams), _PP, _I64, _P],
+    ),
+    "bq_state_create": (
+        ctypes.c_int,
+        [ctypes.POINTER(ctypes.c_void_p), _I64, ctypes.POINTER(BqParams)],
+    ),
+    "bq_state_destroy": (ctypes.c_int, [_P]),
+    "bq_state_seed": (ctypes.c_int, [_P, _PP, _I64, _I64, _P]),
+    "bq_tick": (ctypes.c_int, [_P, _PP, _PP, _P]),
+    "bq_state_symbols": (_I64, [_P]),
+    "bq_state_count": (_I64, [_P]),
+    "bq_market_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _PP, _I64, _P]),
+    "bq_breadth_partial": (ctypes.c_int, [_P, _PP, _I64, _I64, _I64, _I64, _P, _P]),
+}
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+_lib: ctypes.CDLL | None = None
+
+
+def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load (once) and type the native library. Raises if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise NativeLibraryError(
+            f"binquant_amd native library not found at {p}; run `make` "
+            "(or __graft_entry__.build()) — there is no CPU fallback"
+        )
+    lib = ctypes.CDLL(str(p), mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status == BQ_OK:
+        return
+    if status == BQ_EINVAL:
+        raise ValueError(f"{what}: invalid argument (status {status})")
+    raise RuntimeError(f"{what}: native call failed with status {status}")
+
+
+def default_params() -> BqParams:
+    p = BqParams()
+    load().bq_default_params(ctypes.byref(p))
+    return p
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for i, v in enumerate(ptrs):
+        arr[i] = v if v else None
+    return arr

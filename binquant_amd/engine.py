@@ -1,0 +1,268 @@
+"""Batched device entry points over the C ABI (torch tensors in, torch tensors out).
+
+All tensors are float64 CUDA (HIP) tensors shaped [S, T] with unit stride
+along T (any row stride). Launches go on torch's current stream, so results
+are ordered with surrounding torch work and can be timed with torch events.
+There is no CPU path: non-CUDA input raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from ._lib import ENRICH_COLUMNS, FEATURE_COLUMNS, INPUT_FIELDS, PARTIAL_COLUMNS
+
+
+@dataclass
+class IndicatorParams:
+    """Python mirror of ``bq_params``; defaults are the reference's windows
+    (producers/context_evaluator.py:249-261)."""
+
+    ma_periods: tuple[int, int, int] = (7, 25, 100)
+    macd_fast: int = 12
+    macd_slow: int = 26
+    macd_signal: int = 9
+    rsi_window: int = 14
+    bb_window: int = 20
+    bb_ddof: int = 1
+    bb_k: float = 2.0
+    atr_window: int = 14
+    twap_window: int = 12
+    ema_spans: tuple[int, int] = (20, 50)
+    mfi_window: int = 14
+    extra: dict = field(default_factory=dict)
+
+    def to_c(self) -> _lib.BqParams:
+        p = _lib.BqParams()
+        for i, v in enumerate(self.ma_periods):
+            p.ma_periods[i] = int(v)
+        p.macd_fast = int(self.macd_fast)
+        p.macd_slow = int(self.macd_slow)
+        p.macd_signal = int(self.macd_signal)
+        p.rsi_window = int(self.rsi_window)
+        p.bb_window = int(self.bb_window)
+        p.bb_ddof = int(self.bb_ddof)
+        p.atr_window = int(self.atr_window)
+        p.twap_window = int(self.twap_window)
+        p.ema_spans[0] = int(self.ema_spans[0])
+        p.ema_spans[1] = int(self.ema_spans[1])
+        p.mfi_window = int(self.mfi_window)
+        p.bb_k = float(self.bb_k)
+        return p
+
+    def as_oracle_dict(self) -> dict:
+        return dict(
+            ma_periods=tuple(self.ma_periods),
+            macd_fast=self.macd_fast,
+            macd_slow=self.macd_slow,
+            macd_signal=self.macd_signal,
+            rsi_window=self.rsi_window,
+            bb_window=self.bb_window,
+            bb_ddof=self.bb_ddof,
+            bb_k=self.bb_k,
+            atr_window=self.atr_window,
+            twap_window=self.twap_window,
+            ema_spans=tuple(self.ema_spans),
+            mfi_window=self.mfi_window,
+        )
+
+
+def _stream_handle(stream: torch.cuda.Stream | None) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _check_panel(x: torch.Tensor, name: str, shape=None) -> torch.Tensor:
+    if not isinstance(x, torch.Tensor) or not x.is_cuda:
+        raise ValueError(f"{name}: expected a float64 CUDA tensor (no CPU path)")
+    if x.dtype != torch.float64:
+        raise ValueError(f"{name}: expected dtype float64, got {x.dtype}")
+    if x.dim() == 1:
+        x = x.unsqueeze(0)
+    if x.dim() != 2 or (x.shape[1] > 1 and x.stride(1) != 1):
+        raise ValueError(f"{name}: expected [S, T] with unit stride along T")
+    if shape is not None and tuple(x.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(x.shape)} != {tuple(shape)}")
+    return x
+
+
+def _row_stride(x: torch.Tensor) -> int:
+    return int(x.stride(0)) if x.shape[0] > 1 else int(x.shape[1])
+
+
+def enrich(
+    open_: torch.Tensor,
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    volume: torch.Tensor,
+    params: IndicatorParams | None = None,
+    columns=ENRICH_COLUMNS,
+    out: dict[str, torch.Tensor] | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """Full (or partial) indicator set over a [S, T] panel in ONE kernel launch.
+
+    Replaces ContextEvaluator.indicators_enrichment
+    (producers/context_evaluator.py:240-263) applied symbol by symbol.
+    Returns {column_name: [S, T] float64 tensor}.
+    """
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    ins = [
+        _check_panel(t, n, (S, T))
+        for t, n in zip((open_, high, low, close, volume), INPUT_FIELDS)
+    ]
+    ld_in = _row_stride(ins[0])
+    if any(_row_stride(t) != ld_in for t in ins):
+        ins = [t.contiguous() for t in ins]
+        ld_in = T
+    cols = tuple(columns)
+    unknown = set(cols) - set(ENRICH_COLUMNS)
+    if unknown:
+        raise ValueError(f"unknown enrich columns: {sorted(unknown)}")
+    out = dict(out or {})
+    for name in cols:
+        if name not in out:
+            out[name] = torch.empty((S, T), dtype=torch.float64, device=close.device)
+        else:
+            _check_panel(out[name], f"out[{name}]", (S, T))
+    ld_out = T
+    if out:
+        strides = {_row_stride(out[n]) for n in cols}
+        if len(strides) != 1:
+            raise ValueError("all output columns must share one row stride")
+        ld_out = strides.pop()
+    in_arr = _lib.ptr_array([t.data_ptr() for t in ins])
+    out_arr = _lib.ptr_array([out[n].data_ptr() if n in cols else 0 for n in ENRICH_COLUMNS])
+    p = (params or IndicatorParams()).to_c()
+    st = _lib.load().bq_enrich(
+        in_arr, S, T, ld_in, ctypes.byref(p), out_arr, ld_out, _stream_handle(stream)
+    )
+    _lib.check(st, "bq_enrich")
+    return {n: out[n] for n in cols}
+
+
+def market_features(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    max_bars: int = 400,
+    out: dict[str, torch.Tensor] | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """_compute_symbol_features at every timestamp of a [S, T] panel
+    (market_regime/live_market_context_accumulator.py:244-297) under the
+    MarketStateStore history cap ``max_bars`` (klines_provider.py:40,65 uses 400)."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    hlc = [_check_panel(t, n, (S, T)) for t, n in zip((high, low, close), ("high", "low", "close"))]
+    ld_in = _row_stride(hlc[0])
+    if any(_row_stride(t) != ld_in for t in hlc):
+        hlc = [t.contiguous() for t in hlc]
+        ld_in = T
+    out = dict(out or {})
+    for name in FEATURE_COLUMNS:
+        if name not in out:
+            out[name] = torch.empty((S, T), dtype=torch.float64, device=close.device)
+    ld_out = _row_stride(out[FEATURE_COLUMNS[0]])
+    st = _lib.load().bq_market_features(
+        _lib.ptr_array([t.data_ptr() for t in hlc]),
+        S,
+        T,
+        ld_in,
+        int(max_bars),
+        _lib.ptr_array([out[n].data_ptr() for n in FEATURE_COLUMNS]),
+        ld_out,
+        _stream_handle(stream),
+    )
+    _lib.check(st, "bq_market_features")
+    return out
+
+
+def breadth_partial(
+    close: torch.Tensor,
+    feats: dict[str, torch.Tensor],
+    out: torch.Tensor | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> torch.Tensor:
+    """[T, 10] per-timestamp partial counts/sums over this shard's symbols
+    (the reductions of _build_context, live_market_context_accumulator.py:135-163)."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    fs = [_check_panel(feats[n], n, (S, T)) for n in FEATURE_COLUMNS]
+    ld_f = _row_stride(fs[0])
+    if any(_row_stride(t) != ld_f for t in fs):
+        raise ValueError("feature columns must share one row stride")
+    if out is None:
+        out = torch.empty((T, len(PARTIAL_COLUMNS)), dtype=torch.float64, device=close.device)
+    st = _lib.load().bq_breadth_partial(
+        ctypes.c_void_p(close.data_ptr()),
+        _lib.ptr_array([t.data_ptr() for t in fs]),
+        S,
+        T,
+        _row_stride(close),
+        ld_f,
+        ctypes.c_void_p(out.data_ptr()),
+        _stream_handle(stream),
+    )
+    _lib.check(st, "bq_breadth_partial")
+    return out
+
+
+class TickState:
+    """Device-resident streaming state for S symbols (bq_state)."""
+
+    def __init__(self, n_symbols: int, params: IndicatorParams | None = None):
+        self._lib = _lib.load()
+        self._h = ctypes.c_void_p()
+        p = (params or IndicatorParams()).to_c()
+        _lib.check(self._lib.bq_state_create(ctypes.byref(self._h), int(n_symbols), ctypes.byref(p)), "bq_state_create")
+        self.n_symbols = int(n_symbols)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.bq_state_destroy(h)
+            self._h = None
+
+    @property
+    def count(self) -> int:
+        return int(self._lib.bq_state_count(self._h))
+
+    def seed(self, open_, high, low, close, volume, stream=None) -> None:
+        close = _check_panel(close, "close")
+        S, T = close.shape
+        if S != self.n_symbols:
+            raise ValueError(f"seed panel has {S} symbols, state has {self.n_symbols}")
+        ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip((open_, high, low, close, volume), INPUT_FIELDS)]
+        st = self._lib.bq_state_seed(
+            self._h, _lib.ptr_array([t.data_ptr() for t in ins]), T, T, _stream_handle(stream)
+        )
+        _lib.check(st, "bq_state_seed")
+
+    def tick(self, new_ohlcv, out: dict[str, torch.Tensor] | None = None, columns=ENRICH_COLUMNS, stream=None):
+        """new_ohlcv: sequence of 5 float64 CUDA vectors [S] (open, high, low, close, volume)."""
+        vecs = []
+        for t, n in zip(new_ohlcv, INPUT_FIELDS):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.numel() == self.n_symbols):
+                raise ValueError(f"{n}: expected float64 CUDA vector of length {self.n_symbols}")
+            vecs.append(t.contiguous())
+        out = dict(out or {})
+        cols = tuple(columns)
+        dev = vecs[0].device
+        for n in cols:
+            if n not in out:
+                out[n] = torch.empty(self.n_symbols, dtype=torch.float64, device=dev)
+        st = self._lib.bq_tick(
+            self._h,
+            _lib.ptr_array([t.data_ptr() for t in vecs]),
+            _lib.ptr_array([out[n].data_ptr() if n in cols else 0 for n in ENRICH_COLUMNS]),
+            _stream_handle(stream),
+        )
+        _lib.check(st, "bq_tick")
+        return {n: out[n] for n in cols}

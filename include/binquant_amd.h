@@ -1,0 +1,182 @@
+/*
+ * binquant_amd — C ABI of the MI355X (gfx950) technical-indicator engine.
+ *
+ * This is the drop-in boundary for binquant's indicator hot path. Every entry
+ * point takes caller-owned DEVICE buffers (plain pointers + sizes), a
+ * hipStream_t (passed as void* so this header needs no HIP include), and
+ * returns an int status: 0 = ok, < 0 = error (see BQ_E*). No C++ exception
+ * crosses this ABI and the library allocates nothing per call.
+ *
+ * Data layout (all fp64): structure-of-arrays, one array per OHLCV field,
+ * each [S][ld] row-major by symbol (candles of one symbol contiguous), i.e.
+ * exactly the memory of S pandas float64 columns laid side by side.
+ *
+ * Reference interfaces replaced (paths relative to carkod/binquant):
+ *   bq_enrich          <- ContextEvaluator.indicators_enrichment
+ *                         producers/context_evaluator.py:240-263, i.e. the
+ *                         pybinbot.Indicators calls at :249-261
+ *                         (moving_averages x3, macd, rsi, bollinguer_spreads,
+ *                          set_twap, atr) plus Indicators.mfi
+ *                         (strategies/coinrule/price_tracker.py:185) and the
+ *                         ema20/ema50 columns of
+ *                         market_regime/live_market_context_accumulator.py:266-267
+ *   bq_tick            <- per-message recompute of the same columns on the
+ *                         latest candle (consumers/klines_provider.py:300-380
+ *                         -> context_evaluator.py:347-512), as an O(1) state
+ *                         update per symbol
+ *   bq_market_features <- LiveMarketContextAccumulator._compute_symbol_features
+ *                         market_regime/live_market_context_accumulator.py:244-297
+ *                         evaluated at every timestamp of a [S][T] panel
+ *   bq_breadth_partial <- the per-symbol sums/counts of
+ *                         LiveMarketContextAccumulator._build_context
+ *                         market_regime/live_market_context_accumulator.py:135-163
+ */
+#ifndef BINQUANT_AMD_H
+#define BINQUANT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes -------------------------------------------------------- */
+#define BQ_OK              0
+#define BQ_EINVAL         -1   /* bad argument (null pointer, size, window)   */
+#define BQ_EHIP           -2   /* HIP runtime error (launch / memcpy)         */
+#define BQ_EALIGN         -3   /* reserved: misaligned buffer                 */
+#define BQ_ESTATE         -4   /* state handle misuse                         */
+
+/* ---- canonical enrich column set ---------------------------------------- */
+/* Order of the `out` pointer array of bq_enrich / bq_tick. A NULL entry
+ * skips that column (its bytes are neither computed nor written). */
+enum bq_enrich_col {
+  BQ_MA_FAST = 0,     /* "ma_7"        close.rolling(7).mean()              */
+  BQ_MA_MID,          /* "ma_25"       close.rolling(25).mean()             */
+  BQ_MA_SLOW,         /* "ma_100"      close.rolling(100).mean()            */
+  BQ_MACD,            /* "macd"        ema12 - ema26 (adjust=False)         */
+  BQ_MACD_SIGNAL,     /* "macd_signal" macd.ewm(span=9, adjust=False)       */
+  BQ_RSI,             /* "rsi"         SMA-smoothed RSI(14)                 */
+  BQ_BB_UPPER,        /* "bb_upper"    mid + k*std                          */
+  BQ_BB_MID,          /* "bb_mid"      close.rolling(20).mean()             */
+  BQ_BB_LOWER,        /* "bb_lower"    mid - k*std                          */
+  BQ_ATR,             /* "ATR"         true_range.rolling(14).mean()        */
+  BQ_TWAP,            /* "twap"        ohlc4.rolling(12).mean()             */
+  BQ_EMA_FAST,        /* "ema20"       close.ewm(span=20, adjust=False)     */
+  BQ_EMA_SLOW,        /* "ema50"       close.ewm(span=50, adjust=False)     */
+  BQ_MFI,             /* "mfi"         money-flow index(14)                 */
+  BQ_NUM_ENRICH_COLS
+};
+
+/* Input field order of the `in` pointer array. */
+enum bq_ohlcv_field { BQ_OPEN = 0, BQ_HIGH, BQ_LOW, BQ_CLOSE, BQ_VOLUME, BQ_NUM_INPUTS };
+
+/* Indicator parameters; defaults (bq_default_params) are the reference's. */
+typedef struct bq_params {
+  int32_t ma_periods[3];   /* 7, 25, 100   (context_evaluator.py:249-251)   */
+  int32_t macd_fast;       /* 12                                            */
+  int32_t macd_slow;       /* 26                                            */
+  int32_t macd_signal;     /* 9                                             */
+  int32_t rsi_window;      /* 14                                            */
+  int32_t bb_window;       /* 20                                            */
+  int32_t bb_ddof;         /* 1 = pandas default std(); 0 = population      */
+  int32_t atr_window;      /* 14           (context_evaluator.py:261)       */
+  int32_t twap_window;     /* 12                                            */
+  int32_t ema_spans[2];    /* 20, 50       (live_market_context_acc.:266)   */
+  int32_t mfi_window;      /* 14           (price_tracker.py:185)           */
+  int32_t reserved;
+  double  bb_k;            /* 2.0                                           */
+} bq_params;
+
+/* Largest rolling window any kernel supports (LDS halo - 2). */
+#define BQ_MAX_WINDOW 126
+
+void bq_default_params(bq_params* p);
+
+/* Library / device info. */
+const char* bq_version(void);
+int bq_device_arch(char* buf, int buflen);   /* e.g. "gfx950" */
+
+/*
+ * Full indicator set over a [S][T] panel.
+ *   in[BQ_NUM_INPUTS]        device pointers, each [S][ld_in] fp64
+ *   out[BQ_NUM_ENRICH_COLS]  device pointers, each [S][ld_out] fp64 (NULL = skip)
+ * Warm-up rows are NaN exactly where pandas yields NaN (t < window-1).
+ */
+int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in,
+              const bq_params* params, double* const* out, int64_t ld_out,
+              void* stream);
+
+/* ---- streaming tick path ------------------------------------------------- */
+typedef struct bq_state bq_state;   /* opaque, device-resident */
+
+/* Create state for S symbols. Allocates device memory once (not per tick). */
+int bq_state_create(bq_state** st, int64_t S, const bq_params* params);
+int bq_state_destroy(bq_state* st);
+/* Seed the state from a [S][T] history panel (T >= 1): ring of the last
+ * BQ_MAX_WINDOW+2 candles and exact EMA carries at the last candle. */
+int bq_state_seed(bq_state* st, const double* const* in, int64_t T, int64_t ld_in,
+                  void* stream);
+/* Append one candle per symbol. new_ohlcv[BQ_NUM_INPUTS] device pointers of
+ * length S; out[BQ_NUM_ENRICH_COLS] device pointers of length S (NULL skip). */
+int bq_tick(bq_state* st, const double* const* new_ohlcv, double* const* out,
+            void* stream);
+int64_t bq_state_symbols(const bq_state* st);
+int64_t bq_state_count(const bq_state* st);   /* candles seen per symbol */
+
+/* ---- market context (breadth / regime) ----------------------------------- */
+/* Per-symbol feature columns of _compute_symbol_features, order of `feat`. */
+enum bq_feature_col {
+  BQ_F_RETURN = 0,    /* return_pct = safe_pct(c_t, c_{t-1})               */
+  BQ_F_EMA20,         /* ema over the last `max_bars` closes, span 20       */
+  BQ_F_EMA50,         /* span 50                                            */
+  BQ_F_TREND,         /* (ema20-ema50)/|ema50|                              */
+  BQ_F_ATR_PCT,       /* TR.rolling(14,min_periods=1).mean() / close        */
+  BQ_F_BB_WIDTH,      /* 4*std(20,ddof=0)/|mid|                             */
+  BQ_NUM_FEATURES
+};
+
+/* Breadth partial layout per timestamp: [T][BQ_NUM_PARTIALS] fp64. */
+enum bq_partial_col {
+  BQ_P_COUNT = 0,     /* symbols with features at t (history >= 2 bars)    */
+  BQ_P_ADV,           /* return_pct > 0                                    */
+  BQ_P_DEC,           /* return_pct < 0                                    */
+  BQ_P_ABOVE20,       /* close > ema20                                     */
+  BQ_P_ABOVE50,       /* close > ema50                                     */
+  BQ_P_SUM_RET,
+  BQ_P_SUM_TREND,
+  BQ_P_SUM_ATR_PCT,
+  BQ_P_SUM_BB_WIDTH,
+  BQ_P_RESERVED,
+  BQ_NUM_PARTIALS
+};
+
+/*
+ * Per-symbol market features at every timestamp, with the accumulator's
+ * history cap (MarketStateStore max_bars_per_symbol) applied: the features
+ * at t see only candles (t-max_bars, t] (15 <= max_bars <= BQ_MAX_HISTORY).
+ * hlc = {high, low, close} device pointers, each [S][ld_in].
+ * feat[BQ_NUM_FEATURES] device pointers [S][ld_out] (NULL = skip). Row t = 0
+ * (fewer than 2 bars of history -> reference returns None) is NaN.
+ */
+#define BQ_MAX_HISTORY 512
+int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in,
+                       int32_t max_bars, double* const* feat, int64_t ld_out,
+                       void* stream);
+
+/*
+ * Cross-symbol partial sums per timestamp over the S symbols of this shard,
+ * from the feature columns of bq_market_features (all of BQ_F_RETURN,
+ * BQ_F_EMA20, BQ_F_EMA50, BQ_F_TREND, BQ_F_ATR_PCT, BQ_F_BB_WIDTH) and close:
+ * partial[T][BQ_NUM_PARTIALS] fp64, overwritten. Deterministic (fixed
+ * reduction order, no atomics). Feeds an RCCL all-reduce(sum) across shards,
+ * then the scalar scoring of _build_context on the host.
+ */
+int bq_breadth_partial(const double* close, const double* const* feat, int64_t S, int64_t T,
+                       int64_t ld_close, int64_t ld_feat, double* partial, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BINQUANT_AMD_H */

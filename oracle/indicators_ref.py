@@ -1,0 +1,208 @@
+"""pandas restatement of the pybinbot.Indicators contract used by binquant.
+
+TEST INFRASTRUCTURE ONLY (see oracle/__init__.py). pybinbot==1.11.8 is not
+available offline; each formula below is the assumption the GPU kernels are
+held to, with the reference call site / in-repo twin it follows.
+
+Call sites: producers/context_evaluator.py:249-261 (indicators_enrichment),
+strategies/coinrule/price_tracker.py:185 (mfi).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+DEFAULTS = dict(
+    ma_periods=(7, 25, 100),
+    macd_fast=12,
+    macd_slow=26,
+    macd_signal=9,
+    rsi_window=14,
+    bb_window=20,
+    bb_ddof=1,
+    bb_k=2.0,
+    atr_window=14,
+    twap_window=12,
+    ema_spans=(20, 50),
+    mfi_window=14,
+)
+
+
+def moving_averages(df: pd.DataFrame, period: int) -> pd.DataFrame:
+    """ma_{period} = close.rolling(period).mean()  (context_evaluator.py:249-251;
+    post_process then drops the warm-up NaNs, :435-441)."""
+    df[f"ma_{period}"] = df["close"].rolling(period).mean()
+    return df
+
+
+def macd(df: pd.DataFrame, fast: int = 12, slow: int = 26, signal: int = 9) -> pd.DataFrame:
+    """macd = EMA12 - EMA26 (adjust=False); macd_signal = EMA9(macd).
+    Called at context_evaluator.py:254; read at price_tracker.py:184 and
+    gradual_gainer_retest.py:328. macd_signal: parity unpinned."""
+    close = df["close"]
+    e_fast = close.ewm(span=fast, adjust=False).mean()
+    e_slow = close.ewm(span=slow, adjust=False).mean()
+    df["macd"] = e_fast - e_slow
+    df["macd_signal"] = df["macd"].ewm(span=signal, adjust=False).mean()
+    return df
+
+
+def rsi(df: pd.DataFrame, window: int = 14) -> pd.DataFrame:
+    """SMA-smoothed RSI: the pybinbot column 'uses a simple rolling mean'
+    (strategies/mean_reversion_fade.py:42-44); formula of the in-repo twin
+    strategies/coinrule/bb_extreme_reversion.py:134-150."""
+    delta = df["close"].astype(float).diff()
+    gain = delta.where(delta > 0, 0.0).rolling(window).mean()
+    loss = (-delta.where(delta < 0, 0.0)).rolling(window).mean()
+    rs = gain / loss
+    df["rsi"] = 100 - (100 / (1 + rs))
+    return df
+
+
+def ma_spreads(df: pd.DataFrame) -> pd.DataFrame:
+    """No in-repo reader. Restated as the spreads of the MAs
+    (percent): parity unpinned."""
+    df["big_ma_spread"] = (abs(df["ma_100"] - df["ma_25"]) / df["ma_100"]) * 100
+    df["small_ma_spread"] = (abs(df["ma_25"] - df["ma_7"]) / df["ma_25"]) * 100
+    return df
+
+
+def bollinguer_spreads(
+    df: pd.DataFrame, window: int = 20, num_std: float = 2.0, ddof: int = 1
+) -> pd.DataFrame:
+    """bb_mid/bb_upper/bb_lower (context_evaluator.py:202-204 readers).
+    Window 20, k=2; ddof=1 is pandas' default std (the in-repo twin at
+    live_market_context_accumulator.py:270 uses ddof=0)."""
+    mid = df["close"].rolling(window).mean()
+    std = df["close"].rolling(window).std(ddof=ddof)
+    df["bb_mid"] = mid
+    df["bb_upper"] = mid + (num_std * std)
+    df["bb_lower"] = mid - (num_std * std)
+    return df
+
+
+def set_twap(df: pd.DataFrame, periods: int = 12) -> pd.DataFrame:
+    """twap = rolling mean of the bar price (open+high+low+close)/4 over
+    `periods` bars (reader: strategies/coinrule/coinrule.py:67). Parity
+    unpinned."""
+    bar = (df["open"] + df["high"] + df["low"] + df["close"]) / 4
+    df["twap"] = bar.rolling(periods).mean()
+    return df
+
+
+def true_range(df: pd.DataFrame) -> pd.Series:
+    """TR with skip-NaN max: first row is high-low
+    (live_market_context_accumulator.py:256-264)."""
+    prev = df["close"].shift(1)
+    return pd.concat(
+        [df["high"] - df["low"], (df["high"] - prev).abs(), (df["low"] - prev).abs()],
+        axis=1,
+    ).max(axis=1)
+
+
+def atr(df: pd.DataFrame, window: int = 14) -> pd.DataFrame:
+    """ATR = TR.rolling(window).mean() — the rolling-mean smoothing of the
+    in-repo twin live_market_context_accumulator.py:268 (mean_reversion_fade.py:45
+    says the shared ATR 'matches the backtest'). Smoothing choice: parity unpinned."""
+    df["ATR"] = true_range(df).rolling(window).mean()
+    return df
+
+
+def mfi_series(df: pd.DataFrame, window: int = 14) -> pd.Series:
+    """Money-flow index column (typical price, positive/negative flow sums)."""
+    tp = (df["high"] + df["low"] + df["close"]) / 3
+    mf = tp * df["volume"]
+    prev = tp.shift(1)
+    pos = mf.where(tp > prev, 0.0).rolling(window).sum()
+    neg = mf.where(tp < prev, 0.0).rolling(window).sum()
+    return 100 - (100 / (1 + pos / neg))
+
+
+def mfi(df: pd.DataFrame, window: int = 14) -> float:
+    """Indicators.mfi(df) -> float of the last bar (price_tracker.py:185)."""
+    return float(mfi_series(df, window).iloc[-1])
+
+
+def ema(df: pd.DataFrame, span: int) -> pd.Series:
+    """close.ewm(span, adjust=False).mean() (live_market_context_accumulator.py:266-267)."""
+    return df["close"].ewm(span=span, adjust=False).mean()
+
+
+def indicators_enrichment(df: pd.DataFrame, p: dict | None = None) -> pd.DataFrame:
+    """ContextEvaluator.indicators_enrichment (producers/context_evaluator.py:240-263)
+    plus the mfi / ema20 / ema50 columns of the canonical 14-column set."""
+    p = {**DEFAULTS, **(p or {})}
+    for period in p["ma_periods"]:
+        df = moving_averages(df, period)
+    df = macd(df, p["macd_fast"], p["macd_slow"], p["macd_signal"])
+    df = rsi(df, p["rsi_window"])
+    df = bollinguer_spreads(df, p["bb_window"], p["bb_k"], p["bb_ddof"])
+    df = set_twap(df, p["twap_window"])
+    df = atr(df, p["atr_window"])
+    df[f"ema{p['ema_spans'][0]}"] = ema(df, p["ema_spans"][0])
+    df[f"ema{p['ema_spans'][1]}"] = ema(df, p["ema_spans"][1])
+    df["mfi"] = mfi_series(df, p["mfi_window"])
+    return df
+
+
+CANONICAL = (
+    "ma_7",
+    "ma_25",
+    "ma_100",
+    "macd",
+    "macd_signal",
+    "rsi",
+    "bb_upper",
+    "bb_mid",
+    "bb_lower",
+    "ATR",
+    "twap",
+    "ema20",
+    "ema50",
+    "mfi",
+)
+
+
+def enrich_panel(o, h, l, c, v, p: dict | None = None) -> dict[str, np.ndarray]:
+    """Per-symbol reference call pattern over a [S][T] panel: one pandas frame
+    per symbol, exactly as the reference processes one symbol per message."""
+    o, h, l, c, v = (np.asarray(x, dtype=np.float64) for x in (o, h, l, c, v))
+    S, T = c.shape
+    out = {k: np.empty((S, T)) for k in CANONICAL}
+    for s in range(S):
+        df = pd.DataFrame({"open": o[s], "high": h[s], "low": l[s], "close": c[s], "volume": v[s]})
+        df = indicators_enrichment(df, p)
+        for k in CANONICAL:
+            out[k][s] = df[k].to_numpy()
+    return out
+
+
+def ewm_scalar(x, alpha: float) -> np.ndarray:
+    """Pure-Python restatement of pandas' ewm(adjust=False, ignore_na=False)
+    mean recursion (pandas/_libs/window/aggregations.pyx `ewm`), used to pin the
+    update formula the GPU replay uses; small inputs only."""
+    x = np.asarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    if x.size == 0:
+        return out
+    om = 1.0 - alpha
+    weighted = x[0]
+    out[0] = weighted
+    old_wt = 1.0
+    for i in range(1, x.size):
+        cur = x[i]
+        is_obs = cur == cur
+        if weighted == weighted:
+            if is_obs:
+                old_wt *= om
+                if weighted != cur:
+                    weighted = old_wt * weighted + alpha * cur
+                    weighted /= old_wt + alpha
+                old_wt = 1.0
+            else:
+                old_wt *= om
+        elif is_obs:
+            weighted = cur
+        out[i] = weighted
+    return out

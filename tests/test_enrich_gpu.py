@@ -1,0 +1,136 @@
+"""GPU parity: the fused bq_enrich kernel vs the pandas oracle (per-symbol
+reference call pattern of producers/context_evaluator.py:240-263).
+
+Tolerances (tests/util.py): fp64 rtol 1e-9 + atol 1e-11 x series magnitude.
+Derived threshold signals are compared exactly away from the tolerance band.
+"""
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from binquant_amd import engine
+from binquant_amd.synth import numpy_panel
+from oracle import indicators_ref as ref
+from tests.util import assert_close
+
+pytestmark = pytest.mark.gpu
+
+COLS = ref.CANONICAL
+
+
+def run_gpu(panel, params=None, columns=COLS, dev="cuda"):
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in panel.items()}
+    out = engine.enrich(t["open"], t["high"], t["low"], t["close"], t["volume"], params=params, columns=columns)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def compare(got, want, panel, cols=COLS):
+    price = np.abs(panel["close"]).mean(axis=1, keepdims=True)
+    for k in cols:
+        if k in ("rsi", "mfi"):
+            scale = 100.0
+        elif k in ("macd", "macd_signal"):
+            scale = price
+        else:
+            scale = price
+        assert_close(got[k], want[k], k, scale=scale)
+
+
+@pytest.mark.parametrize("S,T", [(64, 1000), (16, 3100), (8, 1024), (8, 1025), (4, 2048)])
+def test_enrich_matches_oracle(cuda, S, T):
+    panel = numpy_panel(S, T, seed0=S * 7 + T)
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    compare(got, want, panel)
+
+
+@pytest.mark.parametrize("T", [1, 2, 3, 7, 13, 14, 20, 99, 100, 101, 127, 128, 129, 1023])
+def test_enrich_short_and_boundary_lengths(cuda, T):
+    panel = numpy_panel(3, T, seed0=T, edges=False)
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    compare(got, want, panel)
+
+
+def test_constant_windows_are_exact(cuda):
+    """pandas returns the value itself / std 0 on constant windows
+    (SURVEY §7 hard parts): [0.3]*n must give ma == 0.3 exactly, std == 0."""
+    T = 2500
+    c = np.full(T, 0.3)
+    c[:50] = np.linspace(0.2, 0.4, 50)
+    c[1500:1600] = 7.1
+    c[1600:] = 7.1 + np.cumsum(np.full(T - 1600, 1e-3))
+    panel = {"open": c.copy(), "high": c * 1.0, "low": c * 1.0, "close": c, "volume": np.full(T, 5.0)}
+    panel = {k: v[None, :].copy() for k, v in panel.items()}
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    for k in ("ma_7", "ma_25", "ma_100", "bb_mid", "bb_upper", "bb_lower", "twap", "ATR"):
+        m = ~np.isnan(want[k])
+        np.testing.assert_array_equal(got[k][m][200:1400], want[k][m][200:1400], err_msg=k)
+    assert (got["bb_upper"][0, 1550:1600] == 7.1).all()
+    compare(got, want, panel)
+
+
+def test_zero_volume_and_flat_bars(cuda):
+    panel = numpy_panel(4, 1500, seed0=99, edges=True)
+    panel["volume"][:, 100:130] = 0.0
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    compare(got, want, panel)
+
+
+def test_subset_of_columns_and_params(cuda):
+    panel = numpy_panel(8, 700, seed0=5)
+    p = engine.IndicatorParams(ma_periods=(5, 30, 126), rsi_window=9, bb_window=10, bb_ddof=0, bb_k=2.5,
+                               atr_window=21, twap_window=8, ema_spans=(9, 34), mfi_window=10,
+                               macd_fast=8, macd_slow=21, macd_signal=5)
+    cols = ("ma_7", "ma_100", "rsi", "bb_upper", "bb_lower", "ATR", "mfi", "macd_signal", "ema50")
+    got = run_gpu(panel, params=p, columns=cols)
+    rename = {"ma_7": "ma_5", "ma_100": "ma_126", "ema50": "ema34"}
+    # oracle names columns by period; map the canonical slot names
+    want_cols = {}
+    for s in range(8):
+        df = pd.DataFrame({k: panel[k][s] for k in panel})
+        df = ref.indicators_enrichment(df, p.as_oracle_dict())
+        for k in cols:
+            want_cols.setdefault(k, []).append(df[rename.get(k, k)].to_numpy())
+    want = {k: np.stack(v) for k, v in want_cols.items()}
+    compare(got, want, panel, cols)
+
+
+def test_derived_signals_exact_away_from_boundary(cuda):
+    """Crossovers / thresholds agree exactly except within tolerance of the cut."""
+    panel = numpy_panel(32, 1200, seed0=3)
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    c = panel["close"]
+    tol = 1e-9 * np.abs(c)
+    for a, b in (("ema20", None), ("ema50", None), ("bb_upper", None), ("bb_lower", None), ("ma_25", None)):
+        w, g = want[a], got[a]
+        m = ~np.isnan(w) & (np.abs(c - w) > 10 * tol)
+        np.testing.assert_array_equal((c > g)[m], (c > w)[m], err_msg=a)
+    for k, cut in (("rsi", 30.0), ("rsi", 70.0), ("mfi", 50.0)):
+        w, g = want[k], got[k]
+        m = ~np.isnan(w) & (np.abs(w - cut) > 1e-6)
+        np.testing.assert_array_equal((g < cut)[m], (w < cut)[m], err_msg=f"{k}<{cut}")
+    m = ~np.isnan(want["macd_signal"]) & (np.abs(want["macd"] - want["macd_signal"]) > 1e-9 * np.abs(c))
+    np.testing.assert_array_equal((got["macd"] > got["macd_signal"])[m], (want["macd"] > want["macd_signal"])[m])
+
+
+def test_row_stride_and_rejects_bad_input(cuda):
+    panel = numpy_panel(4, 300, seed0=11)
+    big = {k: np.concatenate([v, np.zeros((4, 20))], axis=1) for k, v in panel.items()}
+    t = {k: torch.from_numpy(v).cuda()[:, :300] for k, v in big.items()}
+    out = engine.enrich(t["open"], t["high"], t["low"], t["close"], t["volume"])
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    compare({k: v.cpu().numpy() for k, v in out.items()}, want, panel)
+    with pytest.raises(ValueError):
+        engine.enrich(t["open"].float(), t["high"], t["low"], t["close"], t["volume"])
+    with pytest.raises(ValueError):
+        engine.enrich(t["open"].cpu(), t["high"], t["low"], t["close"], t["volume"])
+    with pytest.raises(ValueError):
+        engine.enrich(t["open"], t["high"], t["low"], t["close"], t["volume"],
+                      params=engine.IndicatorParams(ma_periods=(7, 25, 500)))
