@@ -8,22 +8,28 @@
 // market_regime/live_market_context_accumulator.py:266-267 — on a [S][T] panel.
 //
 // Mapping: one 256-thread workgroup (4 waves) owns one symbol and walks its
-// candles in tiles of TT = 1024 (K = 4 consecutive candles per thread, so each
-// lane's 32-byte slice is contiguous and a wave covers 2 KiB per field).
+// candles in tiles of TT = 1024 (K = 4 consecutive candles per lane: a lane's
+// 32 bytes per field are contiguous, a wave covers 2 KiB per field). Inputs of
+// tile n+1 are prefetched into registers while tile n computes; outputs are
+// streamed with non-temporal stores. Two workgroup barriers per tile.
+//
 // Per tile:
-//   * rolling windows = differences of a compensated (double-double) prefix
-//     sum. The prefix is scanned across the wave with __shfl_up, across the 4
-//     waves through LDS, rounded once to fp64 and kept in LDS for the tile plus
-//     a 128-candle halo (re-based each tile so magnitudes stay tile-local);
+//   * close-based rolling means (ma_7/25/100, bb_mid) are differences of a
+//     compensated (double-double) prefix sum: wave scan with __shfl_up, the
+//     wave-local prefix rounded once into LDS, wave bases added on lookup;
+//   * short windows (RSI, ATR, TWAP, MFI, Bollinger std) are summed directly
+//     from per-candle arrays in an LDS ring (tile + 128-candle halo);
 //   * pandas' constant-window exactness (rolling().mean() returns the value
-//     itself and std() returns 0 when every value in the window is identical)
-//     is reproduced by a max-scan of "last index where the value changed";
-//   * EMA / MACD recurrences are associative scans of the affine maps
-//     y -> a*y + b (wave scan + LDS cross-wave + per-tile carry), after which
-//     each lane replays its 4 steps with pandas' exact ewm(adjust=False)
-//     update so per-element rounding matches pandas;
-//   * Bollinger std is an exact two-pass variance over the window in LDS.
-// Every input byte is read from HBM once and every output byte written once.
+//     itself, var() returns 0 when every value in the window is identical)
+//     via a max-scan of the last index where close changed (long windows) or
+//     an all-equal test while summing (short windows);
+//   * the EMA family (macd fast/slow, macd signal, ema20, ema50) is one
+//     associative scan of affine maps on the state (y12, y26, signal, y20,
+//     y50) — macd's signal EMA makes that a 3x3 lower-triangular system —
+//     after which each lane replays its 4 candles with pandas' exact
+//     ewm(adjust=False) update, so per-element rounding follows pandas.
+// HBM traffic: every input byte read once (plus one 24-byte neighbour read per
+// lane and tile), every output byte written once.
 #include "bq_device.h"
 #include "binquant_amd.h"
 
@@ -34,15 +40,12 @@ namespace bq {
 constexpr int EN_NT = 256;
 constexpr int EN_NW = EN_NT / WAVE;
 constexpr int EN_K = 4;
-constexpr int EN_TT = EN_NT * EN_K;
-constexpr int EN_H = 128;
-constexpr int EN_R = EN_H + EN_TT;
+constexpr int EN_TT = EN_NT * EN_K;   // 1024
+constexpr int EN_H = 128;             // halo >= BQ_MAX_WINDOW + 2
+constexpr int EN_R = EN_H + EN_TT;    // 1152
 
-// prefix-summed quantities
-enum { QC = 0, QG, QL, QTR, QO4, QPF, QNF, NQ };
-constexpr int NLC = 5;   // constant-run tracking for QC..QO4
-// EMA slots: 0 macd fast, 1 macd slow, 2 ema span0, 3 ema span1, 4 macd signal
-constexpr int NE = 5;
+// EMA slots in the scan state
+enum { E_FAST = 0, E_SLOW, E_SIG, E_0, E_1, NE };
 
 struct EnrichArgs {
   const double* in[BQ_NUM_INPUTS];
@@ -51,18 +54,62 @@ struct EnrichArgs {
   int T;
   int ma[3];
   int rsi_w, bb_w, bb_ddof, atr_w, twap_w, mfi_w;
+  int span[NE];   // macd fast, macd slow, macd signal, ema0, ema1
   double bb_k;
-  double alpha[NE], om[NE], den[NE];   // pandas ewm: new_wt, old_wt, old_wt+new_wt
-  double lin_a[NE], lin_b[NE];         // linearised step y -> lin_a*y + lin_b*x
-  double apow[NE][8];                  // (lin_a^K)^(2^j)
-  int need_macd, need_sig;
 };
 
-__device__ __forceinline__ void load_k(const double* __restrict__ row, int tb, int T, bool vec,
-                                       double (&x)[EN_K]) {
+// Power of the per-thread state map M^(K n): lower-triangular 3x3 block for
+// (fast, slow, signal) + two scalars.  Applied to v: (a0 v0, a1 v1,
+// p v0 + q v1 + a2 v2, a3 v3, a4 v4).
+struct Pow {
+  double a0, a1, p, q, a2, a3, a4;
+};
+
+__device__ __forceinline__ Pow pow_mul(const Pow& T, const Pow& U) {   // T after U
+  Pow r;
+  r.a0 = T.a0 * U.a0;
+  r.a1 = T.a1 * U.a1;
+  r.p = fma(T.p, U.a0, T.a2 * U.p);
+  r.q = fma(T.q, U.a1, T.a2 * U.q);
+  r.a2 = T.a2 * U.a2;
+  r.a3 = T.a3 * U.a3;
+  r.a4 = T.a4 * U.a4;
+  return r;
+}
+
+struct EmaConsts {
+  double al[NE], om[NE], den[NE], la[NE], lb[NE];
+  int divide[NE];
+  Pow step;            // M (one candle)
+  Pow wstep[6];        // (M^K)^(2^j)
+  Pow lane[WAVE];      // (M^K)^lane
+  Pow wave[EN_NW + 1]; // (M^K)^(64 m)
+};
+
+__device__ __forceinline__ void pow_apply(const Pow& A, const double (&v)[NE], double (&r)[NE]) {
+  r[E_FAST] = A.a0 * v[E_FAST];
+  r[E_SLOW] = A.a1 * v[E_SLOW];
+  r[E_SIG] = fma(A.p, v[E_FAST], fma(A.q, v[E_SLOW], A.a2 * v[E_SIG]));
+  r[E_0] = A.a3 * v[E_0];
+  r[E_1] = A.a4 * v[E_1];
+}
+
+__device__ __forceinline__ double ema_step(double y, double x, const EmaConsts& E, int e) {
+  // pandas ewm(adjust=False): weighted = old_wt*weighted + new_wt*cur;
+  // weighted /= old_wt + new_wt; skipped when weighted == cur.
+  if (y != x) {
+    y = E.om[e] * y + E.al[e] * x;
+    if (E.divide[e]) y = y / E.den[e];
+  }
+  return y;
+}
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void load4(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[EN_K]) {
   if (vec && tb + EN_K <= T) {
-    const double2* p = reinterpret_cast<const double2*>(row + tb);
-    double2 a = p[0], b = p[1];
+    const dbl2* p = reinterpret_cast<const dbl2*>(row + tb);
+    dbl2 a = p[0], b = p[1];
     x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
   } else {
 #pragma unroll
@@ -70,15 +117,11 @@ __device__ __forceinline__ void load_k(const double* __restrict__ row, int tb, i
   }
 }
 
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void store_k(double* __restrict__ row, int tb, int T, bool vec,
-                                        const double (&x)[EN_K]) {
+__device__ __forceinline__ void store4(double* __restrict__ row, int tb, int T, bool vec, const double (&x)[EN_K]) {
   if (vec && tb + EN_K <= T) {
     dbl2* p = reinterpret_cast<dbl2*>(row + tb);
-    dbl2 a = {x[0], x[1]}, b = {x[2], x[3]};
-    __builtin_nontemporal_store(a, p);
-    __builtin_nontemporal_store(b, p + 1);
+    __builtin_nontemporal_store(dbl2{x[0], x[1]}, p);
+    __builtin_nontemporal_store(dbl2{x[2], x[3]}, p + 1);
   } else {
 #pragma unroll
     for (int k = 0; k < EN_K; ++k)
@@ -86,344 +129,470 @@ __device__ __forceinline__ void store_k(double* __restrict__ row, int tb, int T,
   }
 }
 
-__global__ __launch_bounds__(EN_NT) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
-  __shared__ double sP[NQ][EN_R];      // tile-local prefix sums (+ halo)
-  __shared__ double sC[EN_R];          // raw close (+ halo) for the two-pass std
-  __shared__ double sX[5][EN_NW + 1];  // neighbour exchange: c, c[-2], h, l, o of last candle
-  __shared__ double sWh[NQ][EN_NW], sWl[NQ][EN_NW];
-  __shared__ double sWe[NE][EN_NW];
-  __shared__ int sWlc[NLC][EN_NW];
+struct Tile {
+  double o[EN_K], h[EN_K], l[EN_K], c[EN_K], v[EN_K];
+  double ph, pl, pc;   // candle tb-1 (NaN before the series start)
+};
+
+__device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int tb, bool vin, Tile& t) {
+  const int T = A.T;
+  load4(A.in[BQ_OPEN] + row, tb, T, vin, t.o);
+  load4(A.in[BQ_HIGH] + row, tb, T, vin, t.h);
+  load4(A.in[BQ_LOW] + row, tb, T, vin, t.l);
+  load4(A.in[BQ_CLOSE] + row, tb, T, vin, t.c);
+  load4(A.in[BQ_VOLUME] + row, tb, T, vin, t.v);
+  if (tb >= 1 && tb <= T) {
+    t.ph = A.in[BQ_HIGH][row + tb - 1];
+    t.pl = A.in[BQ_LOW][row + tb - 1];
+    t.pc = A.in[BQ_CLOSE][row + tb - 1];
+  } else {
+    t.ph = t.pl = t.pc = qnan();
+  }
+}
+
+__global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
+  // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
+  __shared__ double sP[EN_R];    // close prefix: halo re-based, tile wave-local
+  __shared__ double sC[EN_R];    // close
+  __shared__ double sTR[EN_R];   // true range
+  __shared__ double sO4[EN_R];   // (o+h+l+c)/4
+  __shared__ double sMF[EN_R];   // signed money flow: +tp*v up-tick, -tp*v down-tick, 0 flat
+  __shared__ double sWh[EN_NW], sWl[EN_NW];
+  __shared__ double sWe[EN_NW][NE];
+  __shared__ int sWlc[EN_NW];
   __shared__ double sEcar[NE];
-  __shared__ int sLcar[NLC];
+  __shared__ int sLcar;
+  __shared__ EmaConsts E;
+  __shared__ EnrichArgs sA;   // window sizes / output table, re-read from LDS each
+                              // tile so the compiler cannot hoist them into registers
 
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const int64_t sym = blockIdx.x;
+  const int64_t irow = sym * A.ld_in;
+  const int64_t orow = sym * A.ld_out;
   const int T = A.T;
-  const double* __restrict__ rO = A.in[BQ_OPEN] + sym * A.ld_in;
-  const double* __restrict__ rH = A.in[BQ_HIGH] + sym * A.ld_in;
-  const double* __restrict__ rL = A.in[BQ_LOW] + sym * A.ld_in;
-  const double* __restrict__ rC = A.in[BQ_CLOSE] + sym * A.ld_in;
-  const double* __restrict__ rV = A.in[BQ_VOLUME] + sym * A.ld_in;
+  const bool vin = vec_in != 0, vout = vec_out != 0;
 
+  // ---- per-workgroup constants (pandas: comass = (span-1)/2, alpha = 1/(1+comass))
+  if (tid == 0) {
+    for (int e = 0; e < NE; ++e) {
+      const double com = ((double)A.span[e] - 1.0) / 2.0;
+      const double al = 1.0 / (1.0 + com);
+      E.al[e] = al;
+      E.om[e] = 1.0 - al;
+      E.den[e] = E.om[e] + al;
+      E.divide[e] = E.den[e] != 1.0;
+      E.la[e] = E.om[e] / E.den[e];
+      E.lb[e] = al / E.den[e];
+    }
+    Pow m;
+    m.a0 = E.la[E_FAST];
+    m.a1 = E.la[E_SLOW];
+    m.a2 = E.la[E_SIG];
+    m.p = E.lb[E_SIG] * E.la[E_FAST];
+    m.q = -(E.lb[E_SIG] * E.la[E_SLOW]);
+    m.a3 = E.la[E_0];
+    m.a4 = E.la[E_1];
+    E.step = m;
+    Pow mk = m;
+    for (int k = 1; k < EN_K; ++k) mk = pow_mul(m, mk);
+    for (int j = 0; j < 6; ++j) {
+      E.wstep[j] = mk;
+      mk = pow_mul(mk, mk);
+    }
+  }
+  __syncthreads();
+  if (tid < WAVE) {
+    Pow r = {1.0, 1.0, 0.0, 0.0, 1.0, 1.0, 1.0};
+    for (int j = 0; j < 6; ++j)
+      if (tid & (1 << j)) r = pow_mul(E.wstep[j], r);
+    E.lane[tid] = r;
+  }
+  if (tid == WAVE) {
+    Pow r = {1.0, 1.0, 0.0, 0.0, 1.0, 1.0, 1.0};
+    const Pow w64 = pow_mul(E.wstep[5], E.wstep[5]);   // (M^K)^64
+    for (int m = 0; m <= EN_NW; ++m) {
+      E.wave[m] = r;
+      r = pow_mul(w64, r);
+    }
+  }
   if (tid < NE) sEcar[tid] = 0.0;
-  if (tid < NLC) sLcar[tid] = -1;
-  if (tid < 5) sX[tid][0] = qnan();
-  if (tid < EN_H) {
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) sP[q][tid] = 0.0;
+  if (tid == 0) {
+    sLcar = -1;
+    sA = A;
+  }
+  if (tid < EN_H) {   // candles before the series start: NaN close, zero sums
+    sP[tid] = 0.0;
     sC[tid] = qnan();
+    sTR[tid] = 0.0;
+    sO4[tid] = 0.0;
+    sMF[tid] = 0.0;
   }
   __syncthreads();
 
-  const bool vin = vec_in != 0, vout = vec_out != 0;
+  Tile nx;
+  load_tile(A, irow, EN_K * tid, vin, nx);
 
   for (int t0 = 0; t0 < T; t0 += EN_TT) {
     const int tb = t0 + EN_K * tid;
-    const int pb = EN_H + EN_K * tid;   // LDS position of element k=0
-    double o[EN_K], h[EN_K], l[EN_K], c[EN_K], v[EN_K];
-    load_k(rO, tb, T, vin, o);
-    load_k(rH, tb, T, vin, h);
-    load_k(rL, tb, T, vin, l);
-    load_k(rC, tb, T, vin, c);
-    load_k(rV, tb, T, vin, v);
+    const int pb = EN_H + EN_K * tid;
+    const EnrichArgs& P = sA;
+    const Tile cu = nx;
+    if (t0 + EN_TT < T) load_tile(A, irow, tb + EN_TT, vin, nx);   // prefetch tile n+1
 
-    // ---- neighbour exchange (previous candle's raw values) -----------------
-    double pc1 = __shfl_up(c[EN_K - 1], 1, WAVE);
-    double pc2 = __shfl_up(c[EN_K - 2], 1, WAVE);
-    double ph = __shfl_up(h[EN_K - 1], 1, WAVE);
-    double pl = __shfl_up(l[EN_K - 1], 1, WAVE);
-    double po = __shfl_up(o[EN_K - 1], 1, WAVE);
-    if (lane == WAVE - 1) {
-      sX[0][w + 1] = c[EN_K - 1];
-      sX[1][w + 1] = c[EN_K - 2];
-      sX[2][w + 1] = h[EN_K - 1];
-      sX[3][w + 1] = l[EN_K - 1];
-      sX[4][w + 1] = o[EN_K - 1];
-    }
-#pragma unroll
-    for (int k = 0; k < EN_K; ++k) sC[pb + k] = c[k];
-    __syncthreads();   // B1
-    if (lane == 0) {
-      pc1 = sX[0][w];
-      pc2 = sX[1][w];
-      ph = sX[2][w];
-      pl = sX[3][w];
-      po = sX[4][w];
-    }
-
-    // ---- derived per-candle quantities --------------------------------------
-    double g[EN_K], ls[EN_K], tr[EN_K], o4[EN_K], pf[EN_K], nf[EN_K];
-    int lcl[NLC][EN_K];
+    // ---- phase 1: per-candle quantities into the LDS ring --------------------
+    int lcl[EN_K];
     {
-      // values of candle t-1 (for change detection at k = 0)
-      const double dm1 = pc1 - pc2;
-      double prv[NLC] = {pc1, gain_of(dm1), loss_of(dm1), true_range(ph, pl, pc2),
-                         ohlc4(po, ph, pl, pc1)};
-      double cp = pc1, tpp = typical_price(ph, pl, pc1);
-      int run[NLC] = {-1, -1, -1, -1, -1};
+      double pc = cu.pc;
+      double tpp = typical_price(cu.ph, cu.pl, cu.pc);
+      int run = -1;
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
         const int t = tb + k;
-        const double d = c[k] - cp;
-        g[k] = gain_of(d);
-        ls[k] = loss_of(d);
-        tr[k] = true_range(h[k], l[k], cp);
-        o4[k] = ohlc4(o[k], h[k], l[k], c[k]);
-        const double tp = typical_price(h[k], l[k], c[k]);
-        const double mf = tp * v[k];
-        pf[k] = tp > tpp ? mf : 0.0;
-        nf[k] = tp < tpp ? mf : 0.0;
-        const double cur[NLC] = {c[k], g[k], ls[k], tr[k], o4[k]};
-#pragma unroll
-        for (int q = 0; q < NLC; ++q) {
-          if (t == 0 || cur[q] != prv[q]) run[q] = t;
-          lcl[q][k] = run[q];
-          prv[q] = cur[q];
-        }
-        cp = c[k];
+        const double c = cu.c[k];
+        const double tp = typical_price(cu.h[k], cu.l[k], c);
+        const double mf = tp * cu.v[k];
+        sC[pb + k] = c;
+        sTR[pb + k] = true_range(cu.h[k], cu.l[k], pc);
+        sO4[pb + k] = ohlc4(cu.o[k], cu.h[k], cu.l[k], c);
+        sMF[pb + k] = tp > tpp ? mf : (tp < tpp ? -mf : 0.0);
+        if (t == 0 || c != pc) run = t;
+        lcl[k] = run;
+        pc = c;
         tpp = tp;
       }
     }
-
-    // ---- phase A: per-thread totals, wave scans -----------------------------
-    dd pre[NQ];   // exclusive wave prefix (dd)
+    // close prefix (compensated), wave-local
+    double Ploc[EN_K];
     {
-      const double* qv[NQ] = {c, g, ls, tr, o4, pf, nf};
+      dd tot = {0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        dd tot = {0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < EN_K; ++k) tot = dd_add1(tot, qv[q][k]);
-        dd inc = wave_incl_scan_dd(tot, lane);
-        if (lane == WAVE - 1) {
-          sWh[q][w] = inc.hi;
-          sWl[q][w] = inc.lo;
-        }
-        double eh = __shfl_up(inc.hi, 1, WAVE), el = __shfl_up(inc.lo, 1, WAVE);
-        pre[q] = lane == 0 ? dd{0.0, 0.0} : dd{eh, el};
+      for (int k = 0; k < EN_K; ++k) tot = dd_add1(tot, cu.c[k]);
+      const dd inc = wave_incl_scan_dd(tot, lane);
+      if (lane == WAVE - 1) {
+        sWh[w] = inc.hi;
+        sWl[w] = inc.lo;
       }
-    }
-    double epre[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (e < 2 && !A.need_macd) { epre[e] = 0.0; continue; }
-      double y = 0.0;
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) y = (tb + k == 0) ? c[k] : fma(A.lin_a[e], y, A.lin_b[e] * c[k]);
-      double inc = wave_incl_scan_affine(y, A.apow[e], lane);
-      if (lane == WAVE - 1) sWe[e][w] = inc;
-      double ex = __shfl_up(inc, 1, WAVE);
-      epre[e] = lane == 0 ? 0.0 : ex;
-    }
-    int lpre[NLC];
-#pragma unroll
-    for (int q = 0; q < NLC; ++q) {
-      int inc = wave_incl_scan_max(lcl[q][EN_K - 1], lane);
-      if (lane == WAVE - 1) sWlc[q][w] = inc;
-      int ex = __shfl_up(inc, 1, WAVE);
-      lpre[q] = lane == 0 ? -1 : ex;
-    }
-    __syncthreads();   // B2
-
-    // ---- phase B: carries, prefix to LDS, EMA replay -------------------------
-    {
-      const double* qv[NQ] = {c, g, ls, tr, o4, pf, nf};
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        dd base = {0.0, 0.0};   // halo prefix ends at 0 by construction (re-base)
-        for (int u = 0; u < w; ++u) base = dd_add(base, dd{sWh[q][u], sWl[q][u]});
-        base = dd_add(base, pre[q]);
-#pragma unroll
-        for (int k = 0; k < EN_K; ++k) {
-          base = dd_add1(base, qv[q][k]);
-          sP[q][pb + k] = dd_round(base);
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NLC; ++q) {
-      int carry = sLcar[q];
-      for (int u = 0; u < w; ++u) carry = max(carry, sWlc[q][u]);
-      carry = max(carry, lpre[q]);
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) lcl[q][k] = max(lcl[q][k], carry);
-    }
-    double ema[4][EN_K];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (e < 2 && !A.need_macd) {
-#pragma unroll
-        for (int k = 0; k < EN_K; ++k) ema[e][k] = 0.0;
-        continue;
-      }
-      double C = sEcar[e];
-      for (int u = 0; u < w; ++u) C = fma(A.apow[e][6], C, sWe[e][u]);
-      double y = lane == 0 ? C : fma(pow_bits<6>(A.apow[e], lane), C, epre[e]);
-      const double al = A.alpha[e], om = A.om[e], dn = A.den[e];
+      const double eh = __shfl_up(inc.hi, 1, WAVE), el = __shfl_up(inc.lo, 1, WAVE);
+      dd acc = lane == 0 ? dd{0.0, 0.0} : dd{eh, el};
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
-        const double x = c[k];
-        if (tb + k == 0) y = x;
-        else if (y != x) y = (om * y + al * x) / dn;
-        ema[e][k] = y;
+        acc = dd_add1(acc, cu.c[k]);
+        Ploc[k] = dd_round(acc);
+        sP[pb + k] = Ploc[k];
       }
     }
-    double macd[EN_K], sig[EN_K] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < EN_K; ++k) macd[k] = ema[0][k] - ema[1][k];
-    double spre = 0.0;
-    if (A.need_sig) {
-      double y = 0.0;
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) y = (tb + k == 0) ? macd[k] : fma(A.lin_a[4], y, A.lin_b[4] * macd[k]);
-      double inc = wave_incl_scan_affine(y, A.apow[4], lane);
-      if (lane == WAVE - 1) sWe[4][w] = inc;
-      double ex = __shfl_up(inc, 1, WAVE);
-      spre = lane == 0 ? 0.0 : ex;
-    }
-    __syncthreads();   // B3: prefix sums + signal wave totals visible
-    if (A.need_sig) {
-      double C = sEcar[4];
-      for (int u = 0; u < w; ++u) C = fma(A.apow[4][6], C, sWe[4][u]);
-      double y = lane == 0 ? C : fma(pow_bits<6>(A.apow[4], lane), C, spre);
-      const double al = A.alpha[4], om = A.om[4], dn = A.den[4];
+    // EMA state scan: thread map from the zero state, then wave inclusive scan
+    double ex[NE];
+    {
+      double b[NE] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
-        const double x = macd[k];
-        if (tb + k == 0) y = x;
-        else if (y != x) y = (om * y + al * x) / dn;
-        sig[k] = y;
+        const double x = cu.c[k];
+        if (tb + k == 0) {
+          b[E_FAST] = b[E_SLOW] = b[E_0] = b[E_1] = x;
+          b[E_SIG] = 0.0;
+        } else {
+          b[E_FAST] = fma(E.la[E_FAST], b[E_FAST], E.lb[E_FAST] * x);
+          b[E_SLOW] = fma(E.la[E_SLOW], b[E_SLOW], E.lb[E_SLOW] * x);
+          b[E_SIG] = fma(E.la[E_SIG], b[E_SIG], E.lb[E_SIG] * (b[E_FAST] - b[E_SLOW]));
+          b[E_0] = fma(E.la[E_0], b[E_0], E.lb[E_0] * x);
+          b[E_1] = fma(E.la[E_1], b[E_1], E.lb[E_1] * x);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int d = 1 << j;
+        double v[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) v[e] = __shfl_up(b[e], d, WAVE);
+        if (lane >= d) {
+          double r[NE];
+          pow_apply(E.wstep[j], v, r);
+#pragma unroll
+          for (int e = 0; e < NE; ++e) b[e] += r[e];
+        }
+      }
+      if (lane == WAVE - 1) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) sWe[w][e] = b[e];
+      }
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const double s = __shfl_up(b[e], 1, WAVE);
+        ex[e] = lane == 0 ? 0.0 : s;
       }
     }
+    int lpre;
+    {
+      const int inc = wave_incl_scan_max(lcl[EN_K - 1], lane);
+      if (lane == WAVE - 1) sWlc[w] = inc;
+      const int s = __shfl_up(inc, 1, WAVE);
+      lpre = lane == 0 ? -1 : s;
+    }
+    __syncthreads();   // B1: ring, wave totals, carries visible
 
-    // ---- phase C: window outputs --------------------------------------------
-    const double cur_q[NLC][EN_K] = {{c[0], c[1], c[2], c[3]},
-                                     {g[0], g[1], g[2], g[3]},
-                                     {ls[0], ls[1], ls[2], ls[3]},
-                                     {tr[0], tr[1], tr[2], tr[3]},
-                                     {o4[0], o4[1], o4[2], o4[3]}};
-    auto wmean = [&](int q, int win, int k) -> double {
+    // ---- phase 2: carries --------------------------------------------------------
+    double wb[EN_NW];   // close-prefix base of each wave's tile slice
+    {
+      dd acc = {0.0, 0.0};
+#pragma unroll
+      for (int u = 0; u < EN_NW; ++u) {
+        wb[u] = dd_round(acc);
+        acc = dd_add(acc, dd{sWh[u], sWl[u]});
+      }
+    }
+    {
+      int carry = max(sLcar, lpre);
+      for (int u = 0; u < w; ++u) carry = max(carry, sWlc[u]);
+#pragma unroll
+      for (int k = 0; k < EN_K; ++k) lcl[k] = max(lcl[k], carry);
+    }
+    double y[NE];
+    {
+      double C[NE];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) C[e] = sEcar[e];
+      for (int u = 0; u < w; ++u) {
+        double r[NE];
+        pow_apply(E.wave[1], C, r);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) C[e] = r[e] + sWe[u][e];
+      }
+      double r[NE];
+      pow_apply(E.lane[lane], C, r);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) y[e] = ex[e] + r[e];
+    }
+
+    // ---- EMA family: exact pandas replay ---------------------------------------
+    {
+      double mfast[EN_K], msig[EN_K], e0[EN_K], e1[EN_K];
+#pragma unroll
+      for (int k = 0; k < EN_K; ++k) {
+        const double x = cu.c[k];
+        if (tb + k == 0) {
+          y[E_FAST] = y[E_SLOW] = y[E_0] = y[E_1] = x;
+          y[E_SIG] = y[E_FAST] - y[E_SLOW];
+        } else {
+          y[E_FAST] = ema_step(y[E_FAST], x, E, E_FAST);
+          y[E_SLOW] = ema_step(y[E_SLOW], x, E, E_SLOW);
+          y[E_SIG] = ema_step(y[E_SIG], y[E_FAST] - y[E_SLOW], E, E_SIG);
+          y[E_0] = ema_step(y[E_0], x, E, E_0);
+          y[E_1] = ema_step(y[E_1], x, E, E_1);
+        }
+        mfast[k] = y[E_FAST] - y[E_SLOW];
+        msig[k] = y[E_SIG];
+        e0[k] = y[E_0];
+        e1[k] = y[E_1];
+      }
+      if (P.out[BQ_MACD]) store4(P.out[BQ_MACD] + orow, tb, T, vout, mfast);
+      if (P.out[BQ_MACD_SIGNAL]) store4(P.out[BQ_MACD_SIGNAL] + orow, tb, T, vout, msig);
+      if (P.out[BQ_EMA_FAST]) store4(P.out[BQ_EMA_FAST] + orow, tb, T, vout, e0);
+      if (P.out[BQ_EMA_SLOW]) store4(P.out[BQ_EMA_SLOW] + orow, tb, T, vout, e1);
+    }
+
+    // ---- rolling windows -------------------------------------------------------
+    const double wbw = w == 0 ? wb[0] : w == 1 ? wb[1] : w == 2 ? wb[2] : wb[3];
+    auto Pat = [&](int pos) -> double {   // close prefix at ring position pos
+      const int i = pos - EN_H;   // wave owning ring position pos (-1: halo)
+      const int ow = i < 0 ? -1 : (i >> 8);
+      const double base = ow == 0 ? wb[0] : ow == 1 ? wb[1] : ow == 2 ? wb[2] : ow == 3 ? wb[3] : 0.0;
+      return sP[pos] + base;
+    };
+    // close.rolling(win).mean(): prefix difference / win, or the value itself
+    // on a constant window (pandas same-value rule).
+    auto cmean = [&](int win, int k) -> double {
       const int t = tb + k, p = pb + k;
       if (t < win - 1) return qnan();
-      if (lcl[q][k] <= t - win + 1) return cur_q[q][k];
-      double S = sP[q][p] - sP[q][p - win];
-      if (q != QC && q != QO4) S = S < 0.0 ? 0.0 : S;   // pandas neg_ct clamp
-      return S / (double)win;
+      if (lcl[k] <= t - win + 1) return cu.c[k];
+      return div_exact((Ploc[k] + wbw) - Pat(p - win), (double)win);
     };
-    auto wsum = [&](int q, int win, int k) -> double {
-      const int t = tb + k, p = pb + k;
-      if (t < win - 1) return qnan();
-      double S = sP[q][p] - sP[q][p - win];
-      return S < 0.0 ? 0.0 : S;
-    };
-    const int64_t orow = sym * A.ld_out;
     double res[EN_K];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (A.out[BQ_MA_FAST + i]) {
+      if (P.out[BQ_MA_FAST + i]) {
+        const int win = P.ma[i];
 #pragma unroll
-        for (int k = 0; k < EN_K; ++k) res[k] = wmean(QC, A.ma[i], k);
-        store_k(A.out[BQ_MA_FAST + i] + orow, tb, T, vout, res);
+        for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, k);
+        store4(P.out[BQ_MA_FAST + i] + orow, tb, T, vout, res);
       }
     }
-    if (A.out[BQ_MACD]) store_k(A.out[BQ_MACD] + orow, tb, T, vout, macd);
-    if (A.out[BQ_MACD_SIGNAL]) store_k(A.out[BQ_MACD_SIGNAL] + orow, tb, T, vout, sig);
-    if (A.out[BQ_RSI]) {
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) {
-        const double gm = wmean(QG, A.rsi_w, k), lm = wmean(QL, A.rsi_w, k);
-        res[k] = oscillator(gm, lm);
+    if (P.out[BQ_BB_UPPER] || P.out[BQ_BB_MID] || P.out[BQ_BB_LOWER]) {
+      // mean from the prefix; variance from sliding sums of (c - r), (c - r)^2
+      // with the lane-local reference r = close at the lane's first candle.
+      double up[EN_K], mid[EN_K], lo[EN_K];
+      const int win = P.bb_w;
+      const double wd = (double)win, dv = (double)(win - P.bb_ddof), bk = P.bb_k;
+      const double r = cu.c[0];
+      const int gstart = EN_H - t0;   // ring position of candle 0 (tile 0 only)
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = max(pb - win + 1, gstart); i <= pb; ++i) {
+        const double d = sC[i] - r;
+        s1 += d;
+        s2 = fma(d, d, s2);
       }
-      store_k(A.out[BQ_RSI] + orow, tb, T, vout, res);
-    }
-    if (A.out[BQ_BB_UPPER] || A.out[BQ_BB_MID] || A.out[BQ_BB_LOWER]) {
-      double mid[EN_K], up[EN_K], lo[EN_K];
-      const int win = A.bb_w;
-      const double dv = (double)(win - A.bb_ddof);
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
         const int t = tb + k, p = pb + k;
-        const double m = wmean(QC, win, k);
+        if (k > 0) {
+          const double dn = cu.c[k] - r, dol = p - win >= gstart ? sC[p - win] - r : 0.0;
+          s1 = (s1 + dn) - dol;
+          s2 = fma(-dol, dol, fma(dn, dn, s2));
+        }
+        const double m = cmean(win, k);
         double sd;
         if (t < win - 1 || dv <= 0.0) sd = qnan();
-        else if (lcl[QC][k] <= t - win + 1) sd = 0.0;
+        else if (lcl[k] <= t - win + 1) sd = 0.0;
         else {
-          double acc = 0.0;
-          for (int i = p - win + 1; i <= p; ++i) {
-            const double dlt = sC[i] - m;
-            acc = fma(dlt, dlt, acc);
-          }
-          sd = sqrt(acc / dv);
+          double var = (s2 - s1 * s1 / wd) / dv;
+          sd = sqrt(var < 0.0 ? 0.0 : var);
         }
         mid[k] = m;
-        up[k] = m + A.bb_k * sd;
-        lo[k] = m - A.bb_k * sd;
+        up[k] = m + bk * sd;
+        lo[k] = m - bk * sd;
       }
-      if (A.out[BQ_BB_UPPER]) store_k(A.out[BQ_BB_UPPER] + orow, tb, T, vout, up);
-      if (A.out[BQ_BB_MID]) store_k(A.out[BQ_BB_MID] + orow, tb, T, vout, mid);
-      if (A.out[BQ_BB_LOWER]) store_k(A.out[BQ_BB_LOWER] + orow, tb, T, vout, lo);
+      if (P.out[BQ_BB_UPPER]) store4(P.out[BQ_BB_UPPER] + orow, tb, T, vout, up);
+      if (P.out[BQ_BB_MID]) store4(P.out[BQ_BB_MID] + orow, tb, T, vout, mid);
+      if (P.out[BQ_BB_LOWER]) store4(P.out[BQ_BB_LOWER] + orow, tb, T, vout, lo);
     }
-    if (A.out[BQ_ATR]) {
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) res[k] = wmean(QTR, A.atr_w, k);
-      store_k(A.out[BQ_ATR] + orow, tb, T, vout, res);
-    }
-    if (A.out[BQ_TWAP]) {
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) res[k] = wmean(QO4, A.twap_w, k);
-      store_k(A.out[BQ_TWAP] + orow, tb, T, vout, res);
-    }
-    if (A.out[BQ_EMA_FAST]) store_k(A.out[BQ_EMA_FAST] + orow, tb, T, vout, ema[2]);
-    if (A.out[BQ_EMA_SLOW]) store_k(A.out[BQ_EMA_SLOW] + orow, tb, T, vout, ema[3]);
-    if (A.out[BQ_MFI]) {
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) res[k] = oscillator(wsum(QPF, A.mfi_w, k), wsum(QNF, A.mfi_w, k));
-      store_k(A.out[BQ_MFI] + orow, tb, T, vout, res);
-    }
-
-    if (t0 + EN_TT >= T) break;   // no next tile: skip carry bookkeeping
-    __syncthreads();   // B4: every read of this tile's LDS is done
-
-    // ---- carries into the next tile -----------------------------------------
-    if (tid < EN_H) {
-      const int src = EN_TT + tid;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const double last = sP[q][EN_R - 1];
-        sP[q][tid] = sP[q][src] - last;   // re-base: halo prefix ends at 0
+    if (P.out[BQ_RSI]) {
+      // gain/loss of candle i use close[i-1]; close[-1] is NaN -> 0 (where()).
+      const int win = P.rsi_w;
+      const double wd = (double)win;
+      double sg = 0.0, sl = 0.0, pg = qnan(), pl = qnan();
+      int rg = 0, rl = 0;
+      double prev = sC[pb - win];
+      for (int i = pb - win + 1; i <= pb; ++i) {
+        const double c = sC[i], d = c - prev;
+        const double g = gain_of(d), l = loss_of(d);
+        sg += g;
+        sl += l;
+        rg = g == pg ? rg + 1 : 1;
+        rl = l == pl ? rl + 1 : 1;
+        pg = g;
+        pl = l;
+        prev = c;
       }
-      sC[tid] = sC[src];
-    }
-    if (tid < 5) sX[tid][0] = sX[tid][EN_NW];
-    if (tid == EN_NT - 1) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sEcar[e] = ema[e][EN_K - 1];
-      sEcar[4] = sig[EN_K - 1];
-#pragma unroll
-      for (int q = 0; q < NLC; ++q) sLcar[q] = lcl[q][EN_K - 1];
+      for (int k = 0; k < EN_K; ++k) {
+        const int t = tb + k, p = pb + k;
+        if (k > 0) {
+          const double d = cu.c[k] - cu.c[k - 1];
+          const double dold = sC[p - win] - sC[p - win - 1];
+          const double g = gain_of(d), l = loss_of(d);
+          sg = (sg + g) - gain_of(dold);
+          sl = (sl + l) - loss_of(dold);
+          rg = g == pg ? rg + 1 : 1;
+          rl = l == pl ? rl + 1 : 1;
+          pg = g;
+          pl = l;
+        }
+        if (t < win - 1) {
+          res[k] = qnan();
+          continue;
+        }
+        const double gm = rg >= win ? pg : div_exact(sg < 0.0 ? 0.0 : sg, wd);
+        const double lm = rl >= win ? pl : div_exact(sl < 0.0 ? 0.0 : sl, wd);
+        res[k] = oscillator(gm, lm);
+      }
+      store4(P.out[BQ_RSI] + orow, tb, T, vout, res);
     }
-    __syncthreads();   // B5
-  }
-}
+    // sliding mean of a per-candle ring array with the same-value rule
+    auto smean = [&](const double* Q, int win, bool nonneg) {
+      const double wd = (double)win;
+      double s = 0.0, pq = qnan();
+      int run = 0;
+      for (int i = pb - win + 1; i <= pb; ++i) {
+        const double q = Q[i];
+        s += q;
+        run = q == pq ? run + 1 : 1;
+        pq = q;
+      }
+#pragma unroll
+      for (int k = 0; k < EN_K; ++k) {
+        const int t = tb + k, p = pb + k;
+        if (k > 0) {
+          const double q = Q[p];
+          s = (s + q) - Q[p - win];
+          run = q == pq ? run + 1 : 1;
+          pq = q;
+        }
+        if (t < win - 1) res[k] = qnan();
+        else if (run >= win) res[k] = pq;
+        else res[k] = div_exact(nonneg && s < 0.0 ? 0.0 : s, wd);
+      }
+    };
+    if (P.out[BQ_ATR]) {
+      smean(sTR, P.atr_w, true);
+      store4(P.out[BQ_ATR] + orow, tb, T, vout, res);
+    }
+    if (P.out[BQ_TWAP]) {
+      smean(sO4, P.twap_w, false);
+      store4(P.out[BQ_TWAP] + orow, tb, T, vout, res);
+    }
+    if (P.out[BQ_MFI]) {
+      const int win = P.mfi_w;
+      double pos = 0.0, neg = 0.0, pp = qnan(), pn = qnan();
+      int rp = 0, rn = 0;
+      for (int i = pb - win + 1; i <= pb; ++i) {
+        const double f = sMF[i];
+        const double a = f > 0.0 ? f : 0.0, b = f < 0.0 ? -f : 0.0;
+        pos += a;
+        neg += b;
+        rp = a == pp ? rp + 1 : 1;
+        rn = b == pn ? rn + 1 : 1;
+        pp = a;
+        pn = b;
+      }
+#pragma unroll
+      for (int k = 0; k < EN_K; ++k) {
+        const int t = tb + k, p = pb + k;
+        if (k > 0) {
+          const double f = sMF[p], fo = sMF[p - win];
+          const double a = f > 0.0 ? f : 0.0, b = f < 0.0 ? -f : 0.0;
+          pos = (pos + a) - (fo > 0.0 ? fo : 0.0);
+          neg = (neg + b) - (fo < 0.0 ? -fo : 0.0);
+          rp = a == pp ? rp + 1 : 1;
+          rn = b == pn ? rn + 1 : 1;
+          pp = a;
+          pn = b;
+        }
+        if (t < win - 1) {
+          res[k] = qnan();
+          continue;
+        }
+        // an all-zero flow window sums to exactly 0 (pandas' compensated sum)
+        const double ps = rp >= win && pp == 0.0 ? 0.0 : (pos < 0.0 ? 0.0 : pos);
+        const double ns = rn >= win && pn == 0.0 ? 0.0 : (neg < 0.0 ? 0.0 : neg);
+        res[k] = oscillator(ps, ns);
+      }
+      store4(P.out[BQ_MFI] + orow, tb, T, vout, res);
+    }
 
-// pandas.core.window.ewm: comass from span, alpha = 1 / (1 + comass)
-static double ewm_alpha_from_span(double span) {
-  const double com = (span - 1.0) / 2.0;
-  return 1.0 / (1.0 + com);
-}
+    if (t0 + EN_TT >= T) break;
+    __syncthreads();   // B2: every read of this tile's ring is done
 
-static void set_ema(EnrichArgs& A, int e, double alpha) {
-  const double om = 1.0 - alpha;   // old_wt = 1 * old_wt_factor
-  A.alpha[e] = alpha;
-  A.om[e] = om;
-  A.den[e] = om + alpha;
-  A.lin_a[e] = om / A.den[e];
-  A.lin_b[e] = alpha / A.den[e];
-  double ak = 1.0;
-  for (int k = 0; k < EN_K; ++k) ak *= A.lin_a[e];
-  for (int j = 0; j < 8; ++j) {
-    A.apow[e][j] = ak;
-    ak *= ak;
+    // ---- halo for the next tile: owners of ring positions [TT, R) copy them --
+    {
+      const double plast = __shfl(Ploc[EN_K - 1], WAVE - 1, WAVE);   // wave 3, lane 63
+      if (pb >= EN_TT) {
+#pragma unroll
+        for (int k = 0; k < EN_K; ++k) {
+          const int d = pb + k - EN_TT;
+          sP[d] = Ploc[k] - plast;   // re-based: halo prefix ends at 0
+          sC[d] = sC[pb + k];
+          sTR[d] = sTR[pb + k];
+          sO4[d] = sO4[pb + k];
+          sMF[d] = sMF[pb + k];
+        }
+      }
+      if (tid == EN_NT - 1) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) sEcar[e] = y[e];
+        sLcar = lcl[EN_K - 1];
+      }
+    }
   }
 }
 
@@ -453,7 +622,7 @@ void bq_default_params(bq_params* p) {
   p->bb_k = 2.0;
 }
 
-const char* bq_version(void) { return "binquant_amd 0.1.0 (gfx950)"; }
+const char* bq_version(void) { return "binquant_amd 0.2.0 (gfx950)"; }
 
 int bq_device_arch(char* buf, int buflen) {
   if (!buf || buflen <= 0) return BQ_EINVAL;
@@ -469,14 +638,21 @@ int bq_device_arch(char* buf, int buflen) {
 int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, const bq_params* params,
               double* const* out, int64_t ld_out, void* stream) {
   using namespace bq;
-  if (!in || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || T > (int64_t)0x7fffffff - EN_TT)
+  if (!in || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || T > (int64_t)0x7fffffff - 2 * EN_TT ||
+      S > 0x7fffffff)
     return BQ_EINVAL;
-  if (S == 0 || T == 0) return BQ_OK;
   bq_params dp;
   if (!params) {
     bq_default_params(&dp);
     params = &dp;
   }
+  const bq_params& P = *params;
+  for (int i = 0; i < 3; ++i)
+    if (!window_ok(P.ma_periods[i])) return BQ_EINVAL;
+  if (!window_ok(P.rsi_window) || !window_ok(P.bb_window) || !window_ok(P.atr_window) ||
+      !window_ok(P.twap_window) || !window_ok(P.mfi_window) || P.bb_ddof < 0 || P.macd_fast < 1 ||
+      P.macd_slow < 1 || P.macd_signal < 1 || P.ema_spans[0] < 1 || P.ema_spans[1] < 1)
+    return BQ_EINVAL;
   EnrichArgs A;
   memset(&A, 0, sizeof(A));
   bool any_out = false;
@@ -488,15 +664,7 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
     A.out[i] = out[i];
     any_out |= out[i] != nullptr;
   }
-  if (!any_out) return BQ_OK;
-  const bq_params& P = *params;
-  for (int i = 0; i < 3; ++i)
-    if (!window_ok(P.ma_periods[i])) return BQ_EINVAL;
-  if (!window_ok(P.rsi_window) || !window_ok(P.bb_window) || !window_ok(P.atr_window) ||
-      !window_ok(P.twap_window) || !window_ok(P.mfi_window) || P.bb_ddof < 0 ||
-      P.macd_fast < 1 || P.macd_slow < 1 || P.macd_signal < 1 || P.ema_spans[0] < 1 ||
-      P.ema_spans[1] < 1)
-    return BQ_EINVAL;
+  if (S == 0 || T == 0 || !any_out) return BQ_OK;
   A.ld_in = ld_in;
   A.ld_out = ld_out;
   A.T = (int)T;
@@ -508,13 +676,11 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   A.twap_w = P.twap_window;
   A.mfi_w = P.mfi_window;
   A.bb_k = P.bb_k;
-  set_ema(A, 0, ewm_alpha_from_span(P.macd_fast));
-  set_ema(A, 1, ewm_alpha_from_span(P.macd_slow));
-  set_ema(A, 2, ewm_alpha_from_span(P.ema_spans[0]));
-  set_ema(A, 3, ewm_alpha_from_span(P.ema_spans[1]));
-  set_ema(A, 4, ewm_alpha_from_span(P.macd_signal));
-  A.need_sig = out[BQ_MACD_SIGNAL] != nullptr;
-  A.need_macd = out[BQ_MACD] != nullptr || A.need_sig;
+  A.span[E_FAST] = P.macd_fast;
+  A.span[E_SLOW] = P.macd_slow;
+  A.span[E_SIG] = P.macd_signal;
+  A.span[E_0] = P.ema_spans[0];
+  A.span[E_1] = P.ema_spans[1];
 
   // 16-byte vector access needs every row start 16-byte aligned.
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
@@ -524,8 +690,7 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   for (int i = 0; i < BQ_NUM_ENRICH_COLS; ++i)
     if (out[i]) vout &= aligned(out[i]);
 
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(enrich_kernel, dim3((unsigned)S), dim3(EN_NT), 0, st, A, vin, vout);
+  hipLaunchKernelGGL(enrich_kernel, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
