@@ -82,6 +82,73 @@ __device__ __forceinline__ int wave_incl_scan_max(int x, int lane) {
   return x;
 }
 
+// ---- DPP cross-lane moves (VALU, no LDS traffic) ----------------------------
+// row_shr:n shifts within each 16-lane row; wave_shr:1 shifts the whole wave by
+// one lane (GFX9 DPP). Lanes without a source read 0 (bound_ctrl), which is the
+// identity of every combine used here (sums, affine maps, max of (index+1)).
+constexpr int DPP_ROW_SHR1 = 0x111;
+constexpr int DPP_ROW_SHR2 = 0x112;
+constexpr int DPP_ROW_SHR4 = 0x114;
+constexpr int DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_WAVE_SHR1 = 0x138;
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// Inclusive wave prefix of a double-double: DPP row scans, then the row totals
+// (lanes 15, 31, 47) folded in through readlane.
+__device__ __forceinline__ dd wave_scan_dd_dpp(dd x, int lane) {
+#define BQ_DD_STEP(CTRL)                                       \
+  {                                                            \
+    const dd v = {dpp_f64<CTRL>(x.hi), dpp_f64<CTRL>(x.lo)};   \
+    x = dd_add(v, x);                                          \
+  }
+  BQ_DD_STEP(DPP_ROW_SHR1)
+  BQ_DD_STEP(DPP_ROW_SHR2)
+  BQ_DD_STEP(DPP_ROW_SHR4)
+  BQ_DD_STEP(DPP_ROW_SHR8)
+#undef BQ_DD_STEP
+  const dd r0 = {readlane_f64(x.hi, 15), readlane_f64(x.lo, 15)};
+  const dd r1 = {readlane_f64(x.hi, 31), readlane_f64(x.lo, 31)};
+  const dd r2 = {readlane_f64(x.hi, 47), readlane_f64(x.lo, 47)};
+  const dd c1 = r0, c2 = dd_add(r0, r1), c3 = dd_add(c2, r2);
+  const int row = lane >> 4;
+  if (row > 0) {
+    const dd c = row == 1 ? c1 : (row == 2 ? c2 : c3);
+    x = dd_add(c, x);
+  }
+  return x;
+}
+
+// Inclusive wave max of non-negative ints (DPP rows + readlane).
+__device__ __forceinline__ int wave_scan_max_dpp(int x, int lane) {
+  x = max(x, dpp_i32<DPP_ROW_SHR1>(x));
+  x = max(x, dpp_i32<DPP_ROW_SHR2>(x));
+  x = max(x, dpp_i32<DPP_ROW_SHR4>(x));
+  x = max(x, dpp_i32<DPP_ROW_SHR8>(x));
+  const int r0 = __builtin_amdgcn_readlane(x, 15);
+  const int r1 = max(r0, __builtin_amdgcn_readlane(x, 31));
+  const int r2 = max(r1, __builtin_amdgcn_readlane(x, 47));
+  const int row = lane >> 4;
+  const int c = row == 0 ? 0 : (row == 1 ? r0 : (row == 2 ? r1 : r2));
+  return max(x, c);
+}
+
 // A^n for 0 <= n < 2^NB from the table apow[j] = A^(2^j).
 template <int NB>
 __device__ __forceinline__ double pow_bits(const double* apow, int n) {
@@ -115,17 +182,18 @@ __device__ __forceinline__ double typical_price(double h, double l, double c) {
   return ((h + l) + c) / 3.0;
 }
 
-// 100 - 100 / (1 + a / b) with IEEE inf/NaN semantics, as pandas evaluates it.
+// 100 - 100 / (1 + a / b) for a, b >= 0 (RSI / MFI), written with one divide:
+// 100 a / (a + b). Same special cases as pandas' form (b = 0 < a -> 100,
+// a = b = 0 -> NaN, a = 0 < b -> 0); finite values agree to a few ulps.
 __device__ __forceinline__ double oscillator(double a, double b) {
-  double rs = a / b;
-  return 100.0 - (100.0 / (1.0 + rs));
+  return (100.0 * a) / (a + b);
 }
 
 // x / n for a small integer n via one reciprocal and one FMA correction:
 // the correctly rounded quotient except in rare ties (well inside the 1e-9
 // parity tolerance), at a fraction of the cost of an IEEE fp64 divide.
-__device__ __forceinline__ double div_exact(double x, double n) {
-  const double r = 1.0 / n;   // uniform per window: hoisted by the compiler
+__device__ __forceinline__ double div_exact(double x, double n, double r) {
+  // r = 1.0 / n, computed once on the host
   double q = x * r;
   const double e = fma(-q, n, x);
   return fma(e, r, q);

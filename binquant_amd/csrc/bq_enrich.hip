@@ -56,6 +56,7 @@ struct EnrichArgs {
   int rsi_w, bb_w, bb_ddof, atr_w, twap_w, mfi_w;
   int span[NE];   // macd fast, macd slow, macd signal, ema0, ema1
   double bb_k;
+  double inv_ma[3], inv_rsi, inv_bb, inv_bb_dv, inv_atr, inv_twap;   // 1.0 / window (host)
 };
 
 // Power of the per-thread state map M^(K n): lower-triangular 3x3 block for
@@ -94,12 +95,15 @@ __device__ __forceinline__ void pow_apply(const Pow& A, const double (&v)[NE], d
   r[E_1] = A.a4 * v[E_1];
 }
 
+// pandas ewm(adjust=False): weighted = old_wt*weighted + new_wt*cur;
+// weighted /= old_wt + new_wt; skipped when weighted == cur. For every integer
+// span old_wt + new_wt == 1.0 exactly and the divide is the identity: DIV=false
+// compiles it out (the host checks this with the same IEEE arithmetic).
+template <bool DIV>
 __device__ __forceinline__ double ema_step(double y, double x, const EmaConsts& E, int e) {
-  // pandas ewm(adjust=False): weighted = old_wt*weighted + new_wt*cur;
-  // weighted /= old_wt + new_wt; skipped when weighted == cur.
   if (y != x) {
     y = E.om[e] * y + E.al[e] * x;
-    if (E.divide[e]) y = y / E.den[e];
+    if (DIV) y = y / E.den[e];
   }
   return y;
 }
@@ -150,6 +154,7 @@ __device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int 
   }
 }
 
+template <bool DIV>
 __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
   // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
   __shared__ double sP[EN_R];    // close prefix: halo re-based, tile wave-local
@@ -268,13 +273,12 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
       dd tot = {0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) tot = dd_add1(tot, cu.c[k]);
-      const dd inc = wave_incl_scan_dd(tot, lane);
+      const dd inc = wave_scan_dd_dpp(tot, lane);
       if (lane == WAVE - 1) {
         sWh[w] = inc.hi;
         sWl[w] = inc.lo;
       }
-      const double eh = __shfl_up(inc.hi, 1, WAVE), el = __shfl_up(inc.lo, 1, WAVE);
-      dd acc = lane == 0 ? dd{0.0, 0.0} : dd{eh, el};
+      dd acc = {dpp_f64<DPP_WAVE_SHR1>(inc.hi), dpp_f64<DPP_WAVE_SHR1>(inc.lo)};   // lane 0 -> 0
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
         acc = dd_add1(acc, cu.c[k]);
@@ -300,15 +304,37 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
           b[E_1] = fma(E.la[E_1], b[E_1], E.lb[E_1] * x);
         }
       }
+      // row-internal Hillis-Steele over DPP row_shr 1/2/4/8 (uniform powers)
+#define BQ_EMA_STEP(CTRL, J)                                     \
+  {                                                              \
+    double v[NE], r[NE];                                         \
+    _Pragma("unroll") for (int e = 0; e < NE; ++e) v[e] = dpp_f64<CTRL>(b[e]); \
+    pow_apply(E.wstep[J], v, r);                                 \
+    _Pragma("unroll") for (int e = 0; e < NE; ++e) b[e] += r[e]; \
+  }
+      BQ_EMA_STEP(DPP_ROW_SHR1, 0)
+      BQ_EMA_STEP(DPP_ROW_SHR2, 1)
+      BQ_EMA_STEP(DPP_ROW_SHR4, 2)
+      BQ_EMA_STEP(DPP_ROW_SHR8, 3)
+#undef BQ_EMA_STEP
+      // rows 1..3 take the carry of the rows before them: c1 = R0,
+      // c2 = A^16 c1 + R1, c3 = A^16 c2 + R2, applied with A^((lane&15)+1)
+      {
+        double c1[NE], c2[NE], c3[NE], r[NE];
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int d = 1 << j;
-        double v[NE];
+        for (int e = 0; e < NE; ++e) c1[e] = readlane_f64(b[e], 15);
+        pow_apply(E.wstep[4], c1, r);
 #pragma unroll
-        for (int e = 0; e < NE; ++e) v[e] = __shfl_up(b[e], d, WAVE);
-        if (lane >= d) {
-          double r[NE];
-          pow_apply(E.wstep[j], v, r);
+        for (int e = 0; e < NE; ++e) c2[e] = r[e] + readlane_f64(b[e], 31);
+        pow_apply(E.wstep[4], c2, r);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) c3[e] = r[e] + readlane_f64(b[e], 47);
+        const int row = lane >> 4;
+        if (row > 0) {
+          double c[NE];
+#pragma unroll
+          for (int e = 0; e < NE; ++e) c[e] = row == 1 ? c1[e] : (row == 2 ? c2[e] : c3[e]);
+          pow_apply(E.lane[(lane & 15) + 1], c, r);
 #pragma unroll
           for (int e = 0; e < NE; ++e) b[e] += r[e];
         }
@@ -318,17 +344,13 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
         for (int e = 0; e < NE; ++e) sWe[w][e] = b[e];
       }
 #pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const double s = __shfl_up(b[e], 1, WAVE);
-        ex[e] = lane == 0 ? 0.0 : s;
-      }
+      for (int e = 0; e < NE; ++e) ex[e] = dpp_f64<DPP_WAVE_SHR1>(b[e]);   // lane 0 -> 0
     }
     int lpre;
-    {
-      const int inc = wave_incl_scan_max(lcl[EN_K - 1], lane);
-      if (lane == WAVE - 1) sWlc[w] = inc;
-      const int s = __shfl_up(inc, 1, WAVE);
-      lpre = lane == 0 ? -1 : s;
+    {   // last-change index + 1 (>= 0, so DPP's zero fill is the identity)
+      const int inc = wave_scan_max_dpp(lcl[EN_K - 1] + 1, lane);
+      if (lane == WAVE - 1) sWlc[w] = inc - 1;
+      lpre = dpp_i32<DPP_WAVE_SHR1>(inc) - 1;   // lane 0 -> -1
     }
     __syncthreads();   // B1: ring, wave totals, carries visible
 
@@ -375,11 +397,11 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
           y[E_FAST] = y[E_SLOW] = y[E_0] = y[E_1] = x;
           y[E_SIG] = y[E_FAST] - y[E_SLOW];
         } else {
-          y[E_FAST] = ema_step(y[E_FAST], x, E, E_FAST);
-          y[E_SLOW] = ema_step(y[E_SLOW], x, E, E_SLOW);
-          y[E_SIG] = ema_step(y[E_SIG], y[E_FAST] - y[E_SLOW], E, E_SIG);
-          y[E_0] = ema_step(y[E_0], x, E, E_0);
-          y[E_1] = ema_step(y[E_1], x, E, E_1);
+          y[E_FAST] = ema_step<DIV>(y[E_FAST], x, E, E_FAST);
+          y[E_SLOW] = ema_step<DIV>(y[E_SLOW], x, E, E_SLOW);
+          y[E_SIG] = ema_step<DIV>(y[E_SIG], y[E_FAST] - y[E_SLOW], E, E_SIG);
+          y[E_0] = ema_step<DIV>(y[E_0], x, E, E_0);
+          y[E_1] = ema_step<DIV>(y[E_1], x, E, E_1);
         }
         mfast[k] = y[E_FAST] - y[E_SLOW];
         msig[k] = y[E_SIG];
@@ -402,19 +424,20 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
     };
     // close.rolling(win).mean(): prefix difference / win, or the value itself
     // on a constant window (pandas same-value rule).
-    auto cmean = [&](int win, int k) -> double {
+    auto cmean = [&](int win, double inv, int k) -> double {
       const int t = tb + k, p = pb + k;
       if (t < win - 1) return qnan();
       if (lcl[k] <= t - win + 1) return cu.c[k];
-      return div_exact((Ploc[k] + wbw) - Pat(p - win), (double)win);
+      return div_exact((Ploc[k] + wbw) - Pat(p - win), (double)win, inv);
     };
     double res[EN_K];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (P.out[BQ_MA_FAST + i]) {
         const int win = P.ma[i];
+        const double inv = P.inv_ma[i];
 #pragma unroll
-        for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, k);
+        for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, inv, k);
         store4(P.out[BQ_MA_FAST + i] + orow, tb, T, vout, res);
       }
     }
@@ -423,7 +446,8 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
       // with the lane-local reference r = close at the lane's first candle.
       double up[EN_K], mid[EN_K], lo[EN_K];
       const int win = P.bb_w;
-      const double wd = (double)win, dv = (double)(win - P.bb_ddof), bk = P.bb_k;
+      const double dv = (double)(win - P.bb_ddof), bk = P.bb_k;
+      const double invw = P.inv_bb, invdv = P.inv_bb_dv;
       const double r = cu.c[0];
       const int gstart = EN_H - t0;   // ring position of candle 0 (tile 0 only)
       double s1 = 0.0, s2 = 0.0;
@@ -440,12 +464,12 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
           s1 = (s1 + dn) - dol;
           s2 = fma(-dol, dol, fma(dn, dn, s2));
         }
-        const double m = cmean(win, k);
+        const double m = cmean(win, invw, k);
         double sd;
         if (t < win - 1 || dv <= 0.0) sd = qnan();
         else if (lcl[k] <= t - win + 1) sd = 0.0;
         else {
-          double var = (s2 - s1 * s1 / wd) / dv;
+          double var = (s2 - s1 * s1 * invw) * invdv;
           sd = sqrt(var < 0.0 ? 0.0 : var);
         }
         mid[k] = m;
@@ -459,7 +483,7 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
     if (P.out[BQ_RSI]) {
       // gain/loss of candle i use close[i-1]; close[-1] is NaN -> 0 (where()).
       const int win = P.rsi_w;
-      const double wd = (double)win;
+      const double wd = (double)win, inv = P.inv_rsi;
       double sg = 0.0, sl = 0.0, pg = qnan(), pl = qnan();
       int rg = 0, rl = 0;
       double prev = sC[pb - win];
@@ -492,14 +516,14 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
           res[k] = qnan();
           continue;
         }
-        const double gm = rg >= win ? pg : div_exact(sg < 0.0 ? 0.0 : sg, wd);
-        const double lm = rl >= win ? pl : div_exact(sl < 0.0 ? 0.0 : sl, wd);
+        const double gm = rg >= win ? pg : div_exact(sg < 0.0 ? 0.0 : sg, wd, inv);
+        const double lm = rl >= win ? pl : div_exact(sl < 0.0 ? 0.0 : sl, wd, inv);
         res[k] = oscillator(gm, lm);
       }
       store4(P.out[BQ_RSI] + orow, tb, T, vout, res);
     }
     // sliding mean of a per-candle ring array with the same-value rule
-    auto smean = [&](const double* Q, int win, bool nonneg) {
+    auto smean = [&](const double* Q, int win, double inv, bool nonneg) {
       const double wd = (double)win;
       double s = 0.0, pq = qnan();
       int run = 0;
@@ -520,15 +544,15 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
         }
         if (t < win - 1) res[k] = qnan();
         else if (run >= win) res[k] = pq;
-        else res[k] = div_exact(nonneg && s < 0.0 ? 0.0 : s, wd);
+        else res[k] = div_exact(nonneg && s < 0.0 ? 0.0 : s, wd, inv);
       }
     };
     if (P.out[BQ_ATR]) {
-      smean(sTR, P.atr_w, true);
+      smean(sTR, P.atr_w, P.inv_atr, true);
       store4(P.out[BQ_ATR] + orow, tb, T, vout, res);
     }
     if (P.out[BQ_TWAP]) {
-      smean(sO4, P.twap_w, false);
+      smean(sO4, P.twap_w, P.inv_twap, false);
       store4(P.out[BQ_TWAP] + orow, tb, T, vout, res);
     }
     if (P.out[BQ_MFI]) {
@@ -676,6 +700,12 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   A.twap_w = P.twap_window;
   A.mfi_w = P.mfi_window;
   A.bb_k = P.bb_k;
+  for (int i = 0; i < 3; ++i) A.inv_ma[i] = 1.0 / (double)P.ma_periods[i];
+  A.inv_rsi = 1.0 / (double)P.rsi_window;
+  A.inv_bb = 1.0 / (double)P.bb_window;
+  A.inv_bb_dv = P.bb_window > P.bb_ddof ? 1.0 / (double)(P.bb_window - P.bb_ddof) : 0.0;
+  A.inv_atr = 1.0 / (double)P.atr_window;
+  A.inv_twap = 1.0 / (double)P.twap_window;
   A.span[E_FAST] = P.macd_fast;
   A.span[E_SLOW] = P.macd_slow;
   A.span[E_SIG] = P.macd_signal;
@@ -690,7 +720,17 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   for (int i = 0; i < BQ_NUM_ENRICH_COLS; ++i)
     if (out[i]) vout &= aligned(out[i]);
 
-  hipLaunchKernelGGL(enrich_kernel, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
+  // does any EMA need the explicit `/ (old_wt + new_wt)` (non-unit sum)?
+  bool div = false;
+  for (int e = 0; e < NE; ++e) {
+    const double com = ((double)A.span[e] - 1.0) / 2.0;
+    const double al = 1.0 / (1.0 + com);
+    div |= ((1.0 - al) + al) != 1.0;
+  }
+  if (div)
+    hipLaunchKernelGGL(enrich_kernel<true>, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
+  else
+    hipLaunchKernelGGL(enrich_kernel<false>, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

@@ -1,0 +1,97 @@
+"""Batched live-market-context over a [symbols x candles] panel.
+
+Replaces, for every timestamp of the panel at once, the per-message loop of
+LiveMarketContextAccumulator.refresh_context_for_timestamp
+(market_regime/live_market_context_accumulator.py:72-84): the reference
+recomputes _compute_symbol_features for every fresh symbol on every message
+(O(S^2 * 400) per 15-minute period). Here:
+
+  1. bq_market_features — per-symbol features at every t (device);
+  2. bq_breadth_partial — per-t counts/sums over this rank's symbols (device,
+     deterministic order);
+  3. all_reduce(sum) of the [T x 10] partials over the symbol shards (RCCL
+     over xGMI; the only collective of the whole hot path);
+  4. scalar scoring + market-regime annotation over T (host, numpy).
+
+BTC is replicated on every rank (one extra symbol), so relative strength and
+the BTC regime score need no communication.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import engine
+from .regime import ContextBatch, annotate_market, annotate_symbols, score_contexts
+
+
+@dataclass
+class MarketContextBatch:
+    contexts: ContextBatch
+    features: dict[str, torch.Tensor]   # this rank's [S, T] feature columns
+    partial: torch.Tensor               # reduced [T, 10] partials (device)
+
+    def context_at(self, i: int) -> dict | None:
+        return self.contexts.context_at(i)
+
+    def symbol_features_at(self, i: int, close: torch.Tensor, btc_return_t: float | None,
+                           btc_index: int | None = None) -> dict[str, np.ndarray]:
+        """Per-symbol feature row at timestamp index i (this rank's symbols),
+        with relative strength and the micro-regime annotation."""
+        f = {k: v[:, i].double().cpu().numpy() for k, v in self.features.items()}
+        c = close[:, i].cpu().numpy()
+        ret = f["return_pct"]
+        rs = np.zeros_like(ret) if btc_return_t is None else ret - btc_return_t
+        if btc_index is not None:
+            rs[btc_index] = 0.0
+        out = dict(f)
+        out.update(close=c, above_ema20=c > f["ema20"], above_ema50=c > f["ema50"], relative_strength_vs_btc=rs)
+        out.update(annotate_symbols(f["trend_score"], out["above_ema20"], out["above_ema50"], rs,
+                                    f["bb_width"], f["atr_pct"], ret))
+        return out
+
+
+def market_context_batch(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    btc_hlc: tuple[torch.Tensor, torch.Tensor, torch.Tensor],
+    max_bars: int = 400,
+    timestamps: np.ndarray | None = None,
+    total_tracked: int | None = None,
+    group=None,
+    previous_context: dict | None = None,
+) -> MarketContextBatch:
+    """Contexts at every timestamp of a (possibly sharded) [S, T] panel.
+
+    btc_hlc: the benchmark's (high, low, close) [1, T] rows, replicated.
+    total_tracked: symbols tracked across ALL ranks (default: sum of shards).
+    """
+    feats = engine.market_features(high, low, close, max_bars=max_bars)
+    part = engine.breadth_partial(close, feats)
+    S = close.shape[0]
+    n_total = S
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
+        t = torch.tensor([S], dtype=torch.int64, device=close.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        n_total = int(t.item())
+    bh, bl, bc = btc_hlc
+    bf = engine.market_features(bh, bl, bc, max_bars=max_bars)
+    btc_ret = bf["return_pct"][0].cpu().numpy()
+    btc_trend = bf["trend_score"][0].cpu().numpy()
+    btc_valid = ~np.isnan(btc_ret)
+    batch = score_contexts(
+        part.cpu().numpy(),
+        np.nan_to_num(btc_ret),
+        np.nan_to_num(btc_trend),
+        btc_valid,
+        total_tracked=total_tracked if total_tracked is not None else n_total,
+        timestamps=timestamps,
+    )
+    annotate_market(batch, previous_context)
+    return MarketContextBatch(contexts=batch, features=feats, partial=part)

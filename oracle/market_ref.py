@@ -151,6 +151,7 @@ def _score(n, advancers, decliners, sum_ret, sum_rs, above20, above50, sum_trend
         return None
     return dict(
         fresh_count=n,
+        btc_present=btc is not None,
         total_tracked_symbols=total_tracked,
         coverage_ratio=coverage_ratio,
         advancers=advancers,

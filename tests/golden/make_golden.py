@@ -1,0 +1,318 @@
+"""Generate golden vectors from the REAL reference (carkod/binquant) modules.
+
+Run in the build container only (the reference does not exist on the GPU box):
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.npz|json
+
+The reference targets Python 3.11 and imports packages absent from this
+offline image (pybinbot, pandera, dotenv). A throw-away shim directory supplies
+NAMES ONLY for those imports — enums, a permissive model base class, a
+``__class_getitem__`` for pandera's DataFrame type and ``datetime.UTC`` — and
+no arithmetic (round_numbers is only used by outputs we do not take). The
+reference modules are imported in place from /root/reference by a child
+process; nothing of the reference is copied into this repository. Only the
+numeric inputs/outputs below are written.
+
+Fixtures:
+  market_features.npz   LiveMarketContextAccumulator._compute_symbol_features
+                        (market_regime/live_market_context_accumulator.py:244-297)
+  market_context.json   refresh_context_for_timestamp + annotate_context
+                        (:72-84, :95-242; regime_transitions.py:25-232)
+  rsi_helpers.npz       MeanReversionFade._rsi (strategies/mean_reversion_fade.py:88-109),
+                        BBExtremeReversion._compute_rsi (strategies/coinrule/bb_extreme_reversion.py:134-150)
+  activity_burst.npz    ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)
+  liquidation_sweep.npz LiquidationSweepPump.compute_pump_score (strategies/liquidation_sweep_pump.py:195-269)
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import textwrap
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+REFERENCE = Path("/root/reference")
+
+SHIM_FILES = {
+    "sitecustomize.py": """
+        import datetime as _d
+        if not hasattr(_d, "UTC"):
+            _d.UTC = _d.timezone.utc
+    """,
+    "pybinbot/__init__.py": """
+        import enum
+
+        class ExchangeId(str, enum.Enum):
+            BINANCE = "binance"
+            KUCOIN = "kucoin"
+
+        class MarketType(str, enum.Enum):
+            SPOT = "SPOT"
+            FUTURES = "FUTURES"
+
+        class Position(str, enum.Enum):
+            long = "long"
+            short = "short"
+
+        class _Interval(str, enum.Enum):
+            one_minute = "1m"
+            five_minutes = "5m"
+            fifteen_minutes = "15m"
+            one_hour = "1h"
+            FIVE_MINUTES = "5min"
+            FIFTEEN_MINUTES = "15min"
+
+            def get_ms(self):
+                return {"1m": 60_000, "5m": 300_000, "15m": 900_000, "1h": 3_600_000,
+                        "5min": 300_000, "15min": 900_000}[self.value]
+
+        BinanceKlineIntervals = _Interval
+        KucoinKlineIntervals = _Interval
+
+        def round_numbers(value, decimals=6):
+            return value
+
+        class _Model:
+            def __init__(self, *args, **kwargs):
+                for k, v in kwargs.items():
+                    setattr(self, k, v)
+
+            def __class_getitem__(cls, item):
+                return cls
+
+        def __getattr__(name):
+            return type(name, (_Model,), {})
+    """,
+    "pandera/__init__.py": "",
+    "pandera/typing/__init__.py": """
+        import pandas as pd
+
+        class DataFrame(pd.DataFrame):
+            def __class_getitem__(cls, item):
+                return pd.DataFrame
+    """,
+    "dotenv/__init__.py": """
+        def load_dotenv(*args, **kwargs):
+            return False
+    """,
+}
+
+
+def write_shim(root: Path) -> None:
+    for rel, body in SHIM_FILES.items():
+        p = root / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(textwrap.dedent(body))
+
+
+# ---------------------------------------------------------------------------
+# child process: runs with PYTHONPATH=<shim>:/root/reference
+# ---------------------------------------------------------------------------
+def child(out_dir: Path) -> None:
+    import numpy as np
+    import pandas as pd
+    from types import SimpleNamespace
+
+    from market_regime.live_market_context_accumulator import LiveMarketContextAccumulator
+    from market_regime.market_state_store import MarketStateStore
+
+    rng = np.random.default_rng(20261015)
+
+    def walk(n, scale=100.0, vol=0.004, seed=None):
+        r = np.random.default_rng(seed).normal(0, vol, n)
+        c = scale * np.exp(np.cumsum(r))
+        o = np.r_[c[0], c[:-1]]
+        h = np.maximum(o, c) * (1 + np.random.default_rng(seed + 1).uniform(0, 0.003, n))
+        l = np.minimum(o, c) * (1 - np.random.default_rng(seed + 2).uniform(0, 0.003, n))
+        v = np.random.default_rng(seed + 3).lognormal(3, 1, n)
+        return o, h, l, c, v
+
+    # ---- 1. per-symbol market features ----------------------------------------
+    cases = []
+    for i, n in enumerate([1, 2, 3, 5, 14, 15, 19, 20, 21, 49, 50, 51, 120, 200, 400]):
+        o, h, l, c, v = walk(n, scale=10 ** rng.uniform(-3, 4), seed=100 + i)
+        cases.append((f"walk{n}", h, l, c))
+    c = np.full(60, 0.3)
+    cases.append(("const0.3", c * 1.0, c * 1.0, c))
+    c = np.r_[np.linspace(1, 2, 30), np.full(30, 2.7)]
+    cases.append(("ramp_then_flat", c * 1.01, c * 0.99, c))
+    c = np.r_[np.linspace(5, 1, 30), np.zeros(3)]
+    cases.append(("to_zero", c + 0.1, np.maximum(c - 0.1, 0), c))
+    feats_cols = ["close", "return_pct", "ema20", "ema50", "above_ema20", "above_ema50",
+                  "trend_score", "atr_pct", "bb_width"]
+    arrays = {}
+    names = []
+    for name, h, l, c in cases:
+        df = pd.DataFrame({"timestamp": np.arange(len(c)) * 60_000, "open": c, "high": h, "low": l,
+                           "close": c, "volume": 1.0})
+        f = LiveMarketContextAccumulator._compute_symbol_features("SYMUSDT", df)
+        arrays[f"{name}__high"] = h
+        arrays[f"{name}__low"] = l
+        arrays[f"{name}__close"] = c
+        if f is None:
+            arrays[f"{name}__features"] = np.full(len(feats_cols), np.nan)
+            arrays[f"{name}__none"] = np.array(True)
+        else:
+            arrays[f"{name}__features"] = np.array([float(getattr(f, k)) for k in feats_cols])
+            arrays[f"{name}__none"] = np.array(False)
+        names.append(name)
+    arrays["names"] = np.array(names)
+    arrays["feature_columns"] = np.array(feats_cols)
+    np.savez(out_dir / "market_features.npz", **arrays)
+
+    # ---- 2. cross-symbol context + regime annotation -----------------------------
+    def context_dict(ctx):
+        if ctx is None:
+            return None
+        d = ctx.model_dump()
+        d["symbol_features"] = {k: v for k, v in sorted(d["symbol_features"].items())}
+        d["metadata"] = {k: v for k, v in d["metadata"].items() if k != "fresh_symbols"}
+        return d
+
+    scenarios = {}
+    # (a) 40 symbols seeded at 100+i closing at 103+i, BTC first
+    store = MarketStateStore(max_bars_per_symbol=400)
+    acc = LiveMarketContextAccumulator(store, btc_symbol="BTCUSDT")
+    syms = ["BTCUSDT"] + [f"ALT{i}USDT" for i in range(1, 40)]
+    panel = {}
+    for i, s in enumerate(syms):
+        base = 100.0 + i
+        rows = [dict(timestamp=1_000, open=base * 0.99, high=base * 1.01, low=base * 0.98, close=base, volume=1000.0),
+                dict(timestamp=2_000, open=(base + 3) * 0.99, high=(base + 3) * 1.01, low=(base + 3) * 0.98,
+                     close=base + 3, volume=1000.0)]
+        panel[s] = rows
+        for r in rows:
+            store.update(s, r)
+    ctx = acc.refresh_context_for_timestamp(2_000)
+    scenarios["trend_up_40"] = dict(panel=panel, timestamps=[2_000], contexts=[context_dict(ctx)], max_bars=400,
+                                    btc="BTCUSDT", symbols=syms)
+
+    # (b) 64 random-walk symbols x 260 bars; contexts at the last 6 timestamps
+    #     (transitions between consecutive contexts), history cap 200.
+    for label, drift in (("random_64", 0.0), ("selloff_64", -0.004)):
+        store = MarketStateStore(max_bars_per_symbol=200)
+        acc = LiveMarketContextAccumulator(store, btc_symbol="BTCUSDT")
+        syms = ["BTCUSDT"] + [f"S{i:02d}USDT" for i in range(1, 64)]
+        T = 260
+        panel = {}
+        ts_list = [60_000 * (t + 1) for t in range(T)]
+        for j, s in enumerate(syms):
+            r = np.random.default_rng(500 + j).normal(drift, 0.006, T)
+            c = (10 ** np.random.default_rng(900 + j).uniform(-2, 3)) * np.exp(np.cumsum(r))
+            o = np.r_[c[0], c[:-1]]
+            h = np.maximum(o, c) * 1.002
+            l = np.minimum(o, c) * 0.998
+            rows = [dict(timestamp=ts_list[t], open=float(o[t]), high=float(h[t]), low=float(l[t]),
+                         close=float(c[t]), volume=1.0) for t in range(T)]
+            panel[s] = rows
+        for t in range(T - 6):
+            for s in syms:
+                store.update(s, panel[s][t])
+        contexts = []
+        for t in range(T - 6, T):
+            for s in syms:
+                store.update(s, panel[s][t])
+            contexts.append(context_dict(acc.refresh_context_for_timestamp(ts_list[t])))
+        scenarios[label] = dict(panel=panel, timestamps=ts_list[T - 6:], contexts=contexts, max_bars=200,
+                                btc="BTCUSDT", symbols=syms)
+    # panels as [S, T] arrays (npz); contexts as JSON
+    arrays = {}
+    meta = {}
+    for label, sc in scenarios.items():
+        syms_ = sc["symbols"]
+        for f in ("timestamp", "open", "high", "low", "close", "volume"):
+            arrays[f"{label}__{f}"] = np.array([[r[f] for r in sc["panel"][s]] for s in syms_], dtype=np.float64)
+        meta[label] = {k: v for k, v in sc.items() if k != "panel"}
+    np.savez_compressed(out_dir / "market_context_panels.npz", **arrays)
+    with open(out_dir / "market_context.json", "w") as f:
+        json.dump(meta, f, separators=(",", ":"))
+
+    # ---- 3. RSI helpers -------------------------------------------------------------
+    from strategies.coinrule.bb_extreme_reversion import BBExtremeReversion
+    from strategies.mean_reversion_fade import MeanReversionFade
+
+    rsi = {}
+    series = {
+        "walk": walk(300, seed=7)[3],
+        "rally": 100.0 + np.arange(60, dtype=float),
+        "flat": np.full(40, 5.0),
+        "selloff": 100.0 - 0.5 * np.arange(60, dtype=float),
+    }
+    for k, c in series.items():
+        rsi[f"{k}__close"] = c
+        rsi[f"{k}__wilder"] = MeanReversionFade._rsi(pd.Series(c)).to_numpy()
+        last = []
+        for n in range(1, len(c) + 1):
+            v = BBExtremeReversion._compute_rsi(pd.Series(c[:n]), 14)
+            last.append(np.nan if v is None else v)
+        rsi[f"{k}__sma_rsi_last"] = np.array(last)
+    np.savez(out_dir / "rsi_helpers.npz", **rsi)
+
+    # ---- 4. activity burst features ------------------------------------------------
+    from strategies.activity_burst_pump import ActivityBurstPump
+
+    ctx_ns = SimpleNamespace(config=SimpleNamespace(env="test"), symbol="TESTUSDT", kucoin_symbol="TEST-USDT",
+                             exchange=None, binbot_api=None, telegram_consumer=None, market_type=None,
+                             at_consumer=None, _breadth_cross_tolerance=0.05, _autotrade_stress_threshold=0.35,
+                             current_symbol_data=None, price_precision=8, qty_precision=8)
+    abp = ActivityBurstPump(ctx_ns)
+    out = {}
+    for k, (with_quote, seed) in {"with_quote": (True, 31), "no_quote": (False, 32)}.items():
+        o, h, l, c, v = walk(400, seed=seed)
+        v = v.copy()
+        spikes = np.random.default_rng(seed).choice(np.arange(30, 400), 12, replace=False)
+        v[spikes] *= 8
+        c = c.copy()
+        c[spikes] *= 1.03
+        h = np.maximum(h, c)
+        df = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v})
+        if with_quote:
+            df["quote_asset_volume"] = v * c
+        res = abp.compute_indicators(df)
+        for col in res.columns:
+            out[f"{k}__{col}"] = res[col].to_numpy(dtype=float)
+    np.savez(out_dir / "activity_burst.npz", **out)
+
+    # ---- 5. liquidation sweep pump score ------------------------------------------
+    from strategies.liquidation_sweep_pump import LiquidationSweepPump
+
+    lsp = object.__new__(LiquidationSweepPump)
+    out = {}
+    o, h, l, c, v = walk(400, seed=41)
+    t = np.arange(400, dtype=np.int64) * 900_000
+    df = pd.DataFrame({"open_time": t, "open": o, "high": h, "low": l, "close": c, "volume": v})
+    bo, bh, bl, bc, bv = walk(400, scale=60000.0, seed=42)
+    keep = np.ones(400, bool)
+    keep[[50, 51, 52, 200]] = False   # missing BTC candles -> NaN gaps after the left merge
+    dfb = pd.DataFrame({"open_time": t[keep], "close": bc[keep]})
+    res = lsp.compute_pump_score(df, dfb)
+    for col in res.columns:
+        out[col] = res[col].to_numpy(dtype=float)
+    out["btc_open_time"] = t[keep]
+    out["btc_close"] = bc[keep]
+    np.savez(out_dir / "liquidation_sweep.npz", **out)
+    print("golden fixtures written to", out_dir)
+
+
+def main() -> None:
+    if len(sys.argv) > 1 and sys.argv[1] == "--child":
+        child(Path(sys.argv[2]))
+        return
+    if not REFERENCE.exists():
+        sys.exit("make_golden.py runs only where /root/reference is mounted")
+    with tempfile.TemporaryDirectory(prefix="bq_shim_") as tmp:
+        shim = Path(tmp)
+        write_shim(shim)
+        env = dict(os.environ)
+        env["PYTHONPATH"] = f"{shim}:{REFERENCE}"
+        env["PYTHONDONTWRITEBYTECODE"] = "1"
+        env["ENV"] = "ci"
+        subprocess.run([sys.executable, __file__, "--child", str(HERE)], check=True, env=env, cwd=tmp)
+
+
+if __name__ == "__main__":
+    main()

@@ -64,3 +64,62 @@ def test_breadth_partial_is_the_symbol_sum(cuda):
     # deterministic: a second run is bitwise identical
     part2 = engine.breadth_partial(d["close"], f).cpu().numpy()
     np.testing.assert_array_equal(part, part2)
+
+
+# ---- against the reference's own golden vectors ---------------------------------
+import json  # noqa: E402
+from pathlib import Path  # noqa: E402
+
+from binquant_amd.market_regime.regime import annotate_market, score_contexts  # noqa: E402
+
+G = Path(__file__).resolve().parent / "golden"
+
+
+def test_features_kernel_matches_reference_golden(cuda):
+    z = np.load(G / "market_features.npz")
+    cols = [str(c) for c in z["feature_columns"]]
+    for name in z["names"]:
+        name = str(name)
+        h, l, c = (torch.from_numpy(np.ascontiguousarray(z[f"{name}__{k}"]))[None].cuda() for k in ("high", "low", "close"))
+        f = engine.market_features(h, l, c, max_bars=400)
+        got = {k: float(v[0, -1]) for k, v in f.items()}
+        if bool(z[f"{name}__none"]):
+            assert all(np.isnan(v) for v in got.values()), name
+            continue
+        want = dict(zip(cols, z[f"{name}__features"]))
+        for k in ("return_pct", "ema20", "ema50", "trend_score", "atr_pct", "bb_width"):
+            assert_close([got[k]], [want[k]], f"{name}.{k}", scale=[abs(want["close"]) * 1e-2 + 1e-300])
+        assert (want["close"] > got["ema20"]) == bool(want["above_ema20"]), name
+        assert (want["close"] > got["ema50"]) == bool(want["above_ema50"]), name
+
+
+@pytest.mark.parametrize("label", ["trend_up_40", "random_64", "selloff_64"])
+def test_device_context_pipeline_matches_reference_golden(cuda, label):
+    meta = json.loads((G / "market_context.json").read_text())
+    panels = np.load(G / "market_context_panels.npz")
+    sc = meta[label]
+    syms = sc["symbols"]
+    ts_all = panels[f"{label}__timestamp"][0]
+    h, l, c = (torch.from_numpy(panels[f"{label}__{k}"]).cuda() for k in ("high", "low", "close"))
+    f = engine.market_features(h, l, c, max_bars=sc["max_bars"])
+    part = engine.breadth_partial(c, f).cpu().numpy()
+    b = syms.index(sc["btc"])
+    btc_ret = f["return_pct"][b].cpu().numpy()
+    btc_trend = f["trend_score"][b].cpu().numpy()
+    idx = [int(np.flatnonzero(ts_all == ts)[0]) for ts in sc["timestamps"]]
+    ok = ~np.isnan(btc_ret[idx])
+    batch = score_contexts(part[idx], np.nan_to_num(btc_ret[idx]), np.nan_to_num(btc_trend[idx]), ok,
+                           total_tracked=len(syms), timestamps=np.array(sc["timestamps"]))
+    annotate_market(batch)
+    for i, want in enumerate(sc["contexts"]):
+        got = batch.context_at(i)
+        if want is None:
+            assert got is None
+            continue
+        for k, v in want.items():
+            if k in ("symbol_features", "metadata", "btc_symbol", "confidence", "is_provisional", "timestamp"):
+                continue
+            if isinstance(v, (bool, str, int)) or v is None:
+                assert got[k] == v, (k, got[k], v)
+            else:
+                assert got[k] == pytest.approx(v, rel=1e-9, abs=1e-12), k

@@ -1,0 +1,93 @@
+"""CPU: pin the oracle against golden vectors produced by the reference's own
+modules (tests/golden/make_golden.py), and the oracle's EWM recursion against
+pandas bit for bit."""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import indicators_ref, market_ref
+
+G = Path(__file__).resolve().parent / "golden"
+
+
+def test_ewm_scalar_is_pandas_bitwise():
+    rng = np.random.default_rng(0)
+    x = 100 * np.exp(np.cumsum(rng.normal(0, 0.002, 2000)))
+    x[300:340] = x[300]
+    x[900:905] = np.nan
+    for span in (9, 12, 20, 26, 50):
+        a = 1.0 / (1.0 + (span - 1) / 2.0)
+        want = pd.Series(x).ewm(span=span, adjust=False).mean().to_numpy()
+        np.testing.assert_array_equal(indicators_ref.ewm_scalar(x, a), want)
+
+
+def test_market_features_match_reference_golden():
+    z = np.load(G / "market_features.npz")
+    cols = list(z["feature_columns"])
+    for name in z["names"]:
+        name = str(name)
+        got = market_ref.symbol_features(z[f"{name}__high"], z[f"{name}__low"], z[f"{name}__close"])
+        if bool(z[f"{name}__none"]):
+            assert got is None, name
+            continue
+        want = z[f"{name}__features"]
+        vals = np.array([float(got[k]) for k in cols])
+        np.testing.assert_array_equal(vals, want, err_msg=name)
+
+
+def _reference_contexts():
+    meta = json.loads((G / "market_context.json").read_text())
+    panels = np.load(G / "market_context_panels.npz")
+    return meta, panels
+
+
+@pytest.mark.parametrize("label", ["trend_up_40", "random_64", "selloff_64"])
+def test_oracle_context_matches_reference_golden(label):
+    meta, panels = _reference_contexts()
+    sc = meta[label]
+    syms = sc["symbols"]
+    ts_all = panels[f"{label}__timestamp"][0]
+    h, l, c = (panels[f"{label}__{k}"] for k in ("high", "low", "close"))
+    prev = None
+    for ts, want in zip(sc["timestamps"], sc["contexts"]):
+        t = int(np.flatnonzero(ts_all == ts)[0])
+        feats = {}
+        for i, s in enumerate(syms):
+            f = market_ref.panel_features_at(h[i], l[i], c[i], t, sc["max_bars"])
+            if f is not None:
+                feats[s] = f
+        ctx = market_ref.build_context_from_features(feats, sc["btc"], len(syms), feats.get(sc["btc"]))
+        if want is None:
+            assert ctx is None
+            continue
+        ctx["timestamp"] = ts
+        ctx = market_ref.annotate_market(ctx, prev)
+        for k, v in want.items():
+            if k in ("symbol_features", "metadata", "btc_symbol", "confidence", "is_provisional", "timestamp"):
+                continue
+            if isinstance(v, float):
+                assert ctx[k] == pytest.approx(v, rel=1e-12, abs=1e-15), k
+            else:
+                assert ctx[k] == v, k
+        prev = ctx
+
+
+def test_sma_rsi_matches_reference_helper():
+    """pybinbot's rsi column is SMA-smoothed; the in-repo twin is
+    BBExtremeReversion._compute_rsi (bb_extreme_reversion.py:134-150)."""
+    z = np.load(G / "rsi_helpers.npz")
+    for k in ("walk", "rally", "flat", "selloff"):
+        c = z[f"{k}__close"]
+        df = indicators_ref.rsi(pd.DataFrame({"close": c}))
+        ours = df["rsi"].to_numpy()
+        want = z[f"{k}__sma_rsi_last"]   # last value of the helper on c[:n+1], clamped
+        got = np.clip(ours, 0.0, 100.0)
+        m = ~np.isnan(want)
+        np.testing.assert_array_equal(np.isnan(got[m]), False, err_msg=k)
+        np.testing.assert_allclose(got[m], want[m], rtol=1e-13, atol=1e-12, err_msg=k)
+        # the helper refuses fewer than window+1 closes; the column is NaN for < window
+        assert np.isnan(ours[:13]).all()
