@@ -121,9 +121,17 @@ __device__ __forceinline__ void load4(const double* __restrict__ row, int tb, in
   }
 }
 
-__device__ __forceinline__ void store4(double* __restrict__ row, int tb, int T, bool vec, const double (&x)[EN_K]) {
+// Output pointers are re-read from LDS each tile (see sA), which leaves the
+// compiler with generic pointers; casting to the global address space keeps
+// the stores global_store (flat stores would also count against lgkmcnt and
+// serialise the LDS reads that follow them).
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) dbl2 gdbl2;
+
+__device__ __forceinline__ void store4(double* __restrict__ row_, int tb, int T, bool vec, const double (&x)[EN_K]) {
+  gdouble* row = (gdouble*)row_;
   if (vec && tb + EN_K <= T) {
-    dbl2* p = reinterpret_cast<dbl2*>(row + tb);
+    gdbl2* p = reinterpret_cast<gdbl2*>(row + tb);
     __builtin_nontemporal_store(dbl2{x[0], x[1]}, p);
     __builtin_nontemporal_store(dbl2{x[2], x[3]}, p + 1);
   } else {
