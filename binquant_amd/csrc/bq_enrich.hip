@@ -35,6 +35,8 @@
 
 #include <string.h>
 
+#include <type_traits>
+
 namespace bq {
 
 constexpr int EN_NT = 256;
@@ -423,184 +425,194 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
     }
 
     // ---- rolling windows -------------------------------------------------------
+    // Window start positions are at most BQ_MAX_WINDOW < 128 candles back, i.e.
+    // in this wave's slice, the previous wave's slice, or (wave 0) the halo,
+    // whose prefix is already based at 0.
     const double wbw = w == 0 ? wb[0] : w == 1 ? wb[1] : w == 2 ? wb[2] : wb[3];
-    auto Pat = [&](int pos) -> double {   // close prefix at ring position pos
-      const int i = pos - EN_H;   // wave owning ring position pos (-1: halo)
-      const int ow = i < 0 ? -1 : (i >> 8);
-      const double base = ow == 0 ? wb[0] : ow == 1 ? wb[1] : ow == 2 ? wb[2] : ow == 3 ? wb[3] : 0.0;
-      return sP[pos] + base;
-    };
-    // close.rolling(win).mean(): prefix difference / win, or the value itself
-    // on a constant window (pandas same-value rule).
-    auto cmean = [&](int win, double inv, int k) -> double {
-      const int t = tb + k, p = pb + k;
-      if (t < win - 1) return qnan();
-      if (lcl[k] <= t - win + 1) return cu.c[k];
-      return div_exact((Ploc[k] + wbw) - Pat(p - win), (double)win, inv);
-    };
-    double res[EN_K];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (P.out[BQ_MA_FAST + i]) {
-        const int win = P.ma[i];
-        const double inv = P.inv_ma[i];
-#pragma unroll
-        for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, inv, k);
-        store4(P.out[BQ_MA_FAST + i] + orow, tb, T, vout, res);
-      }
-    }
-    if (P.out[BQ_BB_UPPER] || P.out[BQ_BB_MID] || P.out[BQ_BB_LOWER]) {
-      // mean from the prefix; variance from sliding sums of (c - r), (c - r)^2
-      // with the lane-local reference r = close at the lane's first candle.
-      double up[EN_K], mid[EN_K], lo[EN_K];
-      const int win = P.bb_w;
-      const double dv = (double)(win - P.bb_ddof), bk = P.bb_k;
-      const double invw = P.inv_bb, invdv = P.inv_bb_dv;
-      const double r = cu.c[0];
+    const double wbp = w == 0 ? 0.0 : w == 1 ? wb[0] : w == 2 ? wb[1] : wb[2];
+    const int wstart = EN_H + 256 * w;   // first ring position of this wave's slice
+    // FULL: every output of the tile has a complete window (t0 >= H > max
+    // window) and the tile is complete with vector stores; drops the per-
+    // element warm-up masks and the partial-tile paths.
+    const bool full = t0 >= EN_H && t0 + EN_TT <= T && vout;
+    auto windows = [&](auto fullc) {
+      constexpr bool FULL = decltype(fullc)::value;
       const int gstart = EN_H - t0;   // ring position of candle 0 (tile 0 only)
-      double s1 = 0.0, s2 = 0.0;
-      for (int i = max(pb - win + 1, gstart); i <= pb; ++i) {
-        const double d = sC[i] - r;
-        s1 += d;
-        s2 = fma(d, d, s2);
-      }
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) {
+      auto warm = [&](int t, int win) { return !FULL && t < win - 1; };
+      auto put = [&](double* col, const double (&x)[EN_K]) {
+        if (FULL) store4(col + orow, tb, T, true, x);
+        else store4(col + orow, tb, T, vout, x);
+      };
+      // close.rolling(win).mean(): prefix difference / win, or the value
+      // itself on a constant window (pandas same-value rule).
+      auto cmean = [&](int win, double inv, int k) -> double {
         const int t = tb + k, p = pb + k;
-        if (k > 0) {
-          const double dn = cu.c[k] - r, dol = p - win >= gstart ? sC[p - win] - r : 0.0;
-          s1 = (s1 + dn) - dol;
-          s2 = fma(-dol, dol, fma(dn, dn, s2));
-        }
-        const double m = cmean(win, invw, k);
-        double sd;
-        if (t < win - 1 || dv <= 0.0) sd = qnan();
-        else if (lcl[k] <= t - win + 1) sd = 0.0;
-        else {
-          double var = (s2 - s1 * s1 * invw) * invdv;
-          sd = sqrt(var < 0.0 ? 0.0 : var);
-        }
-        mid[k] = m;
-        up[k] = m + bk * sd;
-        lo[k] = m - bk * sd;
-      }
-      if (P.out[BQ_BB_UPPER]) store4(P.out[BQ_BB_UPPER] + orow, tb, T, vout, up);
-      if (P.out[BQ_BB_MID]) store4(P.out[BQ_BB_MID] + orow, tb, T, vout, mid);
-      if (P.out[BQ_BB_LOWER]) store4(P.out[BQ_BB_LOWER] + orow, tb, T, vout, lo);
-    }
-    if (P.out[BQ_RSI]) {
-      // gain/loss of candle i use close[i-1]; close[-1] is NaN -> 0 (where()).
-      const int win = P.rsi_w;
-      const double wd = (double)win, inv = P.inv_rsi;
-      double sg = 0.0, sl = 0.0, pg = qnan(), pl = qnan();
-      int rg = 0, rl = 0;
-      double prev = sC[pb - win];
-      for (int i = pb - win + 1; i <= pb; ++i) {
-        const double c = sC[i], d = c - prev;
-        const double g = gain_of(d), l = loss_of(d);
-        sg += g;
-        sl += l;
-        rg = g == pg ? rg + 1 : 1;
-        rl = l == pl ? rl + 1 : 1;
-        pg = g;
-        pl = l;
-        prev = c;
-      }
+        if (warm(t, win)) return qnan();
+        if (lcl[k] <= t - win + 1) return cu.c[k];
+        const int q = p - win;
+        const double base = q >= wstart ? wbw : wbp;
+        return div_exact((Ploc[k] + wbw) - (sP[q] + base), (double)win, inv);
+      };
+      double res[EN_K];
 #pragma unroll
-      for (int k = 0; k < EN_K; ++k) {
-        const int t = tb + k, p = pb + k;
-        if (k > 0) {
-          const double d = cu.c[k] - cu.c[k - 1];
-          const double dold = sC[p - win] - sC[p - win - 1];
-          const double g = gain_of(d), l = loss_of(d);
-          sg = (sg + g) - gain_of(dold);
-          sl = (sl + l) - loss_of(dold);
-          rg = g == pg ? rg + 1 : 1;
-          rl = l == pl ? rl + 1 : 1;
-          pg = g;
-          pl = l;
-        }
-        if (t < win - 1) {
-          res[k] = qnan();
-          continue;
-        }
-        const double gm = rg >= win ? pg : div_exact(sg < 0.0 ? 0.0 : sg, wd, inv);
-        const double lm = rl >= win ? pl : div_exact(sl < 0.0 ? 0.0 : sl, wd, inv);
-        res[k] = oscillator(gm, lm);
-      }
-      store4(P.out[BQ_RSI] + orow, tb, T, vout, res);
-    }
-    // sliding mean of a per-candle ring array with the same-value rule
-    auto smean = [&](const double* Q, int win, double inv, bool nonneg) {
-      const double wd = (double)win;
-      double s = 0.0, pq = qnan();
-      int run = 0;
-      for (int i = pb - win + 1; i <= pb; ++i) {
-        const double q = Q[i];
-        s += q;
-        run = q == pq ? run + 1 : 1;
-        pq = q;
-      }
+      for (int i = 0; i < 3; ++i) {
+        if (P.out[BQ_MA_FAST + i]) {
+          const int win = P.ma[i];
+          const double inv = P.inv_ma[i];
 #pragma unroll
-      for (int k = 0; k < EN_K; ++k) {
-        const int t = tb + k, p = pb + k;
-        if (k > 0) {
-          const double q = Q[p];
-          s = (s + q) - Q[p - win];
+          for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, inv, k);
+          put(P.out[BQ_MA_FAST + i], res);
+        }
+      }
+      if (P.out[BQ_BB_UPPER] || P.out[BQ_BB_MID] || P.out[BQ_BB_LOWER]) {
+        // mean from the prefix; variance from sliding sums of (c - r), (c - r)^2
+        // with the lane-local reference r = close at the lane's first candle.
+        double up[EN_K], mid[EN_K], lo[EN_K];
+        const int win = P.bb_w;
+        const double bk = P.bb_k, invw = P.inv_bb, invdv = P.inv_bb_dv;
+        const bool okdv = win > P.bb_ddof;
+        const double r = cu.c[0];
+        double s1 = 0.0, s2 = 0.0;
+        for (int i = FULL ? pb - win + 1 : max(pb - win + 1, gstart); i <= pb; ++i) {
+          const double d = sC[i] - r;
+          s1 += d;
+          s2 = fma(d, d, s2);
+        }
+#pragma unroll
+        for (int k = 0; k < EN_K; ++k) {
+          const int t = tb + k, p = pb + k;
+          if (k > 0) {
+            const double dn = cu.c[k] - r;
+            const double dol = (FULL || p - win >= gstart) ? sC[p - win] - r : 0.0;
+            s1 = (s1 + dn) - dol;
+            s2 = fma(-dol, dol, fma(dn, dn, s2));
+          }
+          const double m = cmean(win, invw, k);
+          double sd;
+          if (warm(t, win) || !okdv) sd = qnan();
+          else if (lcl[k] <= t - win + 1) sd = 0.0;
+          else {
+            const double var = (s2 - s1 * s1 * invw) * invdv;
+            sd = sqrt(var < 0.0 ? 0.0 : var);
+          }
+          mid[k] = m;
+          up[k] = m + bk * sd;
+          lo[k] = m - bk * sd;
+        }
+        if (P.out[BQ_BB_UPPER]) put(P.out[BQ_BB_UPPER], up);
+        if (P.out[BQ_BB_MID]) put(P.out[BQ_BB_MID], mid);
+        if (P.out[BQ_BB_LOWER]) put(P.out[BQ_BB_LOWER], lo);
+      }
+      if (P.out[BQ_RSI]) {
+        // SMA-RSI = 100 * mean(gain) / (mean(gain) + mean(loss)) with
+        // sum(gain) + sum(loss) = A = sum|d| and sum(gain) - sum(loss) = D =
+        // c_t - c_{t-w} (telescoping): RSI = 50 (1 + D / A). Counts of up
+        // and down moves make the all-gain (100), all-loss (0) and flat (NaN)
+        // windows exact. d of candle 0 is NaN -> contributes nothing.
+        const int win = P.rsi_w;
+        double A = 0.0, prev = sC[pb - win];
+        int nup = 0, ndn = 0;
+        for (int i = pb - win + 1; i <= pb; ++i) {
+          const double c = sC[i], d = c - prev;
+          A += fmax(fabs(d), 0.0);   // fmax drops the NaN of candle 0
+          nup += d > 0.0;
+          ndn += d < 0.0;
+          prev = c;
+        }
+#pragma unroll
+        for (int k = 0; k < EN_K; ++k) {
+          const int t = tb + k, p = pb + k;
+          if (k > 0) {
+            const double d = cu.c[k] - cu.c[k - 1];
+            const double dold = sC[p - win] - sC[p - win - 1];
+            A = (A + fabs(d)) - fmax(fabs(dold), 0.0);
+            nup += (d > 0.0) - (dold > 0.0);
+            ndn += (d < 0.0) - (dold < 0.0);
+          }
+          if (warm(t, win)) {
+            res[k] = qnan();
+            continue;
+          }
+          const int q0 = FULL ? p - win : max(p - win, gstart);
+          const double D = cu.c[k] - sC[q0];
+          double v;
+          if (nup == 0 && ndn == 0) v = qnan();
+          else if (ndn == 0) v = 100.0;
+          else if (nup == 0) v = 0.0;
+          else v = 50.0 * (1.0 + D / A);
+          res[k] = v;
+        }
+        put(P.out[BQ_RSI], res);
+      }
+      // sliding mean of a per-candle ring array with the same-value rule
+      auto smean = [&](const double* Q, int win, double inv, bool nonneg) {
+        const double wd = (double)win;
+        double sum = 0.0, pq = qnan();
+        int run = 0;
+        for (int i = pb - win + 1; i <= pb; ++i) {
+          const double q = Q[i];
+          sum += q;
           run = q == pq ? run + 1 : 1;
           pq = q;
         }
-        if (t < win - 1) res[k] = qnan();
-        else if (run >= win) res[k] = pq;
-        else res[k] = div_exact(nonneg && s < 0.0 ? 0.0 : s, wd, inv);
+#pragma unroll
+        for (int k = 0; k < EN_K; ++k) {
+          const int t = tb + k, p = pb + k;
+          if (k > 0) {
+            const double q = Q[p];
+            sum = (sum + q) - Q[p - win];
+            run = q == pq ? run + 1 : 1;
+            pq = q;
+          }
+          if (warm(t, win)) res[k] = qnan();
+          else if (run >= win) res[k] = pq;
+          else res[k] = div_exact(nonneg && sum < 0.0 ? 0.0 : sum, wd, inv);
+        }
+      };
+      if (P.out[BQ_ATR]) {
+        smean(sTR, P.atr_w, P.inv_atr, true);
+        put(P.out[BQ_ATR], res);
+      }
+      if (P.out[BQ_TWAP]) {
+        smean(sO4, P.twap_w, P.inv_twap, false);
+        put(P.out[BQ_TWAP], res);
+      }
+      if (P.out[BQ_MFI]) {
+        // MFI = 100 pos / (pos + neg) with pos + neg = B = sum|f| and
+        // pos - neg = F = sum f (f = signed flow): MFI = 50 (1 + F / B);
+        // counts of up/down flows make the one-sided and empty windows exact.
+        const int win = P.mfi_w;
+        double B = 0.0, F = 0.0;
+        int nup = 0, ndn = 0;
+        for (int i = pb - win + 1; i <= pb; ++i) {
+          const double f = sMF[i];
+          B += fabs(f);
+          F += f;
+          nup += f > 0.0;
+          ndn += f < 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < EN_K; ++k) {
+          const int t = tb + k, p = pb + k;
+          if (k > 0) {
+            const double f = sMF[p], fo = sMF[p - win];
+            B = (B + fabs(f)) - fabs(fo);
+            F = (F + f) - fo;
+            nup += (f > 0.0) - (fo > 0.0);
+            ndn += (f < 0.0) - (fo < 0.0);
+          }
+          double v;
+          if (warm(t, win) || (nup == 0 && ndn == 0)) v = qnan();
+          else if (ndn == 0) v = 100.0;
+          else if (nup == 0) v = 0.0;
+          else v = 50.0 * (1.0 + F / B);
+          res[k] = v;
+        }
+        put(P.out[BQ_MFI], res);
       }
     };
-    if (P.out[BQ_ATR]) {
-      smean(sTR, P.atr_w, P.inv_atr, true);
-      store4(P.out[BQ_ATR] + orow, tb, T, vout, res);
-    }
-    if (P.out[BQ_TWAP]) {
-      smean(sO4, P.twap_w, P.inv_twap, false);
-      store4(P.out[BQ_TWAP] + orow, tb, T, vout, res);
-    }
-    if (P.out[BQ_MFI]) {
-      const int win = P.mfi_w;
-      double pos = 0.0, neg = 0.0, pp = qnan(), pn = qnan();
-      int rp = 0, rn = 0;
-      for (int i = pb - win + 1; i <= pb; ++i) {
-        const double f = sMF[i];
-        const double a = f > 0.0 ? f : 0.0, b = f < 0.0 ? -f : 0.0;
-        pos += a;
-        neg += b;
-        rp = a == pp ? rp + 1 : 1;
-        rn = b == pn ? rn + 1 : 1;
-        pp = a;
-        pn = b;
-      }
-#pragma unroll
-      for (int k = 0; k < EN_K; ++k) {
-        const int t = tb + k, p = pb + k;
-        if (k > 0) {
-          const double f = sMF[p], fo = sMF[p - win];
-          const double a = f > 0.0 ? f : 0.0, b = f < 0.0 ? -f : 0.0;
-          pos = (pos + a) - (fo > 0.0 ? fo : 0.0);
-          neg = (neg + b) - (fo < 0.0 ? -fo : 0.0);
-          rp = a == pp ? rp + 1 : 1;
-          rn = b == pn ? rn + 1 : 1;
-          pp = a;
-          pn = b;
-        }
-        if (t < win - 1) {
-          res[k] = qnan();
-          continue;
-        }
-        // an all-zero flow window sums to exactly 0 (pandas' compensated sum)
-        const double ps = rp >= win && pp == 0.0 ? 0.0 : (pos < 0.0 ? 0.0 : pos);
-        const double ns = rn >= win && pn == 0.0 ? 0.0 : (neg < 0.0 ? 0.0 : neg);
-        res[k] = oscillator(ps, ns);
-      }
-      store4(P.out[BQ_MFI] + orow, tb, T, vout, res);
-    }
+    if (full) windows(std::true_type{});
+    else windows(std::false_type{});
 
     if (t0 + EN_TT >= T) break;
     __syncthreads();   // B2: every read of this tile's ring is done
