@@ -1,0 +1,191 @@
+"""pybinbot.Indicators-compatible DataFrame API backed by the gfx950 kernels.
+
+Drop-in for the calls binquant makes (producers/context_evaluator.py:249-261,
+strategies/coinrule/price_tracker.py:185):
+
+    df = Indicators.moving_averages(df, 7)       # adds "ma_7"
+    df = Indicators.macd(df=df)                  # "macd", "macd_signal"
+    df = Indicators.rsi(df=df)                   # "rsi"
+    df = Indicators.ma_spreads(df)               # "big_ma_spread", "small_ma_spread"
+    df = Indicators.bollinguer_spreads(df)       # "bb_upper", "bb_mid", "bb_lower"
+    df = Indicators.set_twap(df)                 # "twap"
+    df = Indicators.atr(df=df, window=14)        # "ATR"
+    value = Indicators.mfi(df, window=14)        # float of the last candle
+
+Each call returns the frame with the columns added (callers rebind, as in the
+reference). ``indicators_enrichment(df)`` runs the whole
+ContextEvaluator.indicators_enrichment set in ONE launch, and
+``Indicators.batch(panel)`` / ``enrich_frames(frames)`` process many symbols
+per launch — the batched form the hot path is meant to use. Frames of
+different lengths are end-padded into one [S, T_max] panel: every output at t
+depends only on candles <= t, so padding never changes a valid row.
+
+Inputs are coerced with pd.to_numeric like Candles.pre_process does; a missing
+OHLCV column raises ValueError naming it (tests/test_ohlc.py:35-64 semantics).
+"""
+
+from __future__ import annotations
+
+from collections.abc import Mapping, Sequence
+
+import numpy as np
+import pandas as pd
+import torch
+
+from . import engine
+from ._lib import ENRICH_COLUMNS, INPUT_FIELDS, MAX_WINDOW
+
+_DEVICE = "cuda"
+
+
+def _device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("binquant_amd.Indicators needs a HIP device (no CPU fallback)")
+    return torch.device(_DEVICE)
+
+
+def _column(df: pd.DataFrame, name: str) -> np.ndarray:
+    if name not in df.columns:
+        if name == "volume":
+            return np.zeros(len(df))
+        if name == "open":
+            name = "close"
+        else:
+            raise ValueError(f"Missing required candle field '{name}'.")
+    vals = pd.to_numeric(df[name], errors="coerce").to_numpy(dtype=np.float64)
+    return vals
+
+
+def _frame_inputs(df: pd.DataFrame) -> list[np.ndarray]:
+    if "close" not in df.columns:
+        raise ValueError("Missing required candle field 'close'.")
+    return [_column(df, f) for f in INPUT_FIELDS]
+
+
+def _run(df: pd.DataFrame, params: engine.IndicatorParams, columns) -> dict[str, np.ndarray]:
+    host = _frame_inputs(df)   # validates columns before touching the device
+    dev = _device()
+    ins = [torch.from_numpy(np.ascontiguousarray(x)).to(dev)[None, :] for x in host]
+    out = engine.enrich(*ins, params=params, columns=columns)
+    return {k: v[0].cpu().numpy() for k, v in out.items()}
+
+
+def _check_window(w: int, what: str) -> int:
+    w = int(w)
+    if not 1 <= w <= MAX_WINDOW:
+        raise ValueError(f"{what}: window {w} outside [1, {MAX_WINDOW}]")
+    return w
+
+
+class Indicators:
+    """Static-method surface of pybinbot.Indicators (names and arguments as
+    called in binquant). Each method mutates and returns the frame."""
+
+    @staticmethod
+    def moving_averages(df: pd.DataFrame, period: int = 7) -> pd.DataFrame:
+        p = engine.IndicatorParams(ma_periods=(_check_window(period, "moving_averages"), 25, 100))
+        df[f"ma_{int(period)}"] = _run(df, p, ("ma_7",))["ma_7"]
+        return df
+
+    @staticmethod
+    def macd(df: pd.DataFrame, fast: int = 12, slow: int = 26, signal: int = 9) -> pd.DataFrame:
+        p = engine.IndicatorParams(macd_fast=fast, macd_slow=slow, macd_signal=signal)
+        r = _run(df, p, ("macd", "macd_signal"))
+        df["macd"] = r["macd"]
+        df["macd_signal"] = r["macd_signal"]
+        return df
+
+    @staticmethod
+    def rsi(df: pd.DataFrame, window: int = 14) -> pd.DataFrame:
+        p = engine.IndicatorParams(rsi_window=_check_window(window, "rsi"))
+        df["rsi"] = _run(df, p, ("rsi",))["rsi"]
+        return df
+
+    @staticmethod
+    def ma_spreads(df: pd.DataFrame) -> pd.DataFrame:
+        """Spreads of the moving averages (percent). No in-repo reader
+        (SURVEY §8a a4); needs ma_7/ma_25/ma_100, computed if absent."""
+        for p in (7, 25, 100):
+            if f"ma_{p}" not in df.columns:
+                Indicators.moving_averages(df, p)
+        df["big_ma_spread"] = (abs(df["ma_100"] - df["ma_25"]) / df["ma_100"]) * 100
+        df["small_ma_spread"] = (abs(df["ma_25"] - df["ma_7"]) / df["ma_25"]) * 100
+        return df
+
+    @staticmethod
+    def bollinguer_spreads(df: pd.DataFrame, window: int = 20, num_std: float = 2.0, ddof: int = 1) -> pd.DataFrame:
+        p = engine.IndicatorParams(bb_window=_check_window(window, "bollinguer_spreads"), bb_k=num_std, bb_ddof=ddof)
+        r = _run(df, p, ("bb_upper", "bb_mid", "bb_lower"))
+        df["bb_mid"] = r["bb_mid"]
+        df["bb_upper"] = r["bb_upper"]
+        df["bb_lower"] = r["bb_lower"]
+        return df
+
+    @staticmethod
+    def set_twap(df: pd.DataFrame, periods: int = 12) -> pd.DataFrame:
+        p = engine.IndicatorParams(twap_window=_check_window(periods, "set_twap"))
+        df["twap"] = _run(df, p, ("twap",))["twap"]
+        return df
+
+    @staticmethod
+    def atr(df: pd.DataFrame, window: int = 14) -> pd.DataFrame:
+        p = engine.IndicatorParams(atr_window=_check_window(window, "atr"))
+        df["ATR"] = _run(df, p, ("ATR",))["ATR"]
+        return df
+
+    @staticmethod
+    def mfi(df: pd.DataFrame, window: int = 14) -> float:
+        p = engine.IndicatorParams(mfi_window=_check_window(window, "mfi"))
+        return float(_run(df, p, ("mfi",))["mfi"][-1])
+
+    @staticmethod
+    def batch(panel: Mapping[str, np.ndarray | torch.Tensor], params: engine.IndicatorParams | None = None,
+              columns=ENRICH_COLUMNS) -> dict[str, torch.Tensor]:
+        """[S, T] panel (numpy or device tensors) -> {column: [S, T] device tensor}."""
+        dev = _device()
+        ins = []
+        for f in INPUT_FIELDS:
+            x = panel[f]
+            if not isinstance(x, torch.Tensor):
+                x = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.float64)))
+            ins.append(x.to(dev, dtype=torch.float64))
+        return engine.enrich(*ins, params=params, columns=columns)
+
+
+def indicators_enrichment(df: pd.DataFrame, params: engine.IndicatorParams | None = None) -> pd.DataFrame:
+    """ContextEvaluator.indicators_enrichment (producers/context_evaluator.py:240-263)
+    in one kernel launch: ma_7/25/100, macd (+macd_signal), rsi, ma spreads,
+    bb_upper/bb_mid/bb_lower, twap, ATR — plus ema20/ema50 and mfi."""
+    r = _run(df, params or engine.IndicatorParams(), ENRICH_COLUMNS)
+    for k in ENRICH_COLUMNS:
+        df[k] = r[k]
+    df["big_ma_spread"] = (abs(df["ma_100"] - df["ma_25"]) / df["ma_100"]) * 100
+    df["small_ma_spread"] = (abs(df["ma_25"] - df["ma_7"]) / df["ma_25"]) * 100
+    return df
+
+
+def enrich_frames(frames: Sequence[pd.DataFrame], params: engine.IndicatorParams | None = None,
+                  columns=ENRICH_COLUMNS) -> list[pd.DataFrame]:
+    """Enrich many symbols' frames (ragged lengths allowed) in ONE launch."""
+    if not frames:
+        return []
+    lens = [len(f) for f in frames]
+    T = max(lens)
+    S = len(frames)
+    host = {f: np.zeros((S, T)) for f in INPUT_FIELDS}
+    for s, df in enumerate(frames):
+        vals = _frame_inputs(df)
+        n = lens[s]
+        for f, v in zip(INPUT_FIELDS, vals):
+            host[f][s, :n] = v
+            if n and n < T:
+                host[f][s, n:] = v[-1]   # end padding (never read by valid rows)
+    out = Indicators.batch(host, params=params, columns=columns)
+    host_out = {k: v.cpu().numpy() for k, v in out.items()}
+    res = []
+    for s, df in enumerate(frames):
+        n = lens[s]
+        for k in columns:
+            df[k] = host_out[k][s, :n]
+        res.append(df)
+    return res

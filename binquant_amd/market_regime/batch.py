@@ -55,6 +55,34 @@ class MarketContextBatch:
         return out
 
 
+def shard_bounds(n_symbols: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous symbol block of `rank` (S/world per GPU)."""
+    base, extra = divmod(n_symbols, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def reduce_partials(part: torch.Tensor, n_local: int, group=None) -> tuple[torch.Tensor, int]:
+    """all_reduce(sum) of the [T, 10] partials over the symbol shards (RCCL over
+    xGMI on GPUs, gloo on CPU) plus the total symbol count. Identity on one rank."""
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
+        t = torch.tensor([n_local], dtype=torch.int64, device=part.device)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return part, int(t.item())
+    return part, n_local
+
+
+def contexts_from_partials(partial: np.ndarray, btc_return: np.ndarray, btc_trend: np.ndarray,
+                           total_tracked: int, timestamps=None, previous_context: dict | None = None) -> ContextBatch:
+    """Host scoring of reduced partials; btc_* are the benchmark's feature rows
+    (NaN where it has no features)."""
+    btc_valid = ~np.isnan(btc_return)
+    batch = score_contexts(partial, np.nan_to_num(btc_return), np.nan_to_num(btc_trend), btc_valid,
+                           total_tracked=total_tracked, timestamps=timestamps)
+    return annotate_market(batch, previous_context)
+
+
 def market_context_batch(
     high: torch.Tensor,
     low: torch.Tensor,
@@ -73,25 +101,15 @@ def market_context_batch(
     """
     feats = engine.market_features(high, low, close, max_bars=max_bars)
     part = engine.breadth_partial(close, feats)
-    S = close.shape[0]
-    n_total = S
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
-        t = torch.tensor([S], dtype=torch.int64, device=close.device)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        n_total = int(t.item())
+    part, n_total = reduce_partials(part, close.shape[0], group)
     bh, bl, bc = btc_hlc
     bf = engine.market_features(bh, bl, bc, max_bars=max_bars)
-    btc_ret = bf["return_pct"][0].cpu().numpy()
-    btc_trend = bf["trend_score"][0].cpu().numpy()
-    btc_valid = ~np.isnan(btc_ret)
-    batch = score_contexts(
+    batch = contexts_from_partials(
         part.cpu().numpy(),
-        np.nan_to_num(btc_ret),
-        np.nan_to_num(btc_trend),
-        btc_valid,
+        bf["return_pct"][0].cpu().numpy(),
+        bf["trend_score"][0].cpu().numpy(),
         total_tracked=total_tracked if total_tracked is not None else n_total,
         timestamps=timestamps,
+        previous_context=previous_context,
     )
-    annotate_market(batch, previous_context)
     return MarketContextBatch(contexts=batch, features=feats, partial=part)

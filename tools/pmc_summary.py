@@ -1,0 +1,39 @@
+"""Summarise rocprofv3 --pmc passes (tools/pmc_profile.sh) into per-launch
+numbers for one kernel; writes the `traffic` figure bench.py reports.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half
+of the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane streaming stores. Units: KiB.
+Usage: python tools/pmc_summary.py <pmc_dir> <kernel_substring> <out.json> [label]
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+pmc_dir, kern, out = sys.argv[1], sys.argv[2], sys.argv[3]
+label = sys.argv[4] if len(sys.argv) > 4 else pmc_dir
+agg = defaultdict(lambda: defaultdict(float))
+for f in sorted(glob.glob(f"{pmc_dir}/p*/run_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        if kern not in r["Kernel_Name"]:
+            continue
+        agg[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+mean = {c: sum(d.values()) / len(d) for c, d in agg.items()}
+fetch = mean.get("FETCH_SIZE", 0.0) * 1024 * 2
+write = mean.get("WRITE_SIZE", 0.0) * 1024
+try:
+    allk = json.load(open(out))
+except (OSError, ValueError):
+    allk = {}
+allk[kern] = {
+    "source": label,
+    "bytes_per_launch": fetch + write,
+    "fetch_bytes_corrected": fetch,
+    "write_bytes": write,
+    "counters_mean_per_dispatch": mean,
+    "note": "FETCH_SIZE x2 (gfx950 half-count for 16B/lane streaming reads), KiB -> bytes",
+}
+json.dump(allk, open(out, "w"), indent=1)
+print(json.dumps(allk[kern], indent=1))
