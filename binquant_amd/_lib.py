@@ -17,7 +17,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (binds libamdhip64.so.7 before our library loads)
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libbinquant_amd.so"
+LIB_PATH = Path(os.environ.get("BQ_LIB_PATH", Path(__file__).resolve().parent / "lib" / "libbinquant_amd.so"))
 
 BQ_OK = 0
 BQ_EINVAL = -1

@@ -199,6 +199,18 @@ __device__ __forceinline__ double div_exact(double x, double n, double r) {
   return fma(e, r, q);
 }
 
+// sqrt for v >= 0 from the hardware reciprocal square root plus one
+// Newton/Goldschmidt correction (~2^-46 relative; the IEEE lowering spends
+// ~15 instructions on scaling and two iterations). v == 0 -> 0.
+__device__ __forceinline__ double sqrt_nr(double v) {
+  const double r = __builtin_amdgcn_rsq(v);
+  const double s = v * r;
+  const double h = 0.5 * r;
+  const double e = fma(-s, s, v);
+  const double q = fma(h, e, s);
+  return v > 0.0 ? q : 0.0;
+}
+
 // shared/utils.py:20-23
 __device__ __forceinline__ double safe_pct(double cur, double prev) {
   if (prev == 0.0) return 0.0;

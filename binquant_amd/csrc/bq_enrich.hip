@@ -39,12 +39,22 @@
 
 namespace bq {
 
-constexpr int EN_NT = 256;
+#ifndef BQ_EN_NT
+#define BQ_EN_NT 256   // threads per workgroup
+#endif
+#ifndef BQ_EN_K
+#define BQ_EN_K 4      // consecutive candles per lane
+#endif
+#ifndef BQ_EN_WPS
+#define BQ_EN_WPS 3    // __launch_bounds__ min waves per SIMD
+#endif
+constexpr int EN_NT = BQ_EN_NT;
 constexpr int EN_NW = EN_NT / WAVE;
-constexpr int EN_K = 4;
+constexpr int EN_K = BQ_EN_K;
 constexpr int EN_TT = EN_NT * EN_K;   // 1024
 constexpr int EN_H = 128;             // halo >= BQ_MAX_WINDOW + 2
 constexpr int EN_R = EN_H + EN_TT;    // 1152
+static_assert(EN_K % 2 == 0 && EN_TT >= EN_H && EN_K * WAVE > BQ_MAX_WINDOW, "tile shape");
 
 // EMA slots in the scan state
 enum { E_FAST = 0, E_SLOW, E_SIG, E_0, E_1, NE };
@@ -115,8 +125,12 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void load4(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[EN_K]) {
   if (vec && tb + EN_K <= T) {
     const dbl2* p = reinterpret_cast<const dbl2*>(row + tb);
-    dbl2 a = p[0], b = p[1];
-    x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+#pragma unroll
+    for (int j = 0; j < EN_K / 2; ++j) {
+      const dbl2 a = p[j];
+      x[2 * j] = a.x;
+      x[2 * j + 1] = a.y;
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < EN_K; ++k) x[k] = (tb + k < T) ? row[tb + k] : 0.0;
@@ -134,8 +148,8 @@ __device__ __forceinline__ void store4(double* __restrict__ row_, int tb, int T,
   gdouble* row = (gdouble*)row_;
   if (vec && tb + EN_K <= T) {
     gdbl2* p = reinterpret_cast<gdbl2*>(row + tb);
-    __builtin_nontemporal_store(dbl2{x[0], x[1]}, p);
-    __builtin_nontemporal_store(dbl2{x[2], x[3]}, p + 1);
+#pragma unroll
+    for (int j = 0; j < EN_K / 2; ++j) __builtin_nontemporal_store(dbl2{x[2 * j], x[2 * j + 1]}, p + j);
   } else {
 #pragma unroll
     for (int k = 0; k < EN_K; ++k)
@@ -165,7 +179,7 @@ __device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int 
 }
 
 template <bool DIV>
-__global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
+__global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
   // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
   __shared__ double sP[EN_R];    // close prefix: halo re-based, tile wave-local
   __shared__ double sC[EN_R];    // close
@@ -247,6 +261,14 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
 
   Tile nx;
   load_tile(A, irow, EN_K * tid, vin, nx);
+  // EMA carry into candle 0 = (x0, x0, 0, x0, x0): pandas starts every EMA at
+  // its first value (output[0] = x0, macd signal[0] = macd[0] = 0), and the
+  // generic step from y == x leaves y unchanged, so no first-candle branch.
+  if (tid == 0) {
+    const double x0 = nx.c[0];
+    sEcar[E_FAST] = sEcar[E_SLOW] = sEcar[E_0] = sEcar[E_1] = x0;
+    sEcar[E_SIG] = 0.0;
+  }
 
   for (int t0 = 0; t0 < T; t0 += EN_TT) {
     const int tb = t0 + EN_K * tid;
@@ -303,16 +325,11 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
         const double x = cu.c[k];
-        if (tb + k == 0) {
-          b[E_FAST] = b[E_SLOW] = b[E_0] = b[E_1] = x;
-          b[E_SIG] = 0.0;
-        } else {
-          b[E_FAST] = fma(E.la[E_FAST], b[E_FAST], E.lb[E_FAST] * x);
-          b[E_SLOW] = fma(E.la[E_SLOW], b[E_SLOW], E.lb[E_SLOW] * x);
-          b[E_SIG] = fma(E.la[E_SIG], b[E_SIG], E.lb[E_SIG] * (b[E_FAST] - b[E_SLOW]));
-          b[E_0] = fma(E.la[E_0], b[E_0], E.lb[E_0] * x);
-          b[E_1] = fma(E.la[E_1], b[E_1], E.lb[E_1] * x);
-        }
+        b[E_FAST] = fma(E.la[E_FAST], b[E_FAST], E.lb[E_FAST] * x);
+        b[E_SLOW] = fma(E.la[E_SLOW], b[E_SLOW], E.lb[E_SLOW] * x);
+        b[E_SIG] = fma(E.la[E_SIG], b[E_SIG], E.lb[E_SIG] * (b[E_FAST] - b[E_SLOW]));
+        b[E_0] = fma(E.la[E_0], b[E_0], E.lb[E_0] * x);
+        b[E_1] = fma(E.la[E_1], b[E_1], E.lb[E_1] * x);
       }
       // row-internal Hillis-Steele over DPP row_shr 1/2/4/8 (uniform powers)
 #define BQ_EMA_STEP(CTRL, J)                                     \
@@ -403,16 +420,11 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
 #pragma unroll
       for (int k = 0; k < EN_K; ++k) {
         const double x = cu.c[k];
-        if (tb + k == 0) {
-          y[E_FAST] = y[E_SLOW] = y[E_0] = y[E_1] = x;
-          y[E_SIG] = y[E_FAST] - y[E_SLOW];
-        } else {
-          y[E_FAST] = ema_step<DIV>(y[E_FAST], x, E, E_FAST);
-          y[E_SLOW] = ema_step<DIV>(y[E_SLOW], x, E, E_SLOW);
-          y[E_SIG] = ema_step<DIV>(y[E_SIG], y[E_FAST] - y[E_SLOW], E, E_SIG);
-          y[E_0] = ema_step<DIV>(y[E_0], x, E, E_0);
-          y[E_1] = ema_step<DIV>(y[E_1], x, E, E_1);
-        }
+        y[E_FAST] = ema_step<DIV>(y[E_FAST], x, E, E_FAST);
+        y[E_SLOW] = ema_step<DIV>(y[E_SLOW], x, E, E_SLOW);
+        y[E_SIG] = ema_step<DIV>(y[E_SIG], y[E_FAST] - y[E_SLOW], E, E_SIG);
+        y[E_0] = ema_step<DIV>(y[E_0], x, E, E_0);
+        y[E_1] = ema_step<DIV>(y[E_1], x, E, E_1);
         mfast[k] = y[E_FAST] - y[E_SLOW];
         msig[k] = y[E_SIG];
         e0[k] = y[E_0];
@@ -428,9 +440,15 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
     // Window start positions are at most BQ_MAX_WINDOW < 128 candles back, i.e.
     // in this wave's slice, the previous wave's slice, or (wave 0) the halo,
     // whose prefix is already based at 0.
-    const double wbw = w == 0 ? wb[0] : w == 1 ? wb[1] : w == 2 ? wb[2] : wb[3];
-    const double wbp = w == 0 ? 0.0 : w == 1 ? wb[0] : w == 2 ? wb[1] : wb[2];
-    const int wstart = EN_H + 256 * w;   // first ring position of this wave's slice
+    double wbw = wb[0], wbp = 0.0;
+#pragma unroll
+    for (int u = 1; u < EN_NW; ++u) {
+      if (w == u) {
+        wbw = wb[u];
+        wbp = wb[u - 1];
+      }
+    }
+    const int wstart = EN_H + EN_K * WAVE * w;   // first ring position of this wave's slice
     // FULL: every output of the tile has a complete window (t0 >= H > max
     // window) and the tile is complete with vector stores; drops the per-
     // element warm-up masks and the partial-tile paths.
@@ -493,7 +511,7 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
           else if (lcl[k] <= t - win + 1) sd = 0.0;
           else {
             const double var = (s2 - s1 * s1 * invw) * invdv;
-            sd = sqrt(var < 0.0 ? 0.0 : var);
+            sd = sqrt_nr(var);
           }
           mid[k] = m;
           up[k] = m + bk * sd;
@@ -619,7 +637,7 @@ __global__ __launch_bounds__(EN_NT, 3) void enrich_kernel(const EnrichArgs A, in
 
     // ---- halo for the next tile: owners of ring positions [TT, R) copy them --
     {
-      const double plast = __shfl(Ploc[EN_K - 1], WAVE - 1, WAVE);   // wave 3, lane 63
+      const double plast = __shfl(Ploc[EN_K - 1], WAVE - 1, WAVE);   // last wave, lane 63
       if (pb >= EN_TT) {
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
