@@ -102,6 +102,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_state_count": (_I64, [_P]),
     "bq_market_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _PP, _I64, _P]),
     "bq_breadth_partial": (ctypes.c_int, [_P, _PP, _I64, _I64, _I64, _I64, _P, _P]),
+    "bq_beta_corr": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
 }
 
 

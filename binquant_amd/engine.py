@@ -266,3 +266,25 @@ class TickState:
         )
         _lib.check(st, "bq_tick")
         return {n: out[n] for n in cols}
+
+
+def beta_corr(
+    close: torch.Tensor,
+    btc_close: torch.Tensor,
+    window: int = 50,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """Rolling beta / correlation of log returns vs the benchmark at every t
+    (ContextEvaluator.dynamic_btc_beta_corr, producers/context_evaluator.py:154-194).
+    close: [S, T]; btc_close: [T] index-aligned with the panel."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    btc = _check_panel(btc_close.reshape(1, -1), "btc_close", (1, T)).contiguous()
+    beta = torch.empty((S, T), dtype=torch.float64, device=close.device)
+    corr = torch.empty_like(beta)
+    st = _lib.load().bq_beta_corr(
+        ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(btc.data_ptr()), S, T, _row_stride(close),
+        int(window), ctypes.c_void_p(beta.data_ptr()), ctypes.c_void_p(corr.data_ptr()), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_beta_corr")
+    return {"beta": beta, "corr": corr}

@@ -189,3 +189,38 @@ def enrich_frames(frames: Sequence[pd.DataFrame], params: engine.IndicatorParams
             df[k] = host_out[k][s, :n]
         res.append(df)
     return res
+
+
+def dynamic_btc_beta_corr(df: pd.DataFrame, df_btc: pd.DataFrame, window: int = 50,
+                          decimals: int | None = 6) -> tuple[float, float]:
+    """Drop-in for ContextEvaluator.dynamic_btc_beta_corr
+    (producers/context_evaluator.py:154-194): the frames are inner-joined on the
+    index on the host (as the reference does), the rolling beta/corr run on the
+    GPU (bq_beta_corr). Returns (0, 0) below `window` aligned returns and maps
+    NaN to 0; values are rounded to `decimals` with Python's round() in place
+    of pybinbot.round_numbers (decimals=None: unrounded)."""
+    joined = pd.DataFrame({"alt": pd.to_numeric(df["close"], errors="coerce")}).join(
+        pd.DataFrame({"btc": pd.to_numeric(df_btc["close"], errors="coerce")}), how="inner"
+    )
+    if len(joined) - 1 < window:
+        return 0.0, 0.0
+    dev = _device()
+    c = torch.from_numpy(joined["alt"].to_numpy(np.float64)).to(dev)[None, :]
+    b = torch.from_numpy(joined["btc"].to_numpy(np.float64)).to(dev)
+    out = engine.beta_corr(c, b, window=window)
+    beta = float(out["beta"][0, -1])
+    corr = float(out["corr"][0, -1])
+    beta = 0.0 if np.isnan(beta) else beta
+    corr = 0.0 if np.isnan(corr) else corr
+    if decimals is not None:
+        beta, corr = round(beta, decimals), round(corr, decimals)
+    return beta, corr
+
+
+def btc_price_change(df_btc: pd.DataFrame, periods: int = 96) -> float:
+    """BTC 24h change of ContextEvaluator.process_data (producers/context_evaluator.py:427-430):
+    close.pct_change(periods=96) * 100 at the last row (scalar; host arithmetic)."""
+    c = pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)
+    if len(c) <= periods:
+        return float("nan")
+    return float((c[-1] / c[-1 - periods] - 1.0) * 100)

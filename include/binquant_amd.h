@@ -27,6 +27,8 @@
  *   bq_market_features <- LiveMarketContextAccumulator._compute_symbol_features
  *                         market_regime/live_market_context_accumulator.py:244-297
  *                         evaluated at every timestamp of a [S][T] panel
+ *   bq_beta_corr       <- ContextEvaluator.dynamic_btc_beta_corr
+ *                         producers/context_evaluator.py:154-194
  *   bq_breadth_partial <- the per-symbol sums/counts of
  *                         LiveMarketContextAccumulator._build_context
  *                         market_regime/live_market_context_accumulator.py:135-163
@@ -174,6 +176,18 @@ int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t l
  */
 int bq_breadth_partial(const double* close, const double* const* feat, int64_t S, int64_t T,
                        int64_t ld_close, int64_t ld_feat, double* partial, void* stream);
+
+/* ---- benchmark-relative statistics ---------------------------------------- */
+/*
+ * Rolling beta and correlation of log returns vs the benchmark
+ * (ContextEvaluator.dynamic_btc_beta_corr, producers/context_evaluator.py:154-194)
+ * at every timestamp: close [S][ld_in], btc_close [T] (index-aligned with the
+ * panel), window 2..BQ_MAX_WINDOW (reference: 50). beta/corr [S][ld_out]
+ * (NULL = skip). NaN where t < window, beta NaN where var(btc) == 0. Inputs
+ * must be finite and positive (the reference dropna()s only the first return).
+ */
+int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_t T, int64_t ld_in,
+                 int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -206,3 +206,29 @@ def ewm_scalar(x, alpha: float) -> np.ndarray:
             weighted = cur
         out[i] = weighted
     return out
+
+
+def beta_corr_series(close, btc_close, window: int = 50) -> tuple[np.ndarray, np.ndarray]:
+    """ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:154-194)
+    evaluated at every candle t of an index-aligned pair: the raw (unrounded)
+    beta/corr of the last row of the prefix [0, t]; NaN while fewer than
+    `window` returns exist."""
+    alt = pd.Series(np.log(np.asarray(close, float) / np.roll(np.asarray(close, float), 1)))
+    btc = pd.Series(np.log(np.asarray(btc_close, float) / np.roll(np.asarray(btc_close, float), 1)))
+    alt.iloc[0] = np.nan
+    btc.iloc[0] = np.nan
+    r = pd.concat([alt, btc], axis=1, keys=["alt", "btc"]).dropna()
+    cov = r["alt"].rolling(window).cov(r["btc"])
+    var = r["btc"].rolling(window).var()
+    beta = (cov / var.replace(0, np.nan)).reindex(range(len(alt))).to_numpy()
+    corr = r["alt"].rolling(window).corr(r["btc"]).reindex(range(len(alt))).to_numpy()
+    return beta, corr
+
+
+def dynamic_btc_beta_corr(close, btc_close, window: int = 50) -> tuple[float, float]:
+    """Scalar form at the last row, with the reference's NaN -> 0 mapping and
+    the (0, 0) short-history case (rounding is pybinbot's round_numbers: not applied)."""
+    if len(close) - 1 < window:
+        return 0.0, 0.0
+    b, c = beta_corr_series(close, btc_close, window)
+    return (0.0 if np.isnan(b[-1]) else float(b[-1])), (0.0 if np.isnan(c[-1]) else float(c[-1]))

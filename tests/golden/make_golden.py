@@ -22,6 +22,9 @@ Fixtures:
                         BBExtremeReversion._compute_rsi (strategies/coinrule/bb_extreme_reversion.py:134-150)
   activity_burst.npz    ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)
   liquidation_sweep.npz LiquidationSweepPump.compute_pump_score (strategies/liquidation_sweep_pump.py:195-269)
+  beta_corr.npz         ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:154-194)
+                        on every prefix (last-row value), BTC pct_change(96) (:427-430).
+                        round_numbers is stubbed to identity: values are unrounded.
 """
 
 from __future__ import annotations
@@ -99,6 +102,24 @@ SHIM_FILES = {
         def load_dotenv(*args, **kwargs):
             return False
     """,
+    # python-telegram-bot (imported by consumers.telegram_consumer): names only
+    "telegram/__init__.py": """
+        class _Any:
+            def __init__(self, *a, **k):
+                pass
+
+            def __getattr__(self, n):
+                return _Any()
+
+            def __call__(self, *a, **k):
+                return _Any()
+
+        def __getattr__(name):
+            return type(name, (_Any,), {})
+    """,
+    "telegram/constants.py": "from telegram import __getattr__  # noqa\n",
+    "telegram/error.py": "from telegram import __getattr__  # noqa\n",
+    "telegram/helpers.py": "from telegram import __getattr__  # noqa\n",
 }
 
 
@@ -295,6 +316,30 @@ def child(out_dir: Path) -> None:
     out["btc_open_time"] = t[keep]
     out["btc_close"] = bc[keep]
     np.savez(out_dir / "liquidation_sweep.npz", **out)
+    # ---- 6. BTC beta / correlation (producers/context_evaluator.py:154-194) ----
+    from producers.context_evaluator import ContextEvaluator
+
+    out = {}
+    for k, (n, seed, rho) in {"corr_pos": (420, 61, 0.7), "corr_neg": (300, 62, -0.4), "short": (45, 63, 0.5)}.items():
+        rb = np.random.default_rng(seed).normal(0, 0.004, n)
+        ra = rho * rb + np.sqrt(1 - rho**2) * np.random.default_rng(seed + 1).normal(0, 0.006, n)
+        btc = 60000.0 * np.exp(np.cumsum(rb))
+        alt = 3.0 * np.exp(np.cumsum(ra))
+        if k == "corr_pos":
+            alt[200:260] = alt[200]   # flat stretch: constant returns window
+        out[f"{k}__close"] = alt
+        out[f"{k}__btc"] = btc
+        betas, corrs = [], []
+        for m in range(2, n + 1):
+            ns = SimpleNamespace(df_15m=pd.DataFrame({"close": alt[:m]}), df_btc_15m=pd.DataFrame({"close": btc[:m]}))
+            b, c = ContextEvaluator.dynamic_btc_beta_corr(ns, window=50)
+            betas.append(b)
+            corrs.append(c)
+        out[f"{k}__beta_last"] = np.array([np.nan] + betas)
+        out[f"{k}__corr_last"] = np.array([np.nan] + corrs)
+        # BTC 24h change (:427-430): pct_change(periods=96) * 100, last value
+        out[f"{k}__btc_change_96"] = (pd.Series(btc).pct_change(periods=96) * 100).to_numpy()
+    np.savez(out_dir / "beta_corr.npz", **out)
     print("golden fixtures written to", out_dir)
 
 

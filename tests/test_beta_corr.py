@@ -1,0 +1,78 @@
+"""a11/a12: rolling BTC beta/correlation and the BTC 24h change vs the
+reference's own values (tests/golden/beta_corr.npz) and the oracle."""
+
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import indicators_ref as ref
+from tests.util import assert_close
+
+G = Path(__file__).resolve().parent / "golden"
+CASES = ("corr_pos", "corr_neg", "short")
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_matches_reference_golden(case):
+    z = np.load(G / "beta_corr.npz")
+    c, b = z[f"{case}__close"], z[f"{case}__btc"]
+    beta, corr = ref.beta_corr_series(c, b, 50)
+    want_b, want_c = z[f"{case}__beta_last"], z[f"{case}__corr_last"]
+    got_b = np.where(np.isnan(beta), 0.0, beta)
+    got_c = np.where(np.isnan(corr), 0.0, corr)
+    got_b[np.arange(len(c)) < 50] = 0.0
+    got_c[np.arange(len(c)) < 50] = 0.0
+    np.testing.assert_allclose(got_b[1:], want_b[1:], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(got_c[1:], want_c[1:], rtol=1e-12, atol=1e-15)
+    chg = pd.Series(b).pct_change(periods=96).to_numpy() * 100
+    np.testing.assert_allclose(chg, z[f"{case}__btc_change_96"], rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_kernel_matches_reference_golden(cuda, case):
+    from binquant_amd import engine
+
+    z = np.load(G / "beta_corr.npz")
+    c, b = z[f"{case}__close"], z[f"{case}__btc"]
+    out = engine.beta_corr(torch.from_numpy(c)[None].cuda(), torch.from_numpy(b).cuda(), window=50)
+    beta = out["beta"][0].cpu().numpy()
+    corr = out["corr"][0].cpu().numpy()
+    want_b, want_c = z[f"{case}__beta_last"], z[f"{case}__corr_last"]
+    t = np.arange(len(c))
+    assert np.isnan(beta[t < 50]).all() and np.isnan(corr[t < 50]).all()
+    m = t >= 50
+    assert_close(np.nan_to_num(beta[m]), want_b[m], "beta", rtol=1e-9, scale=1.0)
+    assert_close(np.nan_to_num(corr[m]), want_c[m], "corr", rtol=1e-9, scale=1.0)
+
+
+@pytest.mark.gpu
+def test_kernel_panel_matches_oracle_multi_tile(cuda):
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    S, T = 24, 2600
+    p = numpy_panel(S, T, seed0=77, edges=True)
+    btc = p["close"][0].copy()
+    out = engine.beta_corr(torch.from_numpy(p["close"]).cuda(), torch.from_numpy(btc).cuda(), window=50)
+    for s in range(S):
+        wb, wc = ref.beta_corr_series(p["close"][s], btc, 50)
+        assert_close(out["beta"][s].cpu().numpy(), wb, f"beta[{s}]", rtol=1e-8, scale=1.0)
+        assert_close(out["corr"][s].cpu().numpy(), wc, f"corr[{s}]", rtol=1e-8, scale=1.0)
+
+
+@pytest.mark.gpu
+def test_dropin_scalar(cuda):
+    from binquant_amd.indicators import btc_price_change, dynamic_btc_beta_corr
+
+    z = np.load(G / "beta_corr.npz")
+    for case in CASES:
+        c, b = z[f"{case}__close"], z[f"{case}__btc"]
+        beta, corr = dynamic_btc_beta_corr(pd.DataFrame({"close": c}), pd.DataFrame({"close": b}), decimals=None)
+        assert beta == pytest.approx(z[f"{case}__beta_last"][-1], rel=1e-9, abs=1e-12)
+        assert corr == pytest.approx(z[f"{case}__corr_last"][-1], rel=1e-9, abs=1e-12)
+        assert btc_price_change(pd.DataFrame({"close": b})) == pytest.approx(
+            z[f"{case}__btc_change_96"][-1], nan_ok=True)
