@@ -55,6 +55,8 @@ PARTIAL_COLUMNS = (
     "reserved",
 )
 MAX_WINDOW = 126
+MAX_ROLLING_WINDOW = 96
+ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3}
 
 
 class BqParams(ctypes.Structure):
@@ -103,6 +105,8 @@ SIGNATURES: dict[str, tuple] = {
     "bq_market_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _PP, _I64, _P]),
     "bq_breadth_partial": (ctypes.c_int, [_P, _PP, _I64, _I64, _I64, _I64, _P, _P]),
     "bq_beta_corr": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
+    "bq_rolling": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _I64, _P]),
+    "bq_ewm": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _I32, _P, _I64, _P]),
 }
 
 

@@ -288,3 +288,61 @@ def beta_corr(
     )
     _lib.check(st, "bq_beta_corr")
     return {"beta": beta, "corr": corr}
+
+
+def rolling(
+    x: torch.Tensor,
+    window: int,
+    stat: str = "mean",
+    q: float = 0.5,
+    min_periods: int | None = None,
+    shift: int = 0,
+    out: torch.Tensor | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> torch.Tensor:
+    """x.shift(shift).rolling(window, min_periods).<stat>() along T of a [S, T]
+    panel; stat in {"quantile", "median", "mean", "sum", "max", "min"}."""
+    x = _check_panel(x, "x")
+    S, T = x.shape
+    if stat == "max":
+        stat, q = "quantile", 1.0
+    elif stat == "min":
+        stat, q = "quantile", 0.0
+    if stat not in _lib.ROLL_MODES:
+        raise ValueError(f"unknown rolling statistic {stat!r}")
+    if out is None:
+        out = torch.empty((S, T), dtype=torch.float64, device=x.device)
+    st = _lib.load().bq_rolling(
+        ctypes.c_void_p(x.data_ptr()), S, T, _row_stride(x), int(window),
+        int(window if min_periods is None else min_periods), int(shift), _lib.ROLL_MODES[stat], float(q),
+        ctypes.c_void_p(out.data_ptr()), _row_stride(out), _stream_handle(stream),
+    )
+    _lib.check(st, "bq_rolling")
+    return out
+
+
+def ewm(
+    x: torch.Tensor,
+    alpha: float | None = None,
+    span: float | None = None,
+    min_periods: int = 0,
+    out: torch.Tensor | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> torch.Tensor:
+    """x.ewm(alpha|span, adjust=False, min_periods).mean() along T (pandas'
+    exact recursion, NaN gaps decay the old weight)."""
+    x = _check_panel(x, "x")
+    S, T = x.shape
+    if (alpha is None) == (span is None):
+        raise ValueError("give exactly one of alpha / span")
+    # pandas: comass from span or alpha, alpha = 1 / (1 + comass)
+    com = (float(span) - 1.0) / 2.0 if span is not None else 1.0 / float(alpha) - 1.0
+    a = 1.0 / (1.0 + com)
+    if out is None:
+        out = torch.empty((S, T), dtype=torch.float64, device=x.device)
+    st = _lib.load().bq_ewm(
+        ctypes.c_void_p(x.data_ptr()), S, T, _row_stride(x), a, int(min_periods),
+        ctypes.c_void_p(out.data_ptr()), _row_stride(out), _stream_handle(stream),
+    )
+    _lib.check(st, "bq_ewm")
+    return out

@@ -189,6 +189,29 @@ int bq_breadth_partial(const double* close, const double* const* feat, int64_t S
 int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_t T, int64_t ld_in,
                  int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
 
+/* ---- rolling-window statistics (strategy feature pipelines) ---------------- */
+#define BQ_MAX_ROLLING_WINDOW 96
+enum bq_roll_mode { BQ_ROLL_QUANTILE = 0, BQ_ROLL_MEDIAN = 1, BQ_ROLL_MEAN = 2, BQ_ROLL_SUM = 3 };
+/*
+ * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,
+ * pandas semantics (NaNs skipped, NaN below min_periods; quantile = linear
+ * interpolation, q in [0, 1]; q = 0 / 1 give rolling min / max). Replaces the
+ * pandas rolling calls of strategies/activity_burst_pump.py:58-63,134-152,
+ * strategies/liquidation_sweep_pump.py:218-245, strategies/failed_spike_fade.py:376-378.
+ * x, out [S][ld] fp64 device pointers; window <= BQ_MAX_ROLLING_WINDOW.
+ */
+int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
+               int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream);
+
+/*
+ * out = x.ewm(alpha=alpha, adjust=False, min_periods=min_periods).mean()
+ * (ignore_na=False: NaN gaps decay the old weight) per symbol row, the exact
+ * pandas recursion. Replaces strategies/liquidation_sweep_pump.py:215-217,
+ * :265-266 and strategies/mean_reversion_fade.py:94-99.
+ */
+int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, int32_t min_periods, double* out,
+           int64_t ld_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
