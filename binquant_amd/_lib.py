@@ -56,7 +56,7 @@ PARTIAL_COLUMNS = (
 )
 MAX_WINDOW = 126
 MAX_ROLLING_WINDOW = 96
-ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3}
+ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5}
 
 
 class BqParams(ctypes.Structure):
@@ -107,6 +107,8 @@ SIGNATURES: dict[str, tuple] = {
     "bq_beta_corr": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_rolling": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _I64, _P]),
     "bq_ewm": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _I32, _P, _I64, _P]),
+    "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
+    "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
 }
 
 

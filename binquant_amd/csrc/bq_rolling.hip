@@ -10,7 +10,9 @@
 //     median:   pandas roll_median_c (mean of the two middle values for even
 //               nobs);
 //     mean:     sum / nobs with pandas' same-value rule;
-//     sum:      plain sum.
+//     sum:      Kahan-compensated like pandas add_sum / remove_sum, same-value
+//               rule (value * nobs), 0 for an empty window when min_periods = 0;
+//     var/std:  ddof 1, pandas' compensated Welford update, same-value rule -> 0.
 //     Used by ActivityBurstPump.compute_indicators
 //     (strategies/activity_burst_pump.py:58-63 median(19), :134-139
 //     quantile(0.92, 80), :147-152 max(3)), LiquidationSweepPump.compute_pump_score
@@ -117,19 +119,67 @@ __global__ __launch_bounds__(RW_LANES) void rolling_kernel(const RollArgs A) {
     return (i >= 0 && i < T) ? x[i] : qnan();
   };
   Win W{sw, lane, 0};
-  double sum = 0.0, last = qnan();
-  int run = 0;
+  // Moment modes follow pandas' window aggregations update for update
+  // (pandas/_libs/window/aggregations.pyx, 2.3.3): add_sum/remove_sum and
+  // add_mean/remove_mean keep a Kahan sum with SEPARATE add and remove
+  // compensations; add_var/remove_var a compensated Welford mean + ssqdm.
+  // Each step removes the leaving value, then adds the entering one.
+  const bool welford = A.mode >= BQ_ROLL_VAR;
+  double sum = 0.0, c_add = 0.0, c_rem = 0.0, last = qnan();
+  double mean = 0.0, ssq = 0.0;
+  int neg = 0, run = 0;   // signbit count (mean clamps); same-value run
+  auto add = [&](double v) {
+    ++W.n;
+    if (welford) {
+      const double prev_mean = mean - c_add;
+      const double y = v - c_add;
+      const double t = y - mean;
+      c_add = (t + mean) - y;
+      mean = mean + t / (double)W.n;
+      ssq = ssq + (v - prev_mean) * (v - mean);
+    } else {
+      const double y = v - c_add;
+      const double t = sum + y;
+      c_add = (t - sum) - y;
+      sum = t;
+      neg += signbit(v) ? 1 : 0;
+    }
+    run = v == last ? run + 1 : 1;   // pandas counts equal values as they are added
+    last = v;
+  };
+  auto remove = [&](double v) {
+    --W.n;
+    if (welford) {
+      if (W.n) {
+        const double prev_mean = mean - c_rem;
+        const double y = v - c_rem;
+        const double t = y - mean;
+        c_rem = (t + mean) - y;
+        mean = mean - t / (double)W.n;
+        ssq = ssq - (v - prev_mean) * (v - mean);
+      } else {
+        mean = 0.0;
+        ssq = 0.0;
+      }
+    } else {
+      const double y = -v - c_rem;
+      const double t = sum + y;
+      c_rem = (t - sum) - y;
+      sum = t;
+      neg -= signbit(v) ? 1 : 0;
+    }
+  };
   // warm-up: window of output t_begin - 1, i.e. values of t in [t_begin - w, t_begin)
   for (int t = t_begin - w; t < t_begin; ++t) {
     const double v = val(t);
     if (v == v) {
-      if (A.mode <= 1) W.insert(v);
-      else {
-        ++W.n;
-        sum += v;
+      if (A.mode <= 1) {
+        W.insert(v);
+        run = v == last ? run + 1 : 1;
+        last = v;
+      } else {
+        add(v);
       }
-      run = v == last ? run + 1 : 1;   // pandas counts equal values as they are added
-      last = v;
     }
   }
   for (int t = t_begin; t < t_end; ++t) {
@@ -140,22 +190,13 @@ __global__ __launch_bounds__(RW_LANES) void rolling_kernel(const RollArgs A) {
       else if (in) W.insert(vn);
       else if (outv) W.erase(vo);
     } else {
-      if (in) {
-        sum += vn;
-        ++W.n;
-      }
-      if (outv) {
-        sum -= vo;
-        --W.n;
-      }
-    }
-    if (in) {
-      run = vn == last ? run + 1 : 1;
-      last = vn;
+      if (outv) remove(vo);
+      if (in) add(vn);
     }
     const int n = W.n;
     double r;
-    if (n < A.minp || n == 0) r = qnan();
+    if (n == 0 && A.minp == 0 && A.mode == BQ_ROLL_SUM) r = 0.0;
+    else if (n < A.minp || n == 0) r = qnan();
     else if (A.mode == BQ_ROLL_QUANTILE) {
       if (n == 1) r = W.at(0);
       else {
@@ -171,8 +212,19 @@ __global__ __launch_bounds__(RW_LANES) void rolling_kernel(const RollArgs A) {
       r = (n & 1) ? W.at(n >> 1) : (W.at((n >> 1) - 1) + W.at(n >> 1)) / 2.0;
     } else if (A.mode == BQ_ROLL_MEAN) {
       r = run >= n ? last : sum / (double)n;   // same-value rule
-    } else {
-      r = sum;
+      if (neg == 0 && r < 0.0) r = 0.0;        // pandas calc_mean sign clamps
+      else if (neg == n && r > 0.0) r = 0.0;
+    } else if (A.mode == BQ_ROLL_SUM) {
+      r = run >= n ? last * (double)n : sum;   // same-value rule
+    } else {   // var / std, ddof = 1 (pandas calc_var)
+      double var;
+      if (n < 2) var = qnan();
+      else if (run >= n) var = 0.0;
+      else {
+        var = ssq / (double)(n - 1);
+        var = var < 0.0 ? 0.0 : var;
+      }
+      r = A.mode == BQ_ROLL_VAR ? var : sqrt(var);
     }
     out[t] = r;
   }
@@ -218,7 +270,7 @@ int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t win
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream) {
   using namespace bq;
   if (!x || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || window < 1 || window > RW_MAXW ||
-      min_periods < 0 || shift < 0 || mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_SUM || !(q >= 0.0 && q <= 1.0) ||
+      min_periods < 0 || shift < 0 || mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD || !(q >= 0.0 && q <= 1.0) ||
       T > 0x7fffffff)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;

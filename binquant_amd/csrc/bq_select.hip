@@ -1,0 +1,194 @@
+// Whole-series order statistics and the sequential label cooldown of the
+// strategy pipelines.
+//
+//   bq_row_quantile: per row, numpy.quantile(x[~isnan(x)], q) with numpy's
+//     default 'linear' method (numpy/lib/_function_base_impl.py _quantile,
+//     numpy 2.2): virtual index (n-1)*q, previous = floor, next = previous+1
+//     clamped to n-1, gamma = index - previous, and numpy's two-sided _lerp
+//     (a + (b-a)*g for g < 0.5, b - (b-a)*(1-g) otherwise). NaN when the row
+//     has no observation. Restates FailedSpikeFade.auto_calibrate
+//     (strategies/failed_spike_fade.py:229-257, np.quantile of dropna'd
+//     volume_ratio / price_change_abs) and Series.quantile
+//     (relative_strength_reversal_range.py:98).
+//
+//     Mapping: one 256-thread workgroup per row, radix select over the
+//     order-preserving 64-bit image of the doubles: 8 passes of an 8-bit digit
+//     histogram in LDS narrow the k-th key, one more pass finds its successor.
+//     Every pass streams the row (<= 80 KB at T = 10^4, L2-resident after the
+//     first pass); no sort, no scratch in HBM.
+//
+//   bq_cooldown: FailedSpikeFade.apply_cooldown
+//     (strategies/failed_spike_fade.py:495-520): walking forward, a label
+//     within `bars` of the last KEPT label is cleared and flagged suppressed.
+//     The dependence is sequential (the kept set depends on earlier
+//     suppressions), so lane = symbol, one pass over its row.
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+#include <stdint.h>
+#include <string.h>
+
+namespace bq {
+
+constexpr int SQ_NT = 256;
+
+__device__ __forceinline__ uint64_t order_key(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ double key_value(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+// block-wide sum of an int (all threads get the result)
+__device__ __forceinline__ int block_sum(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  int s = 0;
+#pragma unroll
+  for (int w = 0; w < SQ_NT / 64; ++w) s += red[w];
+  return s;
+}
+
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t p = __shfl_xor(v, o);
+    v = p < v ? p : v;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  uint64_t m = red[0];
+#pragma unroll
+  for (int w = 1; w < SQ_NT / 64; ++w) m = red[w] < m ? red[w] : m;
+  return m;
+}
+
+__global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __restrict__ x, int T, int64_t ld_in,
+                                                             double q, double* __restrict__ out) {
+  __shared__ unsigned hist[256];
+  __shared__ int red_i[SQ_NT / 64];
+  __shared__ uint64_t red_u[SQ_NT / 64];
+  __shared__ uint64_t s_prefix;
+  __shared__ int s_k;
+  const int tid = threadIdx.x;
+  const double* __restrict__ r = x + (int64_t)blockIdx.x * ld_in;
+
+  int cnt = 0;
+  for (int t = tid; t < T; t += SQ_NT) cnt += r[t] == r[t];
+  const int n = block_sum(cnt, red_i);
+  if (n == 0) {
+    if (tid == 0) out[blockIdx.x] = qnan();
+    return;
+  }
+  const double vi = (double)(n - 1) * q;
+  const double fl = floor(vi);
+  const int prev = (int)fl;
+  const int next = prev + 1 < n ? prev + 1 : n - 1;
+  const double gamma = vi - fl;
+
+  // radix select of the prev-th smallest key
+  uint64_t prefix = 0, mask = 0;
+  int k = prev;
+  for (int sh = 56; sh >= 0; sh -= 8) {
+    hist[tid] = 0;   // SQ_NT == 256 bins
+    __syncthreads();
+    for (int t = tid; t < T; t += SQ_NT) {
+      const double v = r[t];
+      if (v == v) {
+        const uint64_t key = order_key(v);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int cum = 0, b = 0;
+      for (; b < 255; ++b) {
+        const int h = (int)hist[b];
+        if (cum + h > k) break;
+        cum += h;
+      }
+      s_prefix = prefix | ((uint64_t)b << sh);
+      s_k = k - cum;
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    k = s_k;
+    mask |= 255ull << sh;
+  }
+  const double a = key_value(prefix);
+  double b = a;
+  if (next != prev) {
+    int le = 0;
+    uint64_t above = ~0ull;
+    for (int t = tid; t < T; t += SQ_NT) {
+      const double v = r[t];
+      if (v == v) {
+        const uint64_t key = order_key(v);
+        le += key <= prefix;
+        if (key > prefix && key < above) above = key;
+      }
+    }
+    const int nle = block_sum(le, red_i);
+    const uint64_t mn = block_min_u64(above, red_u);
+    b = nle > next ? a : key_value(mn);
+  }
+  if (tid == 0) {
+    const double d = b - a;
+    out[blockIdx.x] = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+  }
+}
+
+__global__ __launch_bounds__(256) void cooldown_kernel(const uint8_t* __restrict__ label, int64_t S, int T,
+                                                       int64_t ld_in, int bars, uint8_t* __restrict__ kept,
+                                                       uint8_t* __restrict__ suppressed, int64_t ld_out) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= S) return;
+  const uint8_t* __restrict__ l = label + s * ld_in;
+  uint8_t* __restrict__ k = kept + s * ld_out;
+  uint8_t* __restrict__ u = suppressed + s * ld_out;
+  int last = -0x40000000;   // "None": never within reach
+  for (int i = 0; i < T; ++i) {
+    const bool on = l[i] != 0;
+    const bool sup = on && (i - last) <= bars;
+    if (on && !sup) last = i;
+    k[i] = (uint8_t)(on && !sup);
+    u[i] = (uint8_t)sup;
+  }
+}
+
+}  // namespace bq
+
+extern "C" {
+
+int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double q, double* out, void* stream) {
+  using namespace bq;
+  if (!x || !out || S < 0 || T < 0 || ld_in < T || !(q >= 0.0 && q <= 1.0) || T > 0x7fffffff || S > 0x7fffffff)
+    return BQ_EINVAL;
+  if (S == 0) return BQ_OK;
+  hipLaunchKernelGGL(row_quantile_kernel, dim3((unsigned)S), dim3(SQ_NT), 0, (hipStream_t)stream, x, (int)T, ld_in,
+                     q, out);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32_t bars, uint8_t* kept,
+                uint8_t* suppressed, int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!label || !kept || !suppressed || S < 0 || T < 0 || ld_in < T || ld_out < T || bars < 0 ||
+      T > 0x7fffffff)
+    return BQ_EINVAL;
+  if (S == 0 || T == 0) return BQ_OK;
+  hipLaunchKernelGGL(cooldown_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, label, S,
+                     (int)T, ld_in, (int)bars, kept, suppressed, ld_out);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+}  // extern "C"

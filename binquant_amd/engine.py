@@ -301,7 +301,8 @@ def rolling(
     stream: torch.cuda.Stream | None = None,
 ) -> torch.Tensor:
     """x.shift(shift).rolling(window, min_periods).<stat>() along T of a [S, T]
-    panel; stat in {"quantile", "median", "mean", "sum", "max", "min"}."""
+    panel; stat in {"quantile", "median", "mean", "sum", "var", "std", "max",
+    "min"} (var / std: ddof 1)."""
     x = _check_panel(x, "x")
     S, T = x.shape
     if stat == "max":
@@ -346,3 +347,38 @@ def ewm(
     )
     _lib.check(st, "bq_ewm")
     return out
+
+
+def row_quantile(x: torch.Tensor, q: float, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """numpy.quantile(row[~isnan(row)], q) per row (numpy 'linear' method), as
+    FailedSpikeFade.auto_calibrate (strategies/failed_spike_fade.py:229-257)
+    calls it. Returns [S] float64, NaN for rows without observations."""
+    x = _check_panel(x, "x")
+    S, T = x.shape
+    out = torch.empty((S,), dtype=torch.float64, device=x.device)
+    st = _lib.load().bq_row_quantile(
+        ctypes.c_void_p(x.data_ptr()), S, T, _row_stride(x), float(q), ctypes.c_void_p(out.data_ptr()),
+        _stream_handle(stream),
+    )
+    _lib.check(st, "bq_row_quantile")
+    return out
+
+
+def cooldown(label: torch.Tensor, bars: int, stream: torch.cuda.Stream | None = None):
+    """FailedSpikeFade.apply_cooldown (strategies/failed_spike_fade.py:495-520):
+    returns (kept, suppressed) bool [S, T] — a label within `bars` candles of
+    the last kept label is cleared and flagged suppressed."""
+    if not isinstance(label, torch.Tensor) or not label.is_cuda or label.dtype != torch.bool:
+        raise ValueError("label: expected a bool CUDA tensor (no CPU path)")
+    if label.dim() == 1:
+        label = label.unsqueeze(0)
+    label = label.contiguous()
+    S, T = label.shape
+    kept = torch.empty_like(label)
+    sup = torch.empty_like(label)
+    st = _lib.load().bq_cooldown(
+        ctypes.c_void_p(label.data_ptr()), S, T, T, int(bars), ctypes.c_void_p(kept.data_ptr()),
+        ctypes.c_void_p(sup.data_ptr()), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_cooldown")
+    return kept, sup

@@ -4,10 +4,15 @@
   (strategies/activity_burst_pump.py:51-158), the volume/price-burst detector.
 * pump_score_features — LiquidationSweepPump.compute_pump_score
   (strategies/liquidation_sweep_pump.py:195-269).
+* failed_spike_features — FailedSpikeFade.detect
+  (strategies/failed_spike_fade.py:533-544): base / early features, the
+  whole-series auto-calibration, labels, cooldown and streaks.
 
 The order statistics and recurrences run in the hand-written kernels of
-bq_rolling.hip (rolling median / quantile / mean / sum / max / min with pandas'
-NaN and min_periods rules; ewm with NaN-gap decay); the element-wise glue is
+bq_rolling.hip (rolling median / quantile / mean / sum / var / std / max / min
+with pandas' NaN and min_periods rules; ewm with NaN-gap decay) and
+bq_select.hip (whole-series numpy quantile, sequential cooldown); the
+element-wise glue is
 device tensor arithmetic in the reference's operation order. Every column
 keeps the reference's name; booleans are returned as torch.bool.
 """
@@ -24,11 +29,19 @@ NAN = float("nan")
 
 
 def _shift(x: torch.Tensor, n: int) -> torch.Tensor:
-    """pandas Series.shift(n) along T (n >= 0)."""
+    """pandas Series.shift(n) along T (negative n shifts backwards)."""
     out = torch.full_like(x, NAN)
-    if n < x.shape[-1]:
-        out[..., n:] = x[..., : x.shape[-1] - n]
+    T = x.shape[-1]
+    if 0 <= n < T:
+        out[..., n:] = x[..., : T - n]
+    elif -T < n < 0:
+        out[..., : T + n] = x[..., -n:]
     return out
+
+
+def _diff(x: torch.Tensor, n: int = 1) -> torch.Tensor:
+    """Series.diff(n)."""
+    return x - _shift(x, n)
 
 
 def _clip_lower(x: torch.Tensor, lo: float) -> torch.Tensor:
@@ -194,4 +207,180 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -
     be50 = engine.ewm(bench.contiguous(), span=50)
     out["btc_trend_score"] = ((be20 - be50) / be50).expand_as(c)
     out["relative_strength"] = out["momentum_3"] - out["btc_momentum_3"]
+    return out
+
+
+@dataclass
+class SpikeParams:
+    """FailedSpikeFade thresholds (strategies/failed_spike_fade.py:66-91) that
+    detect() uses; the auto_calibrate defaults of :229-235."""
+
+    volume_cluster_min_ratio: float = 1.6
+    volume_cluster_window: int = 8
+    volume_cluster_min_count: int = 2
+    volume_cluster_label_mode: str = "last"   # last | all | first
+    price_break_base_threshold: float = 0.03
+    price_break_dynamic_q: float = 0.85
+    price_break_use_dynamic: bool = True
+    cumulative_price_window: int = 3
+    cumulative_price_threshold: float = 0.025
+    accel_volume_deriv_window: int = 3
+    accel_volume_deriv_min: float = 0.45
+    accel_price_change_min: float = 0.015
+    require_both_patterns: bool = False
+    post_spike_cooldown_bars: int = 8
+    require_bullish_spike: bool = True
+    body_size_pct_min: float = 0.005
+    base_window: int = 12
+    streak_length: int = 3
+    # auto_calibrate(volume_quantile, price_base_floor_quantile, min_volume_ratio, min_price_abs_floor)
+    volume_quantile: float = 0.97
+    price_base_floor_quantile: float = 0.75
+    min_volume_ratio: float = 1.15
+    min_price_abs_floor: float = 0.015
+
+
+def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> dict[str, torch.Tensor]:
+    """FailedSpikeFade.detect on an [S, T] panel (one row per symbol's df_15m,
+    RangeIndex). Integer columns come back as torch.bool (label_pre /
+    label_short_pre likewise); 'volume_cluster_min_ratio' and
+    'price_break_base_threshold' hold the per-symbol auto-calibrated values."""
+    p = p or SpikeParams()
+    eps = 1e-6
+    out: dict[str, torch.Tensor] = {}
+    w = p.base_window
+    # ---- compute_base_features (:260-322) ----
+    pc = _pct_change(c, 1)
+    pca = pc.abs()
+    out["price_change"] = pc
+    out["price_change_abs"] = pca
+    body = (c - o).abs()
+    out["body_size"] = body
+    out["body_size_pct"] = body / (o + eps)
+    out["upper_wick"] = h - torch.fmax(c, o)          # DataFrame.max(axis=1) skips NaN
+    out["lower_wick"] = torch.fmin(c, o) - l
+    out["upper_wick_ratio"] = out["upper_wick"] / (body + eps)
+    out["lower_wick_ratio"] = out["lower_wick"] / (body + eps)
+    out["total_range"] = h - l
+    out["range_pct"] = out["total_range"] / (o + eps)
+    out["is_bullish"] = c > o
+    out["close_open_ratio"] = (c - o) / (o + eps)
+    out["price_ma"] = engine.rolling(c, w, "mean")
+    out["price_std"] = engine.rolling(c, w, "std")
+    out["price_zscore"] = (c - out["price_ma"]) / (out["price_std"] + eps)
+    out["volume_ma"] = engine.rolling(v, w, "mean")
+    vr = v / (out["volume_ma"] + eps)
+    out["volume_ratio"] = vr
+    out["volume_zscore"] = (v - out["volume_ma"]) / (engine.rolling(v, w, "std") + eps)
+    out["quote_volume_ma"] = engine.rolling(qv, w, "mean")
+    out["quote_volume_ratio"] = qv / (out["quote_volume_ma"] + eps)
+    out["momentum_3"] = _pct_change(c, 3)
+    out["momentum_5"] = _pct_change(c, 5)
+    out["close_to_high"] = (h - c) / (h + eps)
+    out["close_to_low"] = (c - l + eps) / (c + eps)
+    # ---- auto_calibrate (:229-257): whole-series np.quantile of the dropna'd columns ----
+    qv_thr = engine.row_quantile(vr, p.volume_quantile).unsqueeze(1)
+    qp_thr = engine.row_quantile(pca, p.price_base_floor_quantile).unsqueeze(1)
+    skip = torch.isnan(qv_thr) | torch.isnan(qp_thr)      # vols.empty or pcs.empty
+    new_vol = torch.where(qv_thr > p.min_volume_ratio, qv_thr, torch.full_like(qv_thr, p.min_volume_ratio))
+    new_floor = torch.where(qp_thr > p.min_price_abs_floor, qp_thr, torch.full_like(qp_thr, p.min_price_abs_floor))
+    base0 = p.price_break_base_threshold
+    new_base = torch.where(new_floor > base0, new_floor, torch.full_like(new_floor, base0))
+    vcmr = torch.where(skip, torch.full_like(new_vol, p.volume_cluster_min_ratio), new_vol)
+    pbbt = torch.where(skip, torch.full_like(new_base, base0), new_base)
+    out["volume_cluster_min_ratio"] = vcmr.squeeze(1)
+    out["price_break_base_threshold"] = pbbt.squeeze(1)
+    # ---- compute_early_features (:324-357) ----
+    s8 = engine.rolling(c, 8, "std")
+    s20 = engine.rolling(c, 20, "std")
+    out["rolling_price_std_8"] = s8
+    out["rolling_price_std_20"] = s20
+    out["std_ratio_8_20"] = s8 / (s20 + eps)
+    out["vol_ratio_slope_3"] = _diff(vr, 3)
+    out["vol_ratio_accel"] = _diff(out["vol_ratio_slope_3"], 1)
+    out["pc_1"] = pc
+    out["pc_2c"] = engine.rolling(pc, 2, "sum")
+    out["pc_3c"] = engine.rolling(pc, 3, "sum")
+    out["pc_pos_count_5"] = engine.rolling((pc > 0).to(torch.float64), 5, "sum")
+    out["pc_abs_sum_5"] = engine.rolling(pca, 5, "sum")
+    bsp = out["body_size_pct"]
+    out["body_size_pct_ma_10"] = engine.rolling(bsp, 10, "mean")
+    out["body_size_pct_std_10"] = engine.rolling(bsp, 10, "std")
+    out["body_size_pct_z"] = (bsp - out["body_size_pct_ma_10"]) / (out["body_size_pct_std_10"] + eps)
+    out["vol_compression_flag"] = s8 < s20 * 0.6
+    # ---- volume_cluster_flag (:360-370) ----
+    cond = vr >= vcmr
+    cnt = engine.rolling(cond.to(torch.float64), p.volume_cluster_window, "sum", min_periods=1)
+    base = (cnt >= p.volume_cluster_min_count) & cond
+    if p.volume_cluster_label_mode == "last":
+        nxt = torch.zeros_like(base)
+        nxt[:, :-1] = base[:, 1:]
+        vcf = base & ~nxt
+    elif p.volume_cluster_label_mode == "first":
+        prv = torch.zeros_like(base)
+        prv[:, 1:] = base[:, :-1]
+        vcf = base & ~prv
+    else:
+        vcf = base
+    out["volume_cluster_flag"] = vcf
+    # ---- price_break_flag (:372-400), auto_tune off ----
+    if p.price_break_use_dynamic:
+        dyn = engine.rolling(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20)
+        thr = _ffill(torch.where(torch.isnan(dyn), dyn, torch.maximum(pbbt.expand_as(dyn), dyn)))
+    else:
+        thr = pbbt.expand_as(pca).clone()
+    out["price_break_flag"] = pca >= thr
+    out["price_break_threshold_series"] = thr
+    # ---- cumulative_price_break_flag (:402-421) ----
+    cw = p.cumulative_price_window
+    if cw <= 1:
+        cum_f = torch.zeros_like(cond)
+        cum_s = torch.zeros_like(cond)
+    else:
+        cum_pos = engine.rolling(_clip_lower(pc, 0.0), cw, "sum")
+        neg_pc = torch.where(pc > 0, torch.zeros_like(pc), pc).abs()   # clip(upper=0).abs(), NaN stays
+        cum_neg = engine.rolling(neg_pc, cw, "sum")
+        vmax = engine.rolling((vr >= vcmr * 0.8).to(torch.float64), cw, "max")
+        vol_cond = torch.isnan(vmax) | (vmax != 0)          # .astype(bool): NaN -> True
+        cum_f = (cum_pos >= p.cumulative_price_threshold) & vol_cond
+        cum_s = (cum_neg >= p.cumulative_price_threshold) & vol_cond
+    out["cumulative_price_break_flag"] = cum_f
+    out["cumulative_price_break_short_flag"] = cum_s
+    # ---- acceleration_flag (:423-444) ----
+    vd = vr - _shift(vr, p.accel_volume_deriv_window)
+    acc = (vd >= p.accel_volume_deriv_min) & (pca >= p.accel_price_change_min)
+    out["accel_spike_flag"] = acc & (pc > 0)
+    out["accel_spike_short_flag"] = acc & (pc < 0)
+    # ---- apply_preliminary_label (:446-488) ----
+    if p.require_both_patterns:
+        combo = vcf & out["price_break_flag"]
+    else:
+        combo = vcf | out["price_break_flag"]
+    label_pre = combo | cum_f | out["accel_spike_flag"]
+    if p.require_bullish_spike:
+        label_pre = label_pre & out["is_bullish"]
+    if p.body_size_pct_min > 0:
+        label_pre = label_pre & (bsp >= p.body_size_pct_min)
+    label_short_pre = (combo | cum_s | out["accel_spike_short_flag"]) & (c < o)
+    if p.body_size_pct_min > 0:
+        label_short_pre = label_short_pre & (bsp >= p.body_size_pct_min)
+    out["label_pre"] = label_pre
+    out["label_short_pre"] = label_short_pre
+    # ---- compute_early_proba (:490-493): disabled in the reference ----
+    out["early_spike_proba"] = torch.full_like(c, NAN)
+    out["early_proba_aug_flag"] = torch.zeros_like(label_pre)
+    # ---- apply_cooldown (:495-520) ----
+    if p.post_spike_cooldown_bars <= 0:
+        out["label"], out["suppressed_label"] = label_pre.clone(), torch.zeros_like(label_pre)
+        out["label_short"], out["suppressed_label_short"] = label_short_pre.clone(), torch.zeros_like(label_pre)
+    else:
+        out["label"], out["suppressed_label"] = engine.cooldown(label_pre, p.post_spike_cooldown_bars)
+        out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_pre,
+                                                                            p.post_spike_cooldown_bars)
+    # ---- detect_streaks (:522-531) ----
+    n = p.streak_length
+    green = engine.rolling((c > o).to(torch.float64), n, "sum")
+    red = engine.rolling((c < o).to(torch.float64), n, "sum")
+    out["upward"] = green >= n
+    out["downward"] = red >= n
     return out

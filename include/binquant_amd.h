@@ -191,11 +191,17 @@ int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_
 
 /* ---- rolling-window statistics (strategy feature pipelines) ---------------- */
 #define BQ_MAX_ROLLING_WINDOW 96
-enum bq_roll_mode { BQ_ROLL_QUANTILE = 0, BQ_ROLL_MEDIAN = 1, BQ_ROLL_MEAN = 2, BQ_ROLL_SUM = 3 };
+enum bq_roll_mode {
+  BQ_ROLL_QUANTILE = 0, BQ_ROLL_MEDIAN = 1, BQ_ROLL_MEAN = 2, BQ_ROLL_SUM = 3,
+  BQ_ROLL_VAR = 4,   /* ddof 1 */
+  BQ_ROLL_STD = 5    /* ddof 1 */
+};
 /*
  * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,
  * pandas semantics (NaNs skipped, NaN below min_periods; quantile = linear
- * interpolation, q in [0, 1]; q = 0 / 1 give rolling min / max). Replaces the
+ * interpolation, q in [0, 1]; q = 0 / 1 give rolling min / max; sum / mean
+ * compensated, pandas' same-value rule for mean / sum / var / std; an empty
+ * window sums to 0 when min_periods is 0). Replaces the
  * pandas rolling calls of strategies/activity_burst_pump.py:58-63,134-152,
  * strategies/liquidation_sweep_pump.py:218-245, strategies/failed_spike_fade.py:376-378.
  * x, out [S][ld] fp64 device pointers; window <= BQ_MAX_ROLLING_WINDOW.
@@ -211,6 +217,25 @@ int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t win
  */
 int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, int32_t min_periods, double* out,
            int64_t ld_out, void* stream);
+
+/* ---- whole-series order statistics and label cooldown ---------------------- */
+/*
+ * out[s] = numpy.quantile(x[s][~isnan], q) (numpy 'linear' method, numpy's
+ * two-sided lerp), NaN for a row without observations. Replaces the
+ * np.quantile calls of FailedSpikeFade.auto_calibrate
+ * (strategies/failed_spike_fade.py:229-257) and Series.quantile
+ * (strategies/relative_strength_reversal_range.py:98). out: S doubles.
+ */
+int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double q, double* out, void* stream);
+
+/*
+ * FailedSpikeFade.apply_cooldown (strategies/failed_spike_fade.py:495-520):
+ * a label (nonzero byte) within `bars` candles of the last kept label is
+ * cleared in kept[] and set in suppressed[]. label/kept/suppressed: uint8
+ * [S][ld] device pointers.
+ */
+int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32_t bars, uint8_t* kept,
+                uint8_t* suppressed, int64_t ld_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,7 @@ Fixtures:
                         BBExtremeReversion._compute_rsi (strategies/coinrule/bb_extreme_reversion.py:134-150)
   activity_burst.npz    ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)
   liquidation_sweep.npz LiquidationSweepPump.compute_pump_score (strategies/liquidation_sweep_pump.py:195-269)
+  failed_spike.npz      FailedSpikeFade.detect (strategies/failed_spike_fade.py:258-544)
   beta_corr.npz         ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:154-194)
                         on every prefix (last-row value), BTC pct_change(96) (:427-430).
                         round_numbers is stubbed to identity: values are unrounded.
@@ -340,6 +341,32 @@ def child(out_dir: Path) -> None:
         # BTC 24h change (:427-430): pct_change(periods=96) * 100, last value
         out[f"{k}__btc_change_96"] = (pd.Series(btc).pct_change(periods=96) * 100).to_numpy()
     np.savez(out_dir / "beta_corr.npz", **out)
+
+    # ---- 7. FailedSpikeFade.detect (strategies/failed_spike_fade.py:258-544) ------
+    from strategies.failed_spike_fade import FailedSpikeFade
+
+    out = {}
+    for k, (n, seed) in {"fsf_a": (400, 71), "fsf_b": (400, 72), "fsf_c": (150, 73)}.items():
+        o, h, l, c, v = walk(n, seed=seed, vol=0.006)
+        c = c.copy()
+        v = v.copy()
+        rng2 = np.random.default_rng(seed)
+        for j in rng2.choice(np.arange(25, n - 2), 10, replace=False):   # volume + price spikes
+            v[j] *= rng2.uniform(3, 8)
+            c[j] *= 1 + rng2.choice([-1, 1]) * rng2.uniform(0.02, 0.06)
+        o = np.r_[c[0], c[:-1]]
+        h = np.maximum(np.maximum(o, c), h)
+        l = np.minimum(np.minimum(o, c), l)
+        df = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v, "quote_asset_volume": v * c})
+        ns = SimpleNamespace(symbol="TESTUSDT", market_type=None, df_15m=df, telegram_consumer=None,
+                             at_consumer=None, current_symbol_data=None, price_precision=8,
+                             market_breadth_data=None, strategy_cooldowns={}, strategy_states={})
+        fsf = FailedSpikeFade(ns)
+        res = fsf.detect()
+        for col in res.columns:
+            out[f"{k}__{col}"] = res[col].to_numpy(dtype=float)
+        out[f"{k}__calibrated"] = np.array([fsf.volume_cluster_min_ratio, fsf.price_break_base_threshold])
+    np.savez(out_dir / "failed_spike.npz", **out)
     print("golden fixtures written to", out_dir)
 
 

@@ -1,8 +1,9 @@
-"""a17/a18: strategy feature pipelines (bq_rolling / bq_ewm kernels + device
-glue) vs the reference's own outputs (tests/golden/activity_burst.npz,
-liquidation_sweep.npz from strategies/activity_burst_pump.py:51-158 and
-strategies/liquidation_sweep_pump.py:195-269), and the rolling primitives vs
-pandas on larger panels."""
+"""a17/a18/a19: strategy feature pipelines (bq_rolling / bq_ewm / bq_select
+kernels + device glue) vs the reference's own outputs
+(tests/golden/activity_burst.npz, liquidation_sweep.npz, failed_spike.npz from
+strategies/activity_burst_pump.py:51-158, strategies/liquidation_sweep_pump.py:195-269
+and strategies/failed_spike_fade.py:533-544), and the primitives vs pandas /
+numpy / the reference's cooldown loop on larger panels."""
 
 from pathlib import Path
 
@@ -57,6 +58,8 @@ def test_pump_score_matches_reference(cuda):
     ("median", 19, 19, 2, 0.5), ("median", 20, 5, 0, 0.5), ("quantile", 80, 20, 1, 0.92),
     ("quantile", 48, 48, 1, 0.80), ("max", 6, 6, 1, 1.0), ("min", 6, 6, 1, 0.0),
     ("mean", 20, 20, 1, 0.5), ("sum", 3, 3, 0, 0.5), ("quantile", 96, 1, 0, 0.33),
+    ("var", 12, 12, 0, 0.5), ("std", 20, 20, 0, 0.5), ("std", 8, 2, 1, 0.5), ("sum", 8, 0, 0, 0.5),
+    ("sum", 8, 1, 0, 0.5), ("mean", 10, 3, 2, 0.5),
 ])
 def test_rolling_primitive_vs_pandas(cuda, stat, window, minp, shift, q):
     from binquant_amd import engine
@@ -69,9 +72,11 @@ def test_rolling_primitive_vs_pandas(cuda, stat, window, minp, shift, q):
     got = engine.rolling(torch.from_numpy(x).cuda(), window, stat, q=q, min_periods=minp, shift=shift).cpu().numpy()
     for s in range(S):
         r = pd.Series(x[s]).shift(shift).rolling(window, min_periods=minp)
-        want = {"median": r.median, "mean": r.mean, "sum": r.sum, "max": r.max, "min": r.min}.get(
-            stat, lambda: r.quantile(q))()
-        np.testing.assert_allclose(got[s], want.to_numpy(), rtol=1e-12, atol=1e-12, equal_nan=True,
+        want = {"median": r.median, "mean": r.mean, "sum": r.sum, "max": r.max, "min": r.min,
+                "var": r.var, "std": r.std}.get(stat, lambda: r.quantile(q))()
+        # var/std: pandas' Welford update vs the kernel's shifted sums -> last-bit noise
+        rtol = 1e-10 if stat in ("var", "std") else 1e-12
+        np.testing.assert_allclose(got[s], want.to_numpy(), rtol=rtol, atol=1e-12, equal_nan=True,
                                    err_msg=f"{stat} row {s}")
 
 
@@ -88,3 +93,126 @@ def test_ewm_primitive_is_pandas_bitwise(cuda, alpha, minp):
     for s in range(4):
         want = pd.Series(x[s]).ewm(alpha=alpha, adjust=False, min_periods=minp).mean().to_numpy()
         np.testing.assert_array_equal(got[s], want)
+
+
+@pytest.mark.parametrize("stat,window,minp", [("sum", 3, 3), ("sum", 2, 2), ("mean", 10, 10), ("std", 10, 10),
+                                              ("var", 12, 3)])
+def test_rolling_signed_series_vs_pandas(cuda, stat, window, minp):
+    """Signed inputs (price changes) exercise the mean sign clamps and the
+    compensated sums."""
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(window)
+    x = rng.normal(0, 0.01, (6, 2000))
+    x[0, :] = np.abs(x[0, :])
+    x[1, :] = -np.abs(x[1, :])
+    x[2, 40:44] = np.nan
+    x[3, 600:900] = -0.0125
+    x[4, 1000:1300] = 0.0
+    got = engine.rolling(torch.from_numpy(x).cuda(), window, stat, min_periods=minp).cpu().numpy()
+    for s in range(6):
+        r = pd.Series(x[s]).rolling(window, min_periods=minp)
+        want = getattr(r, stat)().to_numpy()
+        np.testing.assert_allclose(got[s], want, rtol=1e-10, atol=1e-15, equal_nan=True, err_msg=f"{stat} {s}")
+
+
+def test_row_quantile_is_numpy_bitwise(cuda):
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(11)
+    T = 3000
+    x = rng.lognormal(0, 1, (10, T))
+    x[1] = rng.normal(0, 1, T)                    # negatives
+    x[2] = np.round(rng.normal(0, 3, T))          # heavy ties
+    x[3, :] = np.nan                              # empty row
+    x[4, :] = np.nan
+    x[4, 17] = 2.5                                # single observation
+    x[5, :] = np.nan
+    x[5, [3, 900]] = [4.0, -1.0]                  # two observations
+    x[6, ::3] = np.nan                            # ragged NaNs
+    x[7, :] = 7.0                                 # constant
+    x[8, :11] = np.nan                            # leading NaNs (rolling warm-up)
+    x[9] = -x[9]
+    xt = torch.from_numpy(x).cuda()
+    for q in (0.0, 0.25, 0.5, 0.75, 0.85, 0.97, 1.0, 0.333):
+        got = engine.row_quantile(xt, q).cpu().numpy()
+        for s in range(10):
+            v = x[s][~np.isnan(x[s])]
+            want = np.quantile(v, q) if v.size else np.nan
+            np.testing.assert_array_equal(got[s], want, err_msg=f"q={q} row {s}")
+
+
+def test_row_quantile_large_rows(cuda):
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(12)
+    x = rng.lognormal(0, 2, (64, 20000))
+    x[rng.random(x.shape) < 0.01] = np.nan
+    got = engine.row_quantile(torch.from_numpy(x).cuda(), 0.97).cpu().numpy()
+    want = np.array([np.quantile(r[~np.isnan(r)], 0.97) for r in x])
+    np.testing.assert_array_equal(got, want)
+
+
+def _cooldown_loop(label, bars):
+    """strategies/failed_spike_fade.py:504-518 over one row."""
+    kept, sup = label.copy(), np.zeros_like(label)
+    last = None
+    for i in range(label.size):
+        if kept[i] == 1:
+            if last is not None and (i - last) <= bars:
+                sup[i] = 1
+                kept[i] = 0
+            else:
+                last = i
+    return kept, sup
+
+
+@pytest.mark.parametrize("bars", [0, 1, 8, 30])
+def test_cooldown_matches_reference_loop(cuda, bars):
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(bars)
+    lab = rng.random((300, 700)) < 0.15
+    lab[0] = True
+    lab[1] = False
+    kept, sup = engine.cooldown(torch.from_numpy(lab).cuda(), bars)
+    kept, sup = kept.cpu().numpy(), sup.cpu().numpy()
+    for s in range(lab.shape[0]):
+        k, u = _cooldown_loop(lab[s].astype(int), bars)
+        np.testing.assert_array_equal(kept[s], k.astype(bool), err_msg=f"row {s}")
+        np.testing.assert_array_equal(sup[s], u.astype(bool), err_msg=f"row {s}")
+
+
+@pytest.mark.parametrize("case", ["fsf_a", "fsf_b", "fsf_c"])
+def test_failed_spike_matches_reference(cuda, case):
+    from binquant_amd.strategies import failed_spike_features
+
+    z = np.load(G / "failed_spike.npz")
+    col = lambda k: torch.from_numpy(z[f"{case}__{k}"])[None].cuda()  # noqa: E731
+    out = failed_spike_features(col("open"), col("high"), col("low"), col("close"), col("volume"),
+                                col("quote_asset_volume"))
+    vcmr, pbbt = z[f"{case}__calibrated"]
+    np.testing.assert_allclose(out.pop("volume_cluster_min_ratio").item(), vcmr, rtol=1e-12)
+    np.testing.assert_allclose(out.pop("price_break_base_threshold").item(), pbbt, rtol=1e-12)
+    golden = {k.split("__", 1)[1] for k in z.files if k.startswith(case + "__")} - {"calibrated"}
+    inputs = {"open", "high", "low", "close", "volume", "quote_asset_volume"}
+    assert golden - inputs == set(out), sorted((golden - inputs) ^ set(out))
+    for k, v in out.items():
+        _cmp(v, z[f"{case}__{k}"], f"{case}.{k}")
+    assert z[f"{case}__label"].sum() > 0
+
+
+def test_failed_spike_panel_equals_rows(cuda):
+    """Batched [S, T] evaluation equals per-symbol evaluation (no cross-row
+    leakage in the per-row calibration, cooldown or rolling kernels)."""
+    from binquant_amd.strategies import failed_spike_features
+
+    z = np.load(G / "failed_spike.npz")
+    cols = ["open", "high", "low", "close", "volume", "quote_asset_volume"]
+    panel = [torch.from_numpy(np.stack([z[f"fsf_a__{k}"], z[f"fsf_b__{k}"]])).cuda() for k in cols]
+    both = failed_spike_features(*panel)
+    for r, case in enumerate(["fsf_a", "fsf_b"]):
+        one = failed_spike_features(*[torch.from_numpy(z[f"{case}__{k}"])[None].cuda() for k in cols])
+        for k, v in one.items():
+            a, b = both[k][r].cpu().numpy(), v[0].cpu().numpy() if v.dim() == 2 else v.cpu().numpy()[0]
+            np.testing.assert_array_equal(a, b, err_msg=f"{case}.{k}")
