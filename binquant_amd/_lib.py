@@ -56,7 +56,7 @@ PARTIAL_COLUMNS = (
 )
 MAX_WINDOW = 126
 MAX_ROLLING_WINDOW = 96
-ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5}
+ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
 
 
 class BqParams(ctypes.Structure):

@@ -216,15 +216,16 @@ __global__ __launch_bounds__(RW_LANES) void rolling_kernel(const RollArgs A) {
       else if (neg == n && r > 0.0) r = 0.0;
     } else if (A.mode == BQ_ROLL_SUM) {
       r = run >= n ? last * (double)n : sum;   // same-value rule
-    } else {   // var / std, ddof = 1 (pandas calc_var)
+    } else {   // var / std (pandas calc_var), ddof 1 or 0
+      const int ddof = (A.mode == BQ_ROLL_VAR || A.mode == BQ_ROLL_STD) ? 1 : 0;
       double var;
-      if (n < 2) var = qnan();
-      else if (run >= n) var = 0.0;
+      if (n <= ddof) var = qnan();
+      else if (n == 1 || run >= n) var = 0.0;
       else {
-        var = ssq / (double)(n - 1);
+        var = ssq / (double)(n - ddof);
         var = var < 0.0 ? 0.0 : var;
       }
-      r = A.mode == BQ_ROLL_VAR ? var : sqrt(var);
+      r = (A.mode == BQ_ROLL_VAR || A.mode == BQ_ROLL_VAR0) ? var : sqrt(var);
     }
     out[t] = r;
   }
@@ -270,7 +271,7 @@ int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t win
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream) {
   using namespace bq;
   if (!x || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || window < 1 || window > RW_MAXW ||
-      min_periods < 0 || shift < 0 || mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD || !(q >= 0.0 && q <= 1.0) ||
+      min_periods < 0 || shift < 0 || mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0 || !(q >= 0.0 && q <= 1.0) ||
       T > 0x7fffffff)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;

@@ -194,7 +194,9 @@ int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_
 enum bq_roll_mode {
   BQ_ROLL_QUANTILE = 0, BQ_ROLL_MEDIAN = 1, BQ_ROLL_MEAN = 2, BQ_ROLL_SUM = 3,
   BQ_ROLL_VAR = 4,   /* ddof 1 */
-  BQ_ROLL_STD = 5    /* ddof 1 */
+  BQ_ROLL_STD = 5,   /* ddof 1 */
+  BQ_ROLL_VAR0 = 6,  /* ddof 0 */
+  BQ_ROLL_STD0 = 7   /* ddof 0 */
 };
 /*
  * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,

@@ -23,6 +23,9 @@ Fixtures:
   activity_burst.npz    ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)
   liquidation_sweep.npz LiquidationSweepPump.compute_pump_score (strategies/liquidation_sweep_pump.py:195-269)
   failed_spike.npz      FailedSpikeFade.detect (strategies/failed_spike_fade.py:258-544)
+  signal_helpers.npz    a20 helpers: MeanReversionFade._rsi/_trend_score,
+                        RangeBbRsiMeanReversion._compute_adx/_compute_zscore,
+                        TopGainerEarlyMomentum._features on every prefix
   beta_corr.npz         ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:154-194)
                         on every prefix (last-row value), BTC pct_change(96) (:427-430).
                         round_numbers is stubbed to identity: values are unrounded.
@@ -367,6 +370,58 @@ def child(out_dir: Path) -> None:
             out[f"{k}__{col}"] = res[col].to_numpy(dtype=float)
         out[f"{k}__calibrated"] = np.array([fsf.volume_cluster_min_ratio, fsf.price_break_base_threshold])
     np.savez(out_dir / "failed_spike.npz", **out)
+
+    # ---- 8. inline signal helpers --------------------------------
+    #   MeanReversionFade._rsi / _trend_score (strategies/mean_reversion_fade.py:88-155),
+    #   RangeBbRsiMeanReversion._compute_adx / _compute_zscore
+    #   (strategies/range_bb_rsi_mean_reversion.py:101-138),
+    #   TopGainerEarlyMomentum._features (strategies/top_gainer_early_momentum.py:92-160),
+    #   evaluated on every prefix df.iloc[:k] (they read the last row only).
+    from strategies.mean_reversion_fade import MeanReversionFade
+    from strategies.range_bb_rsi_mean_reversion import RangeBbRsiMeanReversion
+    from strategies.top_gainer_early_momentum import TopGainerEarlyMomentum
+
+    out = {}
+    tg_keys = ["close", "open", "high", "low", "volume", "quote_volume", "previous_high", "return_1h", "return_2h",
+               "return_6h", "extension_return", "extension_window_bars", "extension_cap", "candle_return",
+               "volume_ratio", "quote_volume_ratio", "range_position", "upper_wick_fraction", "ema20", "ema50", "atr"]
+    statuses = []
+    for k, (n, seed, quote) in {"sig_a": (260, 81, True), "sig_b": (180, 82, False), "sig_c": (130, 83, True)}.items():
+        o, h, l, c, v = walk(n, seed=seed, vol=0.008)
+        c = c.copy()
+        if k == "sig_a":
+            c[60:80] = c[59] * np.cumprod(np.full(20, 1.01))   # monotonic rally: RSI -> 100
+            c[120:150] = c[119]                                # flat: RSI neutral 50, std 0
+        o = np.r_[c[0], c[:-1]]
+        h = np.maximum(np.maximum(o, c), h)
+        l = np.minimum(np.minimum(o, c), l)
+        if k == "sig_a":
+            h[120:150] = l[120:150] = c[120:150]
+        df = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v,
+                           "open_time": 1_700_000_000_000 + 900_000 * np.arange(n)})
+        if quote:
+            df["quote_asset_volume"] = v * c
+        for col in df.columns:
+            out[f"{k}__{col}"] = df[col].to_numpy(dtype=float)
+        out[f"{k}__rsi"] = MeanReversionFade._rsi(df["close"]).to_numpy(dtype=float)
+        out[f"{k}__trend_score"] = np.array([MeanReversionFade._trend_score(df["close"].iloc[:j])
+                                             for j in range(1, n + 1)])
+        out[f"{k}__adx"] = np.array([RangeBbRsiMeanReversion._compute_adx(df.iloc[:j], 14)
+                                     for j in range(1, n + 1)])
+        out[f"{k}__zscore"] = np.array([RangeBbRsiMeanReversion._compute_zscore(df.iloc[:j], 20)
+                                        for j in range(1, n + 1)])
+        tg = np.full((n, len(tg_keys)), np.nan)
+        st = []
+        for j in range(1, n + 1):
+            vals, status = TopGainerEarlyMomentum._features(df.iloc[:j])
+            st.append(status)
+            if vals is not None:
+                tg[j - 1] = [vals[key] for key in tg_keys]
+        out[f"{k}__topgainer"] = tg
+        statuses.append(st)
+        out[f"{k}__topgainer_status"] = np.array(st)
+    out["topgainer_keys"] = np.array(tg_keys)
+    np.savez(out_dir / "signal_helpers.npz", **out)
     print("golden fixtures written to", out_dir)
 
 
@@ -383,6 +438,7 @@ def main() -> None:
         env["PYTHONPATH"] = f"{shim}:{REFERENCE}"
         env["PYTHONDONTWRITEBYTECODE"] = "1"
         env["ENV"] = "ci"
+        env["PYTHONHASHSEED"] = "0"   # the accumulator iterates symbol sets: fixed order, stable last bits
         subprocess.run([sys.executable, __file__, "--child", str(HERE)], check=True, env=env, cwd=tmp)
 
 
