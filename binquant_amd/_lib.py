@@ -55,6 +55,8 @@ PARTIAL_COLUMNS = (
     "reserved",
 )
 MAX_WINDOW = 126
+MAX_RESAMPLE_FIELDS = 12
+AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
 
@@ -109,6 +111,12 @@ SIGNATURES: dict[str, tuple] = {
     "bq_ewm": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _I32, _P, _I64, _P]),
     "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
+    "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
+    "bq_resample_count": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P]),
+    "bq_resample": (ctypes.c_int, [_P, _PP, _P, _I32, _P, _I64, _I64, _I64, _I64, _P, _PP, _I64, _P]),
+    "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),
+    "bq_join_returns": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    "bq_beta_corr_pairs": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
 }
 
 

@@ -29,8 +29,8 @@ constexpr int BC_H = 128;
 constexpr int BC_R = BC_H + BC_TT;
 
 struct BetaArgs {
-  const double* close;
-  const double* btc;
+  const double* close;   // PAIRS: symbol returns
+  const double* btc;     // PAIRS: benchmark returns, same row stride
   double* beta;
   double* corr;
   int64_t ld_in, ld_out;
@@ -41,12 +41,16 @@ struct BetaArgs {
 __device__ __forceinline__ double log_return(double c, double p) { return log(c / p); }
 
 
+// PAIRS = false: close / btc prices, returns formed here (first return NaN,
+// first full window at t = w). PAIRS = true: rows of dropna'd return pairs
+// (bq_join_returns), first full window at t = w - 1.
+template <bool PAIRS>
 __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
   __shared__ double sX[BC_R], sY[BC_R];
   const int tid = threadIdx.x;
   const int64_t sym = blockIdx.x;
   const double* __restrict__ rc = A.close + sym * A.ld_in;
-  const double* __restrict__ rb = A.btc;
+  const double* __restrict__ rb = PAIRS ? A.btc + sym * A.ld_in : A.btc;
   const int T = A.T, w = A.win;
   if (tid < BC_H) {
     sX[tid] = qnan();
@@ -63,8 +67,13 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
       for (int k = 0; k < BC_K; ++k) {
         const bool ok = tb + k < T;
         const double c = ok ? rc[tb + k] : qnan(), b = ok ? rb[tb + k] : qnan();
-        x[k] = log_return(c, pc);   // NaN at candle 0 (dropna)
-        y[k] = log_return(b, pbt);
+        if (PAIRS) {
+          x[k] = c;
+          y[k] = b;
+        } else {
+          x[k] = log_return(c, pc);   // NaN at candle 0 (dropna)
+          y[k] = log_return(b, pbt);
+        }
         sX[pb + k] = x[k];
         sY[pb + k] = y[k];
         pc = c;
@@ -113,7 +122,7 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
           add(x[k], y[k], 1.0);
           track(x[k], y[k]);
         }
-        if (t < w || t >= T) {
+        if (t < w - (PAIRS ? 1 : 0) || t >= T) {
           beta[k] = corr[k] = qnan();
           continue;
         }
@@ -152,8 +161,9 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
 
 }  // namespace bq
 
-extern "C" int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_t T, int64_t ld_in,
-                            int32_t window, double* beta, double* corr, int64_t ld_out, void* stream) {
+namespace {
+int launch_beta(bool pairs, const double* close, const double* btc_close, int64_t S, int64_t T, int64_t ld_in,
+                int32_t window, double* beta, double* corr, int64_t ld_out, void* stream) {
   using namespace bq;
   if (!close || !btc_close || S < 0 || T < 0 || ld_in < T || ld_out < T || window < 2 ||
       window > BQ_MAX_WINDOW || T > 0x7fffffff || S > 0x7fffffff)
@@ -171,6 +181,18 @@ extern "C" int bq_beta_corr(const double* close, const double* btc_close, int64_
   A.inv_w = 1.0 / (double)window;
   A.inv_w1 = 1.0 / (double)(window - 1);
   A.bias = (double)window / (double)(window - 1);
-  hipLaunchKernelGGL(beta_corr_kernel, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
+  if (pairs) hipLaunchKernelGGL(beta_corr_kernel<true>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
+  else hipLaunchKernelGGL(beta_corr_kernel<false>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+}  // namespace
+
+extern "C" int bq_beta_corr(const double* close, const double* btc_close, int64_t S, int64_t T, int64_t ld_in,
+                            int32_t window, double* beta, double* corr, int64_t ld_out, void* stream) {
+  return launch_beta(false, close, btc_close, S, T, ld_in, window, beta, corr, ld_out, stream);
+}
+
+extern "C" int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in,
+                                  int32_t window, double* beta, double* corr, int64_t ld_out, void* stream) {
+  return launch_beta(true, x, y, S, T, ld_in, window, beta, corr, ld_out, stream);
 }

@@ -211,6 +211,49 @@ __device__ __forceinline__ double sqrt_nr(double v) {
   return v > 0.0 ? q : 0.0;
 }
 
+// ---- lane-per-symbol staging (sequential state machines) -------------------
+// A wave owns 64 symbols and walks them in chunks of CT candles. A chunk of a
+// [S][ld] row-major array is read coalesced (lane i of pass k takes element
+// e = i + 64k: symbol e / CT, candle e % CT, so CT consecutive lanes read one
+// symbol's contiguous CT * 8 bytes) and transposed through LDS as [CT][PITCH]
+// so that lane l then walks symbol l. PITCH = 64 + 2 keeps both the transposed
+// writes and the per-lane reads free of bank conflicts for 8-byte elements.
+constexpr int STG_PITCH = WAVE + 2;
+
+template <int CT>
+__device__ __forceinline__ void stage_load(const double* __restrict__ base, int64_t ld, int64_t sym0, int64_t S,
+                                           int t0, int T, int lane, double (&r)[CT]) {
+#pragma unroll
+  for (int k = 0; k < CT; ++k) {
+    const int e = lane + WAVE * k;
+    const int64_t s = sym0 + e / CT;
+    const int t = t0 + e % CT;
+    r[k] = (s < S && t < T) ? base[s * ld + t] : qnan();
+  }
+}
+
+template <int CT>
+__device__ __forceinline__ void stage_put(double* lds, int lane, const double (&r)[CT]) {
+#pragma unroll
+  for (int k = 0; k < CT; ++k) {
+    const int e = lane + WAVE * k;
+    lds[(e % CT) * STG_PITCH + e / CT] = r[k];
+  }
+}
+
+// LDS [CT][PITCH] (written by lane = symbol) -> [S][ld] rows, coalesced.
+template <int CT, typename OutT>
+__device__ __forceinline__ void stage_store(const double* lds, OutT* __restrict__ base, int64_t ld, int64_t sym0,
+                                            int64_t S, int t0, int T, int lane) {
+#pragma unroll
+  for (int k = 0; k < CT; ++k) {
+    const int e = lane + WAVE * k;
+    const int64_t s = sym0 + e / CT;
+    const int t = t0 + e % CT;
+    if (s < S && t < T) base[s * ld + t] = (OutT)lds[(e % CT) * STG_PITCH + e / CT];
+  }
+}
+
 // shared/utils.py:20-23
 __device__ __forceinline__ double safe_pct(double cur, double prev) {
   if (prev == 0.0) return 0.0;

@@ -45,6 +45,9 @@ namespace bq {
 #ifndef BQ_EN_K
 #define BQ_EN_K 4      // consecutive candles per lane
 #endif
+#ifndef BQ_EN_NTSTORE
+#define BQ_EN_NTSTORE 1   // non-temporal output stores
+#endif
 #ifndef BQ_EN_WPS
 #define BQ_EN_WPS 3    // __launch_bounds__ min waves per SIMD
 #endif
@@ -149,7 +152,13 @@ __device__ __forceinline__ void store4(double* __restrict__ row_, int tb, int T,
   if (vec && tb + EN_K <= T) {
     gdbl2* p = reinterpret_cast<gdbl2*>(row + tb);
 #pragma unroll
-    for (int j = 0; j < EN_K / 2; ++j) __builtin_nontemporal_store(dbl2{x[2 * j], x[2 * j + 1]}, p + j);
+    for (int j = 0; j < EN_K / 2; ++j) {
+#if BQ_EN_NTSTORE
+      __builtin_nontemporal_store(dbl2{x[2 * j], x[2 * j + 1]}, p + j);
+#else
+      p[j] = dbl2{x[2 * j], x[2 * j + 1]};
+#endif
+    }
   } else {
 #pragma unroll
     for (int k = 0; k < EN_K; ++k)

@@ -1,0 +1,298 @@
+// Frame plumbing on the device: time-bucket resampling and timestamp joins of
+// ragged [S][ld] kline panels.
+//
+//   bq_resample_count / bq_resample: Candles.resample(df, interval="1h")
+//     (producers/context_evaluator.py:403-407; pybinbot, absent) restated as
+//     pandas' df.resample(interval).agg({...}) on the open_time
+//     DatetimeIndex: bins [origin + b*I, origin + (b+1)*I) with origin =
+//     midnight of the first candle's day (pandas origin="start_day",
+//     closed/label left), from the first candle's bin to the last candle's;
+//     per field FIRST/LAST (first/last non-NaN), MAX/MIN (NaN skipped), SUM
+//     (pandas group_sum: Kahan-compensated, NaN skipped, 0 for an empty bin).
+//     Empty bins give NaN (FIRST/LAST/MAX/MIN) and 0 (SUM), as pandas does.
+//   bq_align: LiquidationSweepPump's left merge of the benchmark on open_time
+//     (strategies/liquidation_sweep_pump.py:255-263: drop_duplicates(keep
+//     "last"), merge how="left") -> the benchmark value at each candle's
+//     timestamp, NaN where the benchmark has no candle.
+//   bq_join_returns: the inner join of ContextEvaluator.dynamic_btc_beta_corr
+//     (producers/context_evaluator.py:161-177): log returns of each frame on
+//     its own rows, inner-joined on the timestamp and dropna'd, compacted per
+//     symbol row (pairs feed bq_beta_corr_pairs).
+//
+// Timestamps are int64 ms, ascending within a row; lens[s] is the valid
+// length of row s (NULL: every row has T candles).
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+namespace bq {
+
+constexpr int64_t DAY_MS = 86400000;
+
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
+  const int64_t q = a / b;
+  return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// first index i in [0, n) with ts[i] >= key (n if none)
+__device__ __forceinline__ int lower_bound_i64(const int64_t* __restrict__ ts, int n, int64_t key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (ts[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int row_len(const int64_t* lens, int64_t s, int T) {
+  if (!lens) return T;
+  const int64_t n = lens[s];
+  return n < 0 ? 0 : (n > T ? T : (int)n);
+}
+
+// origin (pandas start_day) and the first bin index of a row
+__device__ __forceinline__ void row_bins(const int64_t* ts, int n, int64_t I, int64_t& origin, int64_t& b0,
+                                         int64_t& nb) {
+  if (n == 0) {
+    origin = b0 = nb = 0;
+    return;
+  }
+  origin = floor_div(ts[0], DAY_MS) * DAY_MS;
+  b0 = floor_div(ts[0] - origin, I);
+  nb = floor_div(ts[n - 1] - origin, I) - b0 + 1;
+}
+
+__global__ void resample_count_kernel(const int64_t* __restrict__ ts, const int64_t* __restrict__ lens, int64_t S,
+                                      int T, int64_t ld_in, int64_t I, int64_t* __restrict__ out_lens) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  int64_t origin, b0, nb;
+  row_bins(ts + s * ld_in, row_len(lens, s, T), I, origin, b0, nb);
+  out_lens[s] = nb;
+}
+
+struct ResampleArgs {
+  const int64_t* ts;
+  const int64_t* lens;
+  const double* in[BQ_MAX_RESAMPLE_FIELDS];
+  double* out[BQ_MAX_RESAMPLE_FIELDS];
+  int32_t agg[BQ_MAX_RESAMPLE_FIELDS];
+  int64_t* out_ts;
+  int64_t S, ld_in, ld_out, I;
+  int T, nf;
+};
+
+// one thread per (symbol, output bin); consecutive threads take consecutive
+// bins of a row, so the candles a wave reads are contiguous
+__global__ __launch_bounds__(256) void resample_kernel(const ResampleArgs A) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= A.S * A.ld_out) return;
+  const int64_t s = i / A.ld_out;
+  const int64_t b = i % A.ld_out;
+  const int64_t* __restrict__ ts = A.ts + s * A.ld_in;
+  const int n = row_len(A.lens, s, A.T);
+  int64_t origin, b0, nb;
+  row_bins(ts, n, A.I, origin, b0, nb);
+  if (b >= nb) return;
+  const int64_t key = origin + (b0 + b) * A.I;
+  const int lo = lower_bound_i64(ts, n, key);
+  const int hi = lower_bound_i64(ts, n, key + A.I);
+  if (A.out_ts) A.out_ts[s * A.ld_out + b] = key;
+  for (int f = 0; f < A.nf; ++f) {
+    const double* __restrict__ x = A.in[f] + s * A.ld_in;
+    double r;
+    switch (A.agg[f]) {
+      case BQ_AGG_FIRST: {
+        r = qnan();
+        for (int j = lo; j < hi; ++j)
+          if (x[j] == x[j]) {
+            r = x[j];
+            break;
+          }
+        break;
+      }
+      case BQ_AGG_LAST: {
+        r = qnan();
+        for (int j = hi - 1; j >= lo; --j)
+          if (x[j] == x[j]) {
+            r = x[j];
+            break;
+          }
+        break;
+      }
+      case BQ_AGG_MAX:
+      case BQ_AGG_MIN: {
+        r = qnan();
+        const bool mx = A.agg[f] == BQ_AGG_MAX;
+        for (int j = lo; j < hi; ++j) {
+          const double v = x[j];
+          if (v != v) continue;
+          if (r != r || (mx ? v > r : v < r)) r = v;
+        }
+        break;
+      }
+      default: {   // BQ_AGG_SUM: pandas group_sum (Kahan)
+        double sum = 0.0, comp = 0.0;
+        for (int j = lo; j < hi; ++j) {
+          const double v = x[j];
+          if (v != v) continue;
+          const double y = v - comp;
+          const double t = sum + y;
+          comp = t - sum - y;
+          if (comp != comp) comp = 0.0;
+          sum = t;
+        }
+        r = sum;
+      }
+    }
+    A.out[f][s * A.ld_out + b] = r;
+  }
+}
+
+// last j with bts[j] == key (keep="last"), -1 if none
+__device__ __forceinline__ int match_last(const int64_t* __restrict__ bts, int nb, int64_t key) {
+  const int j = lower_bound_i64(bts, nb, key + 1) - 1;
+  return (j >= 0 && bts[j] == key) ? j : -1;
+}
+
+__global__ __launch_bounds__(256) void align_kernel(const int64_t* __restrict__ ts, const int64_t* __restrict__ lens,
+                                                    int64_t S, int T, int64_t ld_in, const int64_t* __restrict__ bts,
+                                                    const double* __restrict__ bval, int nb, double* __restrict__ out,
+                                                    int64_t ld_out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= S * (int64_t)T) return;
+  const int64_t s = i / T;
+  const int t = (int)(i % T);
+  double r = qnan();
+  if (t < row_len(lens, s, T)) {
+    const int j = match_last(bts, nb, ts[s * ld_in + t]);
+    if (j >= 0) r = bval[j];
+  }
+  out[s * ld_out + t] = r;
+}
+
+// One workgroup per symbol row: keep flag per candle, block-wide exclusive
+// scan (wave ballots + LDS wave offsets), scatter the kept pairs in order.
+constexpr int JR_NT = 256;
+
+__global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __restrict__ ts,
+                                                             const double* __restrict__ close,
+                                                             const int64_t* __restrict__ lens, int T, int64_t ld_in,
+                                                             const int64_t* __restrict__ bts,
+                                                             const double* __restrict__ bclose, int nb,
+                                                             double* __restrict__ x, double* __restrict__ y,
+                                                             int64_t ld_out, int64_t* __restrict__ out_lens) {
+  __shared__ int sWave[JR_NT / WAVE];
+  __shared__ int sBase;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const int64_t s = blockIdx.x;
+  const int64_t* __restrict__ rts = ts + s * ld_in;
+  const double* __restrict__ rc = close + s * ld_in;
+  const int n = row_len(lens, s, T);
+  if (tid == 0) sBase = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < n; t0 += JR_NT) {
+    const int t = t0 + tid;
+    double xa = qnan(), yb = qnan();
+    if (t < n && t > 0) {
+      xa = log(rc[t] / rc[t - 1]);   // the frame's own previous row
+      const int j = match_last(bts, nb, rts[t]);
+      if (j > 0) yb = log(bclose[j] / bclose[j - 1]);
+    }
+    const bool keep = xa == xa && yb == yb;
+    const uint64_t m = __ballot(keep);
+    const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (lane == 0) sWave[w] = __popcll(m);
+    __syncthreads();
+    int off = sBase;
+    for (int k = 0; k < w; ++k) off += sWave[k];
+    if (keep) {
+      x[s * ld_out + off + before] = xa;
+      y[s * ld_out + off + before] = yb;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int k = 0; k < JR_NT / WAVE; ++k) tot += sWave[k];
+      sBase += tot;
+    }
+    __syncthreads();
+  }
+  // NaN tail so the row reads as a dropna'd series of length out_lens[s]
+  for (int t = sBase + tid; t < T; t += JR_NT) {
+    x[s * ld_out + t] = qnan();
+    y[s * ld_out + t] = qnan();
+  }
+  if (tid == 0) out_lens[s] = sBase;
+}
+
+}  // namespace bq
+
+extern "C" {
+
+int bq_resample_count(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in,
+                      int64_t interval_ms, int64_t* out_lens, void* stream) {
+  using namespace bq;
+  if (!ts || !out_lens || S < 0 || T < 0 || ld_in < T || interval_ms <= 0 || T > 0x7fffffff) return BQ_EINVAL;
+  if (S == 0) return BQ_OK;
+  hipLaunchKernelGGL(resample_count_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ts,
+                     lens, S, (int)T, ld_in, interval_ms, out_lens);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
+                double* const* out_fields, int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!ts || S < 0 || T < 0 || ld_in < T || ld_out < 0 || interval_ms <= 0 || nfields < 0 ||
+      nfields > BQ_MAX_RESAMPLE_FIELDS || (nfields > 0 && (!fields || !aggs || !out_fields)) || T > 0x7fffffff)
+    return BQ_EINVAL;
+  ResampleArgs A = {};
+  for (int f = 0; f < nfields; ++f) {
+    if (!fields[f] || !out_fields[f] || aggs[f] < BQ_AGG_FIRST || aggs[f] > BQ_AGG_SUM) return BQ_EINVAL;
+    A.in[f] = fields[f];
+    A.out[f] = out_fields[f];
+    A.agg[f] = aggs[f];
+  }
+  if (S == 0 || ld_out == 0) return BQ_OK;
+  A.ts = ts;
+  A.lens = lens;
+  A.out_ts = out_ts;
+  A.S = S;
+  A.ld_in = ld_in;
+  A.ld_out = ld_out;
+  A.I = interval_ms;
+  A.T = (int)T;
+  A.nf = nfields;
+  const int64_t items = S * ld_out;
+  hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_align(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, const int64_t* bench_ts,
+             const double* bench_val, int64_t n_bench, double* out, int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!ts || !bench_ts || !bench_val || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || n_bench < 0 ||
+      T > 0x7fffffff || n_bench > 0x7fffffff)
+    return BQ_EINVAL;
+  if (S == 0 || T == 0) return BQ_OK;
+  const int64_t items = S * T;
+  hipLaunchKernelGGL(align_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream, ts, lens,
+                     S, (int)T, ld_in, bench_ts, bench_val, (int)n_bench, out, ld_out);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in,
+                    const int64_t* bench_ts, const double* bench_close, int64_t n_bench, double* x, double* y,
+                    int64_t ld_out, int64_t* out_lens, void* stream) {
+  using namespace bq;
+  if (!ts || !close || !bench_ts || !bench_close || !x || !y || !out_lens || S < 0 || T < 0 || ld_in < T ||
+      ld_out < T || n_bench < 0 || T > 0x7fffffff || n_bench > 0x7fffffff)
+    return BQ_EINVAL;
+  if (S == 0) return BQ_OK;
+  hipLaunchKernelGGL(join_returns_kernel, dim3((unsigned)S), dim3(JR_NT), 0, (hipStream_t)stream, ts, close, lens,
+                     (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+}  // extern "C"

@@ -382,3 +382,159 @@ def cooldown(label: torch.Tensor, bars: int, stream: torch.cuda.Stream | None = 
     )
     _lib.check(st, "bq_cooldown")
     return kept, sup
+
+
+def supertrend(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    period: int = 10,
+    multiplier: float = 3.0,
+    atr: torch.Tensor | None = None,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """pybinbot Indicators.set_supertrend (strategies/coinrule/coinrule.py:143-160)
+    on a [S, T] panel: {"supertrend": bool (uptrend), "supertrend_upper",
+    "supertrend_lower": final bands}. ATR = TR.rolling(period).mean() from the
+    enrich kernel unless given."""
+    high = _check_panel(high, "high")
+    S, T = high.shape
+    low = _check_panel(low, "low", (S, T))
+    close = _check_panel(close, "close", (S, T))
+    if atr is None:
+        zero = torch.zeros_like(close)
+        atr = enrich(close, high, low, close, zero, params=IndicatorParams(atr_window=int(period)),
+                     columns=("ATR",), stream=stream)["ATR"]
+    atr = _check_panel(atr, "atr", (S, T))
+    ins = [t.contiguous() for t in (high, low, close, atr)]
+    up = torch.empty((S, T), dtype=torch.bool, device=close.device)
+    upper = torch.empty((S, T), dtype=torch.float64, device=close.device)
+    lower = torch.empty_like(upper)
+    st = _lib.load().bq_supertrend(
+        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, float(multiplier), ctypes.c_void_p(up.data_ptr()),
+        ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_supertrend")
+    return {"supertrend": up, "supertrend_upper": upper, "supertrend_lower": lower}
+
+
+# ---- frame plumbing: resample / timestamp joins (bq_frame.hip) -----------------
+
+
+def _check_ts(ts: torch.Tensor, name: str = "ts") -> torch.Tensor:
+    if not isinstance(ts, torch.Tensor) or not ts.is_cuda or ts.dtype != torch.int64:
+        raise ValueError(f"{name}: expected an int64 CUDA tensor of ms timestamps (no CPU path)")
+    if ts.dim() == 1:
+        ts = ts.unsqueeze(0)
+    return ts.contiguous()
+
+
+def _check_lens(lens, S: int, device) -> torch.Tensor | None:
+    if lens is None:
+        return None
+    if not isinstance(lens, torch.Tensor):
+        lens = torch.as_tensor(lens, dtype=torch.int64)
+    lens = lens.to(device=device, dtype=torch.int64).contiguous()
+    if lens.numel() != S:
+        raise ValueError(f"lens: expected {S} entries, got {lens.numel()}")
+    return lens
+
+
+def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
+def resample(
+    ts: torch.Tensor,
+    fields: dict[str, torch.Tensor],
+    aggs: dict[str, str],
+    interval_ms: int,
+    lens=None,
+    stream: torch.cuda.Stream | None = None,
+) -> tuple[torch.Tensor, dict[str, torch.Tensor], torch.Tensor]:
+    """Candles.resample (producers/context_evaluator.py:403-407) on a ragged
+    [S, T] panel: pandas resample(interval, origin="start_day").agg(aggs) on
+    the open_time index. Returns (bin labels int64 [S, B], {field: [S, B]},
+    bins per row int64 [S]); B = the longest row's bin count."""
+    ts = _check_ts(ts)
+    S, T = ts.shape
+    names = list(fields)
+    if len(names) > _lib.MAX_RESAMPLE_FIELDS:
+        raise ValueError(f"at most {_lib.MAX_RESAMPLE_FIELDS} fields per resample call")
+    ins = [_check_panel(fields[n], n, (S, T)).contiguous() for n in names]
+    codes = []
+    for n in names:
+        a = aggs.get(n)
+        if a not in _lib.AGG_CODES:
+            raise ValueError(f"{n}: aggregation {a!r} not in {sorted(_lib.AGG_CODES)}")
+        codes.append(_lib.AGG_CODES[a])
+    lens = _check_lens(lens, S, ts.device)
+    L = _lib.load()
+    out_lens = torch.empty(S, dtype=torch.int64, device=ts.device)
+    _lib.check(L.bq_resample_count(_ptr(ts), _ptr(lens), S, T, T, int(interval_ms), _ptr(out_lens),
+                                   _stream_handle(stream)), "bq_resample_count")
+    B = int(out_lens.max().item()) if S else 0
+    out_ts = torch.empty((S, B), dtype=torch.int64, device=ts.device)
+    outs = [torch.empty((S, B), dtype=torch.float64, device=ts.device) for _ in names]
+    agg_arr = (ctypes.c_int32 * max(1, len(codes)))(*codes)
+    st = L.bq_resample(
+        _ptr(ts), _lib.ptr_array([t.data_ptr() for t in ins]), ctypes.cast(agg_arr, ctypes.c_void_p), len(names),
+        _ptr(lens), S, T, T, int(interval_ms), _ptr(out_ts), _lib.ptr_array([t.data_ptr() for t in outs]), B,
+        _stream_handle(stream),
+    )
+    _lib.check(st, "bq_resample")
+    return out_ts, dict(zip(names, outs)), out_lens
+
+
+def align(ts: torch.Tensor, bench_ts: torch.Tensor, bench_val: torch.Tensor, lens=None,
+          stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Benchmark value at each candle's timestamp (left merge on open_time,
+    duplicates keep "last"; strategies/liquidation_sweep_pump.py:255-263),
+    NaN where the benchmark has no candle. ts [S, T] int64, bench_ts [Tb]
+    ascending, bench_val [Tb] float64."""
+    ts = _check_ts(ts)
+    S, T = ts.shape
+    bts = _check_ts(bench_ts, "bench_ts").reshape(-1)
+    bval = _check_panel(bench_val.reshape(1, -1), "bench_val", (1, bts.numel())).contiguous()
+    lens = _check_lens(lens, S, ts.device)
+    out = torch.empty((S, T), dtype=torch.float64, device=ts.device)
+    st = _lib.load().bq_align(_ptr(ts), _ptr(lens), S, T, T, _ptr(bts), _ptr(bval), bts.numel(), _ptr(out), T,
+                              _stream_handle(stream))
+    _lib.check(st, "bq_align")
+    return out
+
+
+def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
+                 lens=None, stream: torch.cuda.Stream | None = None):
+    """Aligned (symbol, benchmark) log-return pairs of
+    ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:161-177):
+    returns on each frame's own rows, inner join on the timestamp, dropna,
+    compacted per row. Returns (x [S, T], y [S, T], pairs per row int64 [S])."""
+    ts = _check_ts(ts)
+    S, T = ts.shape
+    close = _check_panel(close, "close", (S, T)).contiguous()
+    bts = _check_ts(bench_ts, "bench_ts").reshape(-1)
+    bc = _check_panel(bench_close.reshape(1, -1), "bench_close", (1, bts.numel())).contiguous()
+    lens = _check_lens(lens, S, ts.device)
+    x = torch.empty((S, T), dtype=torch.float64, device=ts.device)
+    y = torch.empty_like(x)
+    n = torch.empty(S, dtype=torch.int64, device=ts.device)
+    st = _lib.load().bq_join_returns(_ptr(ts), _ptr(close), _ptr(lens), S, T, T, _ptr(bts), _ptr(bc), bts.numel(),
+                                     _ptr(x), _ptr(y), T, _ptr(n), _stream_handle(stream))
+    _lib.check(st, "bq_join_returns")
+    return x, y, n
+
+
+def beta_corr_pairs(x: torch.Tensor, y: torch.Tensor, window: int = 50,
+                    stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
+    """Rolling beta / corr over aligned return pairs (join_returns output):
+    NaN for rows < window - 1."""
+    x = _check_panel(x, "x").contiguous()
+    S, T = x.shape
+    y = _check_panel(y, "y", (S, T)).contiguous()
+    beta = torch.empty((S, T), dtype=torch.float64, device=x.device)
+    corr = torch.empty_like(beta)
+    st = _lib.load().bq_beta_corr_pairs(_ptr(x), _ptr(y), S, T, T, int(window), _ptr(beta), _ptr(corr), T,
+                                        _stream_handle(stream))
+    _lib.check(st, "bq_beta_corr_pairs")
+    return {"beta": beta, "corr": corr}

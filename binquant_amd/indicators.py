@@ -10,6 +10,7 @@ strategies/coinrule/price_tracker.py:185):
     df = Indicators.bollinguer_spreads(df)       # "bb_upper", "bb_mid", "bb_lower"
     df = Indicators.set_twap(df)                 # "twap"
     df = Indicators.atr(df=df, window=14)        # "ATR"
+    df = Indicators.set_supertrend(df, 3.0)      # "supertrend" (+ final bands)
     value = Indicators.mfi(df, window=14)        # float of the last candle
 
 Each call returns the frame with the columns added (callers rebind, as in the
@@ -139,6 +140,20 @@ class Indicators:
         return float(_run(df, p, ("mfi",))["mfi"][-1])
 
     @staticmethod
+    def set_supertrend(df: pd.DataFrame, multiplier: float = 3.0, period: int = 10) -> pd.DataFrame:
+        """Adds "supertrend" (bool: uptrend) and the final bands
+        "supertrend_upper" / "supertrend_lower" (coinrule.py:143-160 reads
+        bool(df["supertrend"].iloc[-1]))."""
+        period = _check_window(period, "set_supertrend")
+        host = _frame_inputs(df)
+        dev = _device()
+        h, l, c = (torch.from_numpy(np.ascontiguousarray(x)).to(dev)[None, :] for x in host[1:4])
+        r = engine.supertrend(h, l, c, period=period, multiplier=float(multiplier))
+        for k, v in r.items():
+            df[k] = v[0].cpu().numpy()
+        return df
+
+    @staticmethod
     def batch(panel: Mapping[str, np.ndarray | torch.Tensor], params: engine.IndicatorParams | None = None,
               columns=ENRICH_COLUMNS) -> dict[str, torch.Tensor]:
         """[S, T] panel (numpy or device tensors) -> {column: [S, T] device tensor}."""
@@ -215,6 +230,49 @@ def dynamic_btc_beta_corr(df: pd.DataFrame, df_btc: pd.DataFrame, window: int = 
     if decimals is not None:
         beta, corr = round(beta, decimals), round(corr, decimals)
     return beta, corr
+
+
+def dynamic_btc_beta_corr_frames(frames: Sequence[pd.DataFrame], df_btc: pd.DataFrame, window: int = 50,
+                                 decimals: int | None = 6, key: str = "open_time") -> list[tuple[float, float]]:
+    """Batched dynamic_btc_beta_corr for many symbols' frames against one
+    benchmark frame, joined on the `key` timestamp column (the frames' time
+    index): per-frame log returns, inner join, dropna (bq_join_returns), then
+    rolling(window) beta/corr at each symbol's last joined row
+    (bq_beta_corr_pairs). (0, 0) below `window` joined returns; NaN -> 0."""
+    if not frames:
+        return []
+    dev = _device()
+    S = len(frames)
+    lens = [len(f) for f in frames]
+    T = max(1, max(lens))
+    ts = np.zeros((S, T), dtype=np.int64)
+    cl = np.full((S, T), np.nan)
+    for s, df in enumerate(frames):
+        n = lens[s]
+        if n:
+            ts[s, :n] = pd.to_numeric(df[key]).to_numpy(np.int64)
+            ts[s, n:] = ts[s, n - 1]
+            cl[s, :n] = pd.to_numeric(df["close"], errors="coerce").to_numpy(np.float64)
+    bts = torch.from_numpy(pd.to_numeric(df_btc[key]).to_numpy(np.int64)).to(dev)
+    bcl = torch.from_numpy(pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)).to(dev)
+    x, y, n = engine.join_returns(torch.from_numpy(ts).to(dev), torch.from_numpy(cl).to(dev), bts, bcl, lens=lens)
+    bc = engine.beta_corr_pairs(x, y, window=window)
+    n = n.cpu().numpy()
+    last = torch.from_numpy(np.maximum(n - 1, 0)).to(dev)
+    rows = torch.arange(S, device=dev)
+    beta = bc["beta"][rows, last].cpu().numpy()
+    corr = bc["corr"][rows, last].cpu().numpy()
+    res = []
+    for s in range(S):
+        if n[s] < window:
+            res.append((0.0, 0.0))
+            continue
+        b = 0.0 if np.isnan(beta[s]) else float(beta[s])
+        c = 0.0 if np.isnan(corr[s]) else float(corr[s])
+        if decimals is not None:
+            b, c = round(b, decimals), round(c, decimals)
+        res.append((b, c))
+    return res
 
 
 def btc_price_change(df_btc: pd.DataFrame, periods: int = 96) -> float:

@@ -29,6 +29,14 @@
  *                         evaluated at every timestamp of a [S][T] panel
  *   bq_beta_corr       <- ContextEvaluator.dynamic_btc_beta_corr
  *                         producers/context_evaluator.py:154-194
+ *   bq_supertrend      <- pybinbot Indicators.set_supertrend
+ *                         strategies/coinrule/coinrule.py:143-160
+ *   bq_resample*       <- pybinbot Candles.resample(df, "1h")
+ *                         producers/context_evaluator.py:403-407
+ *   bq_align           <- the benchmark left merge of
+ *                         strategies/liquidation_sweep_pump.py:255-263
+ *   bq_join_returns,   <- the inner join + rolling beta/corr of
+ *   bq_beta_corr_pairs    producers/context_evaluator.py:161-194
  *   bq_breadth_partial <- the per-symbol sums/counts of
  *                         LiveMarketContextAccumulator._build_context
  *                         market_regime/live_market_context_accumulator.py:135-163
@@ -238,6 +246,63 @@ int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double
  */
 int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32_t bars, uint8_t* kept,
                 uint8_t* suppressed, int64_t ld_out, void* stream);
+
+/* ---- sequential state machines (lane = symbol) ----------------------------- */
+/*
+ * Supertrend trend flag and final bands (pybinbot Indicators.set_supertrend,
+ * called at strategies/coinrule/coinrule.py:143 with multiplier 3.0, period 10;
+ * the consumer reads bool(df["supertrend"].iloc[-1]) at :160). hlca = {high,
+ * low, close, ATR} [S][ld_in] fp64 (ATR = bq_enrich's ATR column with
+ * atr_window = period). up: uint8 [S][ld_out] (1 = uptrend); upper/lower:
+ * fp64 [S][ld_out] final bands (NULL = skip). Recurrence: see bq_seq.hip.
+ */
+int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, int64_t ld_in, double multiplier,
+                  uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream);
+
+/* ---- frame plumbing: resample and timestamp joins (ragged rows) ------------ */
+/* Timestamps are int64 ms, ascending within a row; lens[s] = valid candles of
+ * row s (NULL: all T). */
+#define BQ_MAX_RESAMPLE_FIELDS 12
+enum bq_agg { BQ_AGG_FIRST = 0, BQ_AGG_LAST = 1, BQ_AGG_MAX = 2, BQ_AGG_MIN = 3, BQ_AGG_SUM = 4 };
+/*
+ * Candles.resample(df, interval="1h") (producers/context_evaluator.py:403-407,
+ * pybinbot): pandas resample(interval, origin="start_day", closed/label left)
+ * .agg(...) on the open_time index. bq_resample_count writes the number of
+ * bins of each row (first candle's bin .. last candle's bin) to out_lens[S];
+ * bq_resample fills out_ts (bin labels, NULL = skip) and out_fields
+ * [nfields][S][ld_out] (ld_out >= max out_lens) with per-field aggregation
+ * aggs[f] (bq_agg; NaN-skipping, SUM Kahan-compensated like pandas group_sum;
+ * empty bins NaN, SUM 0).
+ */
+int bq_resample_count(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in,
+                      int64_t interval_ms, int64_t* out_lens, void* stream);
+int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
+                double* const* out_fields, int64_t ld_out, void* stream);
+/*
+ * Left merge of a benchmark series on the timestamp
+ * (strategies/liquidation_sweep_pump.py:255-263, duplicates keep "last"):
+ * out[s][t] = bench_val[j] with bench_ts[j] == ts[s][t], NaN if absent.
+ * bench_ts ascending, n_bench entries.
+ */
+int bq_align(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, const int64_t* bench_ts,
+             const double* bench_val, int64_t n_bench, double* out, int64_t ld_out, void* stream);
+/*
+ * The aligned returns of ContextEvaluator.dynamic_btc_beta_corr
+ * (producers/context_evaluator.py:161-177): log(c/c.shift(1)) on each frame's
+ * own rows, inner-joined on the timestamp, dropna'd, compacted in order into
+ * x (symbol) / y (benchmark) [S][ld_out] with out_lens[s] pairs (NaN tail).
+ */
+int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in,
+                    const int64_t* bench_ts, const double* bench_close, int64_t n_bench, double* x, double* y,
+                    int64_t ld_out, int64_t* out_lens, void* stream);
+/*
+ * bq_beta_corr on already-aligned return pairs (x, y [S][ld_in], dropna'd
+ * prefix of each row): beta/corr of rolling(window) at every row, NaN for
+ * rows < window - 1.
+ */
+int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in, int32_t window,
+                       double* beta, double* corr, int64_t ld_out, void* stream);
 
 #ifdef __cplusplus
 }

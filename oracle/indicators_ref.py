@@ -232,3 +232,35 @@ def dynamic_btc_beta_corr(close, btc_close, window: int = 50) -> tuple[float, fl
         return 0.0, 0.0
     b, c = beta_corr_series(close, btc_close, window)
     return (0.0 if np.isnan(b[-1]) else float(b[-1])), (0.0 if np.isnan(c[-1]) else float(c[-1]))
+
+
+def supertrend(df: pd.DataFrame, multiplier: float = 3.0, period: int = 10) -> pd.DataFrame:
+    """pybinbot Indicators.set_supertrend(df, multiplier=3.0) as called at
+    strategies/coinrule/coinrule.py:143 ("period adjusted to 10"); the
+    consumer reads bool(df["supertrend"].iloc[-1]) (:160). pybinbot is absent:
+    this is the common band-recursion form (parity unpinned). hl2 = (h+l)/2,
+    ATR = the `atr` restatement above, bands hl2 +- m*ATR; for t >= 1 the
+    trend flips up when close > upper[t-1], down when close < lower[t-1],
+    otherwise it holds and the band on the trend's side ratchets."""
+    hl2 = (df["high"] + df["low"]) / 2
+    a = true_range(df).rolling(period).mean()
+    upper = (hl2 + (multiplier * a)).to_numpy(np.float64).copy()
+    lower = (hl2 - (multiplier * a)).to_numpy(np.float64).copy()
+    close = df["close"].to_numpy(np.float64)
+    up = np.ones(len(df), dtype=bool)
+    for t in range(1, len(df)):
+        p = t - 1
+        if close[t] > upper[p]:
+            up[t] = True
+        elif close[t] < lower[p]:
+            up[t] = False
+        else:
+            up[t] = up[p]
+            if up[t] and lower[t] < lower[p]:
+                lower[t] = lower[p]
+            if not up[t] and upper[t] > upper[p]:
+                upper[t] = upper[p]
+    df["supertrend"] = up
+    df["supertrend_upper"] = upper
+    df["supertrend_lower"] = lower
+    return df

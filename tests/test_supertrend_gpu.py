@@ -1,0 +1,101 @@
+"""GPU parity: bq_supertrend (Indicators.set_supertrend, strategies/coinrule/
+coinrule.py:143-160) vs the oracle's band recursion (oracle/indicators_ref.py:
+supertrend; pybinbot absent -> parity unpinned against pybinbot itself).
+
+The trend flag is a state machine over comparisons, so it is compared exactly
+up to the first candle whose decision lies within the 1e-9 tolerance band of
+its threshold (a near-tie may legitimately flip and then propagate); the
+bands are compared with the fp64 tolerance of tests/util.py over the same span.
+"""
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from binquant_amd import engine
+from binquant_amd.indicators import Indicators
+from binquant_amd.synth import numpy_panel
+from oracle import indicators_ref as ref
+from tests.util import assert_close
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_panel(panel, period, mult):
+    S, T = panel["close"].shape
+    out = {k: np.empty((S, T)) for k in ("supertrend", "supertrend_upper", "supertrend_lower")}
+    out["supertrend"] = np.empty((S, T), dtype=bool)
+    tie_free = np.full(S, T)
+    for s in range(S):
+        df = pd.DataFrame({k: panel[k][s] for k in ("open", "high", "low", "close", "volume")})
+        df = ref.supertrend(df, mult, period)
+        for k in out:
+            out[k][s] = df[k].to_numpy()
+        c = panel["close"][s]
+        up_p, lo_p = out["supertrend_upper"][s][:-1], out["supertrend_lower"][s][:-1]
+        tol = 1e-9 * np.abs(c[1:])
+        near = (np.abs(c[1:] - up_p) <= tol) | (np.abs(c[1:] - lo_p) <= tol)
+        if near.any():
+            tie_free[s] = int(np.argmax(near)) + 1
+    return out, tie_free
+
+
+def run(panel, period=10, mult=3.0):
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in panel.items()}
+    r = engine.supertrend(t["high"], t["low"], t["close"], period=period, multiplier=mult)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in r.items()}
+
+
+@pytest.mark.parametrize("S,T,period,mult", [(70, 700, 10, 3.0), (3, 1, 10, 3.0), (5, 9, 10, 3.0),
+                                             (64, 257, 7, 2.0), (130, 33, 14, 1.5), (1, 2000, 10, 3.0)])
+def test_supertrend_matches_oracle(cuda, S, T, period, mult):
+    panel = numpy_panel(S, T, seed0=S + T + period, edges=False)
+    got = run(panel, period, mult)
+    want, n_ok = oracle_panel(panel, period, mult)
+    price = np.abs(panel["close"]).mean(axis=1, keepdims=True)
+    for s in range(S):
+        n = n_ok[s]
+        np.testing.assert_array_equal(got["supertrend"][s, :n], want["supertrend"][s, :n], err_msg=f"symbol {s}")
+        for k in ("supertrend_upper", "supertrend_lower"):
+            assert_close(got[k][s, :n], want[k][s, :n], f"{k}[{s}]", scale=price[s])
+    assert (n_ok == T).mean() > 0.9   # near-ties are rare on random walks
+
+
+def test_supertrend_flips_on_trend_and_holds_bands(cuda):
+    """Rally then sell-off: the flag must be up at the top and down at the end,
+    and the held lower band must never fall while the trend stays up."""
+    T = 300
+    close = np.concatenate([np.linspace(100, 160, 150), np.linspace(160, 90, 150)])
+    panel = {"open": np.r_[close[0], close[:-1]][None], "close": close[None],
+             "high": (close * 1.002)[None], "low": (close * 0.998)[None], "volume": np.ones((1, T))}
+    got = run(panel)
+    want, _ = oracle_panel(panel, 10, 3.0)
+    np.testing.assert_array_equal(got["supertrend"], want["supertrend"])
+    assert got["supertrend"][0, 149] and not got["supertrend"][0, -1]
+    lo = got["supertrend_lower"][0, 10:150]
+    assert (np.diff(lo) >= 0).all()
+
+
+def test_supertrend_constant_market_is_exact(cuda):
+    """A halted market (h == l == c) has ATR exactly 0 in both paths, so the
+    bands equal the price and every comparison is an exact tie resolved the
+    same way (hold)."""
+    T = 80
+    c = np.full(T, 0.3)
+    c[:20] = np.linspace(0.29, 0.31, 20)
+    panel = {"open": c[None], "high": c[None].copy(), "low": c[None].copy(), "close": c[None], "volume": np.ones((1, T))}
+    got = run(panel)
+    want, _ = oracle_panel(panel, 10, 3.0)
+    np.testing.assert_array_equal(got["supertrend"], want["supertrend"])
+    np.testing.assert_array_equal(got["supertrend_upper"][0, 40:], want["supertrend_upper"][0, 40:])
+
+
+def test_set_supertrend_dataframe_api(cuda):
+    panel = numpy_panel(1, 400, seed0=5, edges=False)
+    df = pd.DataFrame({k: v[0] for k, v in panel.items()})
+    out = Indicators.set_supertrend(df, multiplier=3.0)
+    assert out is df and out["supertrend"].dtype == bool
+    want = ref.supertrend(pd.DataFrame({k: v[0] for k, v in panel.items()}), 3.0, 10)
+    assert bool(out["supertrend"].iloc[-1]) == bool(want["supertrend"].iloc[-1])
