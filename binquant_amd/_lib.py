@@ -56,6 +56,7 @@ PARTIAL_COLUMNS = (
 )
 MAX_WINDOW = 126
 MAX_RESAMPLE_FIELDS = 12
+STORE_MAX_BARS = 512
 AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
@@ -78,6 +79,21 @@ class BqParams(ctypes.Structure):
         ("mfi_window", ctypes.c_int32),
         ("reserved", ctypes.c_int32),
         ("bb_k", ctypes.c_double),
+    ]
+
+
+class BqStoreView(ctypes.Structure):
+    """Mirror of ``bq_store_view`` (include/binquant_amd.h)."""
+
+    _fields_ = [
+        ("ts", ctypes.c_void_p),
+        ("field", ctypes.c_void_p * 5),
+        ("head", ctypes.c_void_p),
+        ("count", ctypes.c_void_p),
+        ("last", ctypes.c_void_p),
+        ("capacity", ctypes.c_int64),
+        ("max_bars", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -117,6 +133,9 @@ SIGNATURES: dict[str, tuple] = {
     "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),
     "bq_join_returns": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
     "bq_beta_corr_pairs": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
+    "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
+    "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
+    "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
 }
 
 

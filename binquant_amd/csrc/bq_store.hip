@@ -1,0 +1,471 @@
+// Device-resident MarketStateStore and the per-message
+// features of the live market context (§8a a13/a16).
+//
+// market_regime/market_state_store.py:19-31 keeps, per symbol, the closed
+// candles sorted by timestamp, de-duplicated (keep="last") and capped to the
+// last max_bars (tail). Here every symbol owns a ring of max_bars candles in
+// HBM (bq_store_view): an update is an in-order append in the common case
+// (a new closed candle), and an LDS merge of the incoming sorted run with the
+// ring otherwise (a late / corrected candle or a REST history sync,
+// klines_provider.py:135-181).
+//
+// bq_store_features runs LiveMarketContextAccumulator._compute_symbol_features
+// (market_regime/live_market_context_accumulator.py:244-297) on the selected
+// rings by REPLAYING pandas' own recurrences over the whole history, so the
+// values are the pandas values bit for bit:
+//   ewm(span, adjust=False, min_periods=1).mean()   (aggregations.pyx ewm)
+//   rolling(w, min_periods=1).mean()                (roll_mean: Kahan add /
+//       remove with separate compensations, same-value and sign rules)
+//   rolling(w, min_periods=1).std(ddof=0)           (roll_var: compensated
+//       Welford add / remove, same-value rule), sqrt, fillna(0)
+// (restatements pinned bit-exact against pandas 2.3.3 in tests/).
+// Lane = symbol; chunks of the rings are read coalesced and transposed
+// through LDS; each lane keeps its last 14 true ranges / 20 closes in a
+// private LDS ring for the window removals.
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+namespace bq {
+
+struct StoreArgs {
+  int64_t* ts;
+  double* f[BQ_NUM_INPUTS];
+  int32_t* head;
+  int32_t* count;
+  int64_t* last;
+  int64_t cap;
+  int M;
+};
+
+__device__ __forceinline__ int ring_at(int h, int i, int M) {
+  const int p = h + i;
+  return p >= M ? p - M : p;
+}
+
+// ---- update --------------------------------------------------------------------
+constexpr int SU_NT = 64;
+
+struct UpdArgs {
+  const int64_t* slot;
+  const int64_t* ts;
+  const double* f[BQ_NUM_INPUTS];
+  const int64_t* seg;
+};
+
+// first i in [0, n) with key(i) >= v
+template <typename F>
+__device__ __forceinline__ int lower_bound_fn(int n, int64_t v, F key) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (key(mid) < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(SU_NT) void store_update_kernel(const StoreArgs V, const UpdArgs U) {
+  __shared__ int64_t sT[BQ_STORE_MAX_BARS];
+  __shared__ double sF[BQ_NUM_INPUTS][BQ_STORE_MAX_BARS];
+  __shared__ int sPK[BQ_STORE_MAX_BARS + 1];
+  __shared__ int sCnt[SU_NT];
+  const int tid = threadIdx.x;
+  const int64_t b = U.seg[blockIdx.x], e = U.seg[blockIdx.x + 1];
+  const int k = (int)(e - b);
+  if (k <= 0) return;
+  const int64_t s = U.slot[b];
+  const int M = V.M;
+  const int n = V.count[s], h = V.head[s];
+  const int64_t row = s * (int64_t)M;
+  const int64_t* __restrict__ its = U.ts + b;
+
+  if (n == 0 || its[0] > V.last[s]) {   // in-order append (the live path)
+    const int total = n + k;
+    const int keep = min(M, total);
+    for (int j = max(0, k - M) + tid; j < k; j += SU_NT) {
+      const int p = ring_at(h, (n + j) % M, M);
+      V.ts[row + p] = its[j];
+#pragma unroll
+      for (int c = 0; c < BQ_NUM_INPUTS; ++c) V.f[c][row + p] = U.f[c][b + j];
+    }
+    if (tid == 0) {
+      V.count[s] = keep;
+      V.head[s] = (int)((h + (int64_t)(total - keep)) % M);
+      V.last[s] = its[k - 1];
+    }
+    return;
+  }
+
+  // general merge: an existing candle is dropped when the run carries its
+  // timestamp (keep="last"); sPK[i] = kept existing candles before i
+  auto ets = [&](int i) { return V.ts[row + ring_at(h, i, M)]; };
+  auto in_run = [&](int64_t v) {
+    const int j = lower_bound_fn(k, v, [&](int q) { return its[q]; });
+    return j < k && its[j] == v;
+  };
+  const int chunk = (n + SU_NT - 1) / SU_NT;
+  const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
+  int cnt = 0;
+  for (int i = i0; i < i1; ++i) cnt += in_run(ets(i)) ? 0 : 1;
+  sCnt[tid] = cnt;
+  __syncthreads();
+  int base = 0;
+  for (int q = 0; q < tid; ++q) base += sCnt[q];
+  for (int i = i0; i < i1; ++i) {
+    sPK[i] = base;
+    base += in_run(ets(i)) ? 0 : 1;
+  }
+  if (tid == SU_NT - 1) sPK[n] = base;
+  __syncthreads();
+  const int L = sPK[n] + k;
+  const int keep = min(M, L), off = L - keep;
+  for (int i = tid; i < n; i += SU_NT) {
+    if (sPK[i + 1] == sPK[i]) continue;   // dropped
+    const int64_t te = ets(i);
+    const int pos = sPK[i] + lower_bound_fn(k, te, [&](int q) { return its[q]; });
+    if (pos >= off) {
+      const int p = ring_at(h, i, M);
+      sT[pos - off] = te;
+#pragma unroll
+      for (int c = 0; c < BQ_NUM_INPUTS; ++c) sF[c][pos - off] = V.f[c][row + p];
+    }
+  }
+  for (int j = tid; j < k; j += SU_NT) {
+    const int64_t tj = its[j];
+    const int pos = j + sPK[lower_bound_fn(n, tj, ets)];
+    if (pos >= off) {
+      sT[pos - off] = tj;
+#pragma unroll
+      for (int c = 0; c < BQ_NUM_INPUTS; ++c) sF[c][pos - off] = U.f[c][b + j];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < keep; q += SU_NT) {
+    V.ts[row + q] = sT[q];
+#pragma unroll
+    for (int c = 0; c < BQ_NUM_INPUTS; ++c) V.f[c][row + q] = sF[c][q];
+  }
+  if (tid == 0) {
+    V.count[s] = keep;
+    V.head[s] = 0;
+    V.last[s] = sT[keep - 1];
+  }
+}
+
+// ---- features of the latest candle -------------------------------------------------
+constexpr int SF_CT = 16;
+constexpr int SF_ATR = 14;   // live_market_context_accumulator.py:268
+constexpr int SF_BB = 20;    // :269-270
+
+// pandas roll_mean state (add_mean / remove_mean / calc_mean)
+struct RollMean {
+  double sum, comp_add, comp_rem, prev;
+  int nobs, neg, same;
+  __device__ __forceinline__ void init() {
+    sum = comp_add = comp_rem = 0.0;
+    nobs = neg = same = 0;
+    prev = 0.0;
+  }
+  __device__ __forceinline__ void add(double v) {
+    if (v != v) return;
+    ++nobs;
+    const double y = v - comp_add;
+    const double t = sum + y;
+    comp_add = t - sum - y;
+    sum = t;
+    if (signbit(v)) ++neg;
+    same = (v == prev) ? same + 1 : 1;
+    prev = v;
+  }
+  __device__ __forceinline__ void remove(double v) {
+    if (v != v) return;
+    --nobs;
+    const double y = -v - comp_rem;
+    const double t = sum + y;
+    comp_rem = t - sum - y;
+    sum = t;
+    if (signbit(v)) --neg;
+  }
+  __device__ __forceinline__ double value() const {   // min_periods = 1
+    if (nobs <= 0) return qnan();
+    double r = sum / (double)nobs;
+    if (same >= nobs) r = prev;
+    else if (neg == 0 && r < 0.0) r = 0.0;
+    else if (neg == nobs && r > 0.0) r = 0.0;
+    return r;
+  }
+};
+
+// pandas roll_var state (add_var / remove_var / calc_var), ddof 0
+struct RollVar {
+  double nobs, mean, ssq, comp_add, comp_rem, prev;
+  int same;
+  __device__ __forceinline__ void init(double first) {
+    nobs = mean = ssq = comp_add = comp_rem = 0.0;
+    same = 0;
+    prev = first;
+  }
+  __device__ __forceinline__ void add(double v) {
+    if (v != v) return;
+    same = (v == prev) ? same + 1 : 1;
+    prev = v;
+    nobs += 1.0;
+    const double pm = mean - comp_add;
+    const double y = v - comp_add;
+    const double t = y - mean;
+    comp_add = t + mean - y;
+    mean = nobs != 0.0 ? mean + t / nobs : 0.0;
+    ssq = ssq + (v - pm) * (v - mean);
+  }
+  __device__ __forceinline__ void remove(double v) {
+    if (v != v) return;
+    nobs -= 1.0;
+    if (nobs != 0.0) {
+      const double pm = mean - comp_rem;
+      const double y = v - comp_rem;
+      const double t = y - mean;
+      comp_rem = t + mean - y;
+      mean = mean - t / nobs;
+      ssq = ssq - (v - pm) * (v - mean);
+    } else {
+      mean = ssq = 0.0;
+    }
+  }
+  __device__ __forceinline__ double var0() const {   // min_periods 1, ddof 0
+    if (!(nobs >= 1.0 && nobs > 0.0)) return qnan();
+    if (nobs == 1.0 || (double)same >= nobs) return 0.0;
+    const double r = ssq / nobs;
+    return r < 0.0 ? 0.0 : r;
+  }
+};
+
+// pandas ewm(adjust=False, min_periods=1) over a NaN-free close series
+struct Ewm {
+  double w, old_wt;
+  bool have;
+  __device__ __forceinline__ void step(double x, double alpha, double om) {
+    if (!have) {
+      w = x;
+      have = x == x;
+      old_wt = 1.0;
+      return;
+    }
+    if (x != x) {   // NaN gap: decay only (closes are NaN-free in the store)
+      old_wt *= om;
+      return;
+    }
+    old_wt *= om;
+    if (w != x) {
+      w = old_wt * w + alpha * x;
+      w /= old_wt + alpha;
+    }
+    old_wt = 1.0;
+  }
+};
+
+struct FeatSel {
+  const int64_t* slots;
+  int64_t n;
+  double* feat[BQ_NUM_FEATURES];
+  double* close;
+  double a20, om20, a50, om50;
+};
+
+__global__ __launch_bounds__(WAVE) void store_features_kernel(const StoreArgs V, const FeatSel F) {
+  __shared__ double sX[3][SF_CT * STG_PITCH];   // high, low, close chunk (transposed)
+  __shared__ double sTR[SF_ATR][WAVE];          // per-lane ring of true ranges
+  __shared__ double sCL[SF_BB][WAVE];           // per-lane ring of closes
+  __shared__ int sH[WAVE], sN[WAVE];
+  __shared__ int64_t sRow[WAVE];
+  const int lane = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * WAVE + lane;
+  const int M = V.M;
+  int n = 0;
+  if (i < F.n) {
+    const int64_t s = F.slots[i];
+    n = V.count[s];
+    sH[lane] = V.head[s];
+    sRow[lane] = s * (int64_t)M;
+  } else {
+    sH[lane] = 0;
+    sRow[lane] = 0;
+  }
+  sN[lane] = n;
+  int nmax = n;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
+  __syncthreads();
+
+  Ewm e20 = {0.0, 1.0, false}, e50 = {0.0, 1.0, false};
+  RollMean atr, mid;
+  RollVar var;
+  atr.init();
+  mid.init();
+  double pc = qnan(), c_last = qnan(), c_prev = qnan();
+  for (int t0 = 0; t0 < nmax; t0 += SF_CT) {
+    // coalesced chunk load: element e -> lane e / CT, candle e % CT of its ring
+#pragma unroll
+    for (int q = 0; q < SF_CT; ++q) {
+      const int el = lane + WAVE * q;
+      const int l = el / SF_CT, tt = el % SF_CT, t = t0 + tt;
+      double vh = qnan(), vl = qnan(), vc = qnan();
+      if (t < sN[l]) {
+        const int64_t p = sRow[l] + ring_at(sH[l], t, M);
+        vh = V.f[BQ_HIGH][p];
+        vl = V.f[BQ_LOW][p];
+        vc = V.f[BQ_CLOSE][p];
+      }
+      sX[0][tt * STG_PITCH + l] = vh;
+      sX[1][tt * STG_PITCH + l] = vl;
+      sX[2][tt * STG_PITCH + l] = vc;
+    }
+    __syncthreads();
+    const int m = min(SF_CT, n - t0);
+    for (int j = 0; j < m; ++j) {
+      const int t = t0 + j;
+      const int x = j * STG_PITCH + lane;
+      const double h = sX[0][x], l = sX[1][x], c = sX[2][x];
+      const double tr = true_range(h, l, pc);
+      if (t == 0) var.init(c);
+      if (t >= SF_ATR) atr.remove(sTR[t % SF_ATR][lane]);
+      atr.add(tr);
+      sTR[t % SF_ATR][lane] = tr;
+      if (t >= SF_BB) {
+        const double old = sCL[t % SF_BB][lane];
+        mid.remove(old);
+        var.remove(old);
+      }
+      mid.add(c);
+      var.add(c);
+      sCL[t % SF_BB][lane] = c;
+      e20.step(c, F.a20, F.om20);
+      e50.step(c, F.a50, F.om50);
+      c_prev = c_last;
+      c_last = c;
+      pc = c;
+    }
+    __syncthreads();
+  }
+  if (i >= F.n) return;
+  double ret = qnan(), ema20 = qnan(), ema50 = qnan(), trend = qnan(), atr_pct = qnan(), bbw = qnan();
+  if (n >= 2) {   // _compute_symbol_features returns None below 2 bars (:249-250)
+    ema20 = e20.w;
+    ema50 = e50.w;
+    const double a = atr.value();
+    const double mu = mid.value();
+    double v = var.var0();
+    const double sd = v == v ? sqrt(v) : 0.0;   // std(ddof=0).fillna(0)
+    const double up = mu + (2.0 * sd), lo = mu - (2.0 * sd);
+    ret = safe_pct(c_last, c_prev);
+    atr_pct = c_last != 0.0 ? a / c_last : 0.0;
+    bbw = mu != 0.0 ? (up - lo) / fabs(mu) : 0.0;
+    trend = ema50 != 0.0 ? (ema20 - ema50) / fabs(ema50) : 0.0;
+  }
+  if (F.feat[BQ_F_RETURN]) F.feat[BQ_F_RETURN][i] = ret;
+  if (F.feat[BQ_F_EMA20]) F.feat[BQ_F_EMA20][i] = ema20;
+  if (F.feat[BQ_F_EMA50]) F.feat[BQ_F_EMA50][i] = ema50;
+  if (F.feat[BQ_F_TREND]) F.feat[BQ_F_TREND][i] = trend;
+  if (F.feat[BQ_F_ATR_PCT]) F.feat[BQ_F_ATR_PCT][i] = atr_pct;
+  if (F.feat[BQ_F_BB_WIDTH]) F.feat[BQ_F_BB_WIDTH][i] = bbw;
+  if (F.close) F.close[i] = n >= 1 ? c_last : qnan();
+}
+
+// ---- ordered export -------------------------------------------------------------
+struct OutTab {
+  int64_t* ts;
+  double* f[BQ_NUM_INPUTS];
+};
+
+__global__ __launch_bounds__(256) void store_gather_kernel(const StoreArgs V, const int64_t* __restrict__ slots,
+                                                           int64_t n_sel, const OutTab O, int64_t ld_out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int M = V.M;
+  if (i >= n_sel * (int64_t)M) return;
+  const int64_t r = i / M;
+  const int t = (int)(i % M);
+  const int64_t s = slots[r];
+  const int n = V.count[s];
+  const bool ok = t < n;
+  const int64_t p = s * (int64_t)M + ring_at(V.head[s], ok ? t : 0, M);
+  if (O.ts) O.ts[r * ld_out + t] = ok ? V.ts[p] : 0;
+#pragma unroll
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c)
+    if (O.f[c]) O.f[c][r * ld_out + t] = ok ? V.f[c][p] : qnan();
+}
+
+__host__ bool view_ok(const bq_store_view* v) {
+  if (!v || !v->ts || !v->head || !v->count || !v->last || v->capacity < 0 || v->max_bars < 2 ||
+      v->max_bars > BQ_STORE_MAX_BARS)
+    return false;
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c)
+    if (!v->field[c]) return false;
+  return true;
+}
+
+__host__ StoreArgs to_args(const bq_store_view* v) {
+  StoreArgs A;
+  A.ts = v->ts;
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c) A.f[c] = v->field[c];
+  A.head = v->head;
+  A.count = v->count;
+  A.last = v->last;
+  A.cap = v->capacity;
+  A.M = v->max_bars;
+  return A;
+}
+
+}  // namespace bq
+
+extern "C" {
+
+int bq_store_update(const bq_store_view* st, const int64_t* slot, const int64_t* ts, const double* const* ohlcv,
+                    const int64_t* seg_begin, int64_t n_seg, void* stream) {
+  using namespace bq;
+  if (!view_ok(st) || !slot || !ts || !ohlcv || !seg_begin || n_seg < 0 || n_seg > 0x7fffffff) return BQ_EINVAL;
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c)
+    if (!ohlcv[c]) return BQ_EINVAL;
+  if (n_seg == 0) return BQ_OK;
+  UpdArgs U;
+  U.slot = slot;
+  U.ts = ts;
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c) U.f[c] = ohlcv[c];
+  U.seg = seg_begin;
+  hipLaunchKernelGGL(store_update_kernel, dim3((unsigned)n_seg), dim3(SU_NT), 0, (hipStream_t)stream, to_args(st), U);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_sel, double* const* feat,
+                      double* close_out, void* stream) {
+  using namespace bq;
+  if (!view_ok(st) || !slots || !feat || n_sel < 0) return BQ_EINVAL;
+  if (n_sel == 0) return BQ_OK;
+  FeatSel F;
+  F.slots = slots;
+  F.n = n_sel;
+  for (int i = 0; i < BQ_NUM_FEATURES; ++i) F.feat[i] = feat[i];
+  F.close = close_out;
+  // pandas: comass = (span - 1) / 2, alpha = 1 / (1 + comass)
+  F.a20 = 1.0 / (1.0 + (20.0 - 1.0) / 2.0);
+  F.om20 = 1.0 - F.a20;
+  F.a50 = 1.0 / (1.0 + (50.0 - 1.0) / 2.0);
+  F.om50 = 1.0 - F.a50;
+  const unsigned blocks = (unsigned)((n_sel + WAVE - 1) / WAVE);
+  hipLaunchKernelGGL(store_features_kernel, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, to_args(st), F);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,
+                    double* const* out, int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!view_ok(st) || !slots || !out || n_sel < 0 || ld_out < st->max_bars) return BQ_EINVAL;
+  if (n_sel == 0) return BQ_OK;
+  OutTab O;
+  O.ts = ts_out;
+  for (int c = 0; c < BQ_NUM_INPUTS; ++c) O.f[c] = out[c];
+  const int64_t items = n_sel * (int64_t)st->max_bars;
+  hipLaunchKernelGGL(store_gather_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     to_args(st), slots, n_sel, O, ld_out);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,401 @@
+"""Device-resident MarketStateStore and live market-context accumulator
+(§8a a13, a14, a16).
+
+``DeviceMarketStateStore`` keeps the API of market_regime/market_state_store.py
+(update / get_symbol_history / get_all_histories / get_last_closed_timestamp /
+get_tracked_symbols / get_fresh_symbols, same normalisation and errors) but
+the histories live in HBM as per-symbol rings (bq_store_view): a closed
+candle is an O(1) in-order append on the device instead of a pandas
+concat + drop_duplicates + sort + tail (3.9 ms per update),
+and ``update_batch`` / ``update_slots`` take a whole tick of symbols in one
+launch.
+
+``DeviceLiveMarketContextAccumulator`` keeps the API of
+market_regime/live_market_context_accumulator.py (on_closed_candle,
+refresh_context_for_timestamp, get_context, get_latest_context). A context
+build is: fresh slots (last == ts) on the device -> bq_store_features on
+their histories (pandas recurrences replayed bit for bit) ->
+bq_breadth_partial (fixed-order sums) -> one all-reduce of 12 doubles when
+symbols are sharded over ranks -> host scoring and regime annotation
+(regime.py). The reference instead recomputes every fresh symbol's features
+in pandas on every message (O(S^2 * 400) per period).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from collections import deque
+from collections.abc import Mapping, Sequence
+from math import ceil
+from typing import Any
+
+import numpy as np
+import pandas as pd
+import torch
+import torch.distributed as dist
+
+from .. import _lib, engine
+from .._lib import FEATURE_COLUMNS, INPUT_FIELDS
+from .regime import MIN_COVERAGE_RATIO, REQUIRED_FRESH_SYMBOLS, annotate_market, annotate_symbols, score_contexts
+
+STORE_COLUMNS = ["timestamp", "open", "high", "low", "close", "volume"]
+
+
+def normalize_candles(candle: Mapping[str, Any] | pd.Series | pd.DataFrame) -> pd.DataFrame:
+    """MarketStateStore._normalize_input (market_regime/market_state_store.py:56-87):
+    same defaults (volume 0, open/high/low = close), same ValueErrors, numeric
+    coercion, rows without timestamp / close dropped."""
+    if isinstance(candle, pd.DataFrame):
+        df = candle.copy()
+    elif isinstance(candle, pd.Series):
+        df = candle.to_frame().T
+    else:
+        df = pd.DataFrame([dict(candle)])
+    if "timestamp" not in df.columns:
+        raise ValueError("MarketStateStore.update requires a 'timestamp' column.")
+    for column in STORE_COLUMNS:
+        if column not in df.columns:
+            if column == "volume":
+                df[column] = 0.0
+            elif column in ("open", "high", "low"):
+                df[column] = df["close"] if "close" in df.columns else np.nan
+            else:
+                raise ValueError(f"Missing required candle field '{column}'.")
+    for column in STORE_COLUMNS:
+        df[column] = pd.to_numeric(df[column], errors="coerce")
+    df = df.dropna(subset=["timestamp", "close"])
+    df["timestamp"] = df["timestamp"].astype(int)
+    return df[STORE_COLUMNS].copy()
+
+
+def _device(device) -> torch.device:
+    if device is not None:
+        return torch.device(device)
+    if not torch.cuda.is_available():
+        raise RuntimeError("DeviceMarketStateStore needs a HIP device (no CPU fallback)")
+    return torch.device("cuda")
+
+
+class DeviceMarketStateStore:
+    """MarketStateStore with the histories in HBM (one ring per symbol slot)."""
+
+    def __init__(self, max_bars_per_symbol: int = 200, capacity: int = 1024, device=None) -> None:
+        if not 2 <= int(max_bars_per_symbol) <= _lib.STORE_MAX_BARS:
+            raise ValueError(f"max_bars_per_symbol must be in [2, {_lib.STORE_MAX_BARS}]")
+        self.max_bars_per_symbol = int(max_bars_per_symbol)
+        self.device = _device(device)
+        self._slots: dict[str, int] = {}
+        self._names: list[str] = []
+        self._alloc(max(1, int(capacity)))
+
+    # -- storage ----------------------------------------------------------------
+    def _alloc(self, cap: int, old=None) -> None:
+        M, dev = self.max_bars_per_symbol, self.device
+        ts = torch.zeros((cap, M), dtype=torch.int64, device=dev)
+        f = torch.full((len(INPUT_FIELDS), cap, M), float("nan"), dtype=torch.float64, device=dev)
+        head = torch.zeros(cap, dtype=torch.int32, device=dev)
+        count = torch.zeros(cap, dtype=torch.int32, device=dev)
+        last = torch.zeros(cap, dtype=torch.int64, device=dev)
+        if old is not None:
+            n = old["ts"].shape[0]
+            ts[:n] = old["ts"]
+            f[:, :n] = old["f"]
+            head[:n] = old["head"]
+            count[:n] = old["count"]
+            last[:n] = old["last"]
+        self._t = dict(ts=ts, f=f, head=head, count=count, last=last)
+        self.capacity = cap
+        v = _lib.BqStoreView()
+        v.ts = ts.data_ptr()
+        for c in range(len(INPUT_FIELDS)):
+            v.field[c] = f[c].data_ptr()
+        v.head, v.count, v.last = head.data_ptr(), count.data_ptr(), last.data_ptr()
+        v.capacity, v.max_bars = cap, M
+        self._view = v
+
+    def _slot(self, symbol: str) -> int:
+        s = self._slots.get(symbol)
+        if s is None:
+            s = len(self._names)
+            if s >= self.capacity:
+                self._alloc(2 * self.capacity, old=self._t)
+            self._slots[symbol] = s
+            self._names.append(symbol)
+        return s
+
+    def slot_of(self, symbol: str) -> int | None:
+        return self._slots.get(symbol)
+
+    def symbol_of(self, slot: int) -> str:
+        return self._names[slot]
+
+    @property
+    def n_tracked(self) -> int:
+        return len(self._names)
+
+    # -- batched updates (device) ---------------------------------------------------
+    def update_slots(self, slots: torch.Tensor, ts: torch.Tensor, fields: Sequence[torch.Tensor], stream=None) -> None:
+        """One launch for a batch of candles (arrival order; device tensors):
+        rows with NaN close are dropped, each (slot, timestamp) keeps its LAST
+        row, runs are sorted by timestamp per slot, then merged into the rings."""
+        slots = slots.to(self.device, torch.int64).reshape(-1)
+        ts = ts.to(self.device, torch.int64).reshape(-1)
+        fields = [x.to(self.device, torch.float64).reshape(-1) for x in fields]
+        if len(fields) != len(INPUT_FIELDS) or any(x.numel() != slots.numel() for x in fields) or ts.numel() != slots.numel():
+            raise ValueError("update_slots: slots, ts and the five OHLCV fields must have one entry per candle")
+        if slots.numel() and (int(slots.min()) < 0 or int(slots.max()) >= self.n_tracked):
+            raise ValueError("update_slots: slot out of range (register symbols first)")
+        ok = ~torch.isnan(fields[INPUT_FIELDS.index("close")])
+        idx = torch.nonzero(ok).reshape(-1)
+        if idx.numel() == 0:
+            return
+        order = idx[torch.argsort(ts[idx], stable=True)]
+        order = order[torch.argsort(slots[order], stable=True)]
+        s2, t2 = slots[order], ts[order]
+        last_row = torch.ones_like(s2, dtype=torch.bool)
+        last_row[:-1] = (s2[1:] != s2[:-1]) | (t2[1:] != t2[:-1])
+        sel = order[last_row]
+        s3, t3 = slots[sel].contiguous(), ts[sel].contiguous()
+        f3 = [x[sel].contiguous() for x in fields]
+        _, counts = torch.unique_consecutive(s3, return_counts=True)
+        seg = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=self.device)
+        seg[1:] = torch.cumsum(counts, 0)
+        st = _lib.load().bq_store_update(
+            ctypes.byref(self._view), ctypes.c_void_p(s3.data_ptr()), ctypes.c_void_p(t3.data_ptr()),
+            _lib.ptr_array([x.data_ptr() for x in f3]), ctypes.c_void_p(seg.data_ptr()), counts.numel(),
+            engine._stream_handle(stream),
+        )
+        _lib.check(st, "bq_store_update")
+
+    def update_batch(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume) -> None:
+        """Many symbols' candles (host arrays, arrival order) in one launch."""
+        slots = torch.tensor([self._slot(s) for s in symbols], dtype=torch.int64)
+        cols = [torch.as_tensor(np.asarray(x, dtype=np.float64)) for x in (open_, high, low, close, volume)]
+        self.update_slots(slots, torch.as_tensor(np.asarray(timestamp, dtype=np.int64)), cols)
+
+    # -- reference API ----------------------------------------------------------------
+    def update(self, symbol: str, candle: Mapping[str, Any] | pd.Series | pd.DataFrame) -> pd.DataFrame:
+        normalized = normalize_candles(candle)
+        s = self._slot(symbol)
+        if len(normalized):
+            self.update_slots(
+                torch.full((len(normalized),), s, dtype=torch.int64),
+                torch.from_numpy(normalized["timestamp"].to_numpy(np.int64)),
+                [torch.from_numpy(normalized[c].to_numpy(np.float64)) for c in INPUT_FIELDS],
+            )
+        history = self.get_symbol_history(symbol)
+        if history.empty:
+            # the reference stores the empty history and then fails on
+            # history.iloc[-1] (market_state_store.py:31)
+            raise IndexError("MarketStateStore.update: no candle with a timestamp and a close")
+        return history
+
+    def _gather(self, slots: list[int]) -> tuple[np.ndarray, np.ndarray, dict[str, np.ndarray]]:
+        M = self.max_bars_per_symbol
+        sl = torch.tensor(slots, dtype=torch.int64, device=self.device)
+        ts = torch.empty((len(slots), M), dtype=torch.int64, device=self.device)
+        outs = [torch.empty((len(slots), M), dtype=torch.float64, device=self.device) for _ in INPUT_FIELDS]
+        st = _lib.load().bq_store_gather(
+            ctypes.byref(self._view), ctypes.c_void_p(sl.data_ptr()), len(slots), ctypes.c_void_p(ts.data_ptr()),
+            _lib.ptr_array([o.data_ptr() for o in outs]), M, engine._stream_handle(None),
+        )
+        _lib.check(st, "bq_store_gather")
+        counts = self._t["count"][sl].cpu().numpy()
+        return counts, ts.cpu().numpy(), {c: o.cpu().numpy() for c, o in zip(INPUT_FIELDS, outs)}
+
+    @staticmethod
+    def _frame(n: int, ts: np.ndarray, f: dict[str, np.ndarray], r: int) -> pd.DataFrame:
+        d = {"timestamp": ts[r, :n].astype(np.int64)}
+        for c in INPUT_FIELDS:
+            d[c] = f[c][r, :n]
+        return pd.DataFrame(d, columns=STORE_COLUMNS)
+
+    def get_symbol_history(self, symbol: str) -> pd.DataFrame:
+        s = self._slots.get(symbol)
+        if s is None:
+            return pd.DataFrame()
+        counts, ts, f = self._gather([s])
+        return self._frame(int(counts[0]), ts, f, 0)
+
+    def get_all_histories(self) -> dict[str, pd.DataFrame]:
+        if not self._names:
+            return {}
+        counts, ts, f = self._gather(list(range(self.n_tracked)))
+        return {name: self._frame(int(counts[i]), ts, f, i) for i, name in enumerate(self._names)}
+
+    def get_last_closed_timestamp(self, symbol: str) -> int | None:
+        s = self._slots.get(symbol)
+        if s is None or int(self._t["count"][s]) == 0:
+            return None
+        return int(self._t["last"][s])
+
+    def get_tracked_symbols(self) -> list[str]:
+        return sorted(self._names)
+
+    def fresh_slots(self, timestamp: int) -> torch.Tensor:
+        """Slots whose last closed candle is `timestamp` (ascending slot ids, device)."""
+        n = self.n_tracked
+        m = (self._t["last"][:n] == int(timestamp)) & (self._t["count"][:n] > 0)
+        return torch.nonzero(m).reshape(-1)
+
+    def get_fresh_symbols(self, timestamp: int) -> set[str]:
+        return {self._names[i] for i in self.fresh_slots(timestamp).cpu().tolist()}
+
+    # -- features ---------------------------------------------------------------------------
+    def features(self, slots: torch.Tensor, stream=None) -> tuple[dict[str, torch.Tensor], torch.Tensor]:
+        """_compute_symbol_features of each slot's history (NaN rows where the
+        reference returns None). Returns ({feature: [n]}, latest close [n])."""
+        slots = slots.to(self.device, torch.int64).contiguous()
+        n = slots.numel()
+        feats = {k: torch.empty(n, dtype=torch.float64, device=self.device) for k in FEATURE_COLUMNS}
+        close = torch.empty(n, dtype=torch.float64, device=self.device)
+        st = _lib.load().bq_store_features(
+            ctypes.byref(self._view), ctypes.c_void_p(slots.data_ptr()), n,
+            _lib.ptr_array([feats[k].data_ptr() for k in FEATURE_COLUMNS]), ctypes.c_void_p(close.data_ptr()),
+            engine._stream_handle(stream),
+        )
+        _lib.check(st, "bq_store_features")
+        return feats, close
+
+
+class DeviceLiveMarketContextAccumulator:
+    """LiveMarketContextAccumulator over a DeviceMarketStateStore.
+
+    With torch.distributed initialised and a symbol-sharded store per rank
+    (the benchmark symbol replicated on every rank), the per-timestamp
+    partial sums and the tracked / fresh counts are all-reduced in ONE call
+    (12 doubles); every rank then scores the same context.
+    """
+
+    def __init__(self, state_store: DeviceMarketStateStore, btc_symbol: str, group=None) -> None:
+        self.state_store = state_store
+        self.btc_symbol = btc_symbol
+        self.group = group
+        self._contexts_by_timestamp: dict[int, dict] = {}
+        self._context_order: deque[int] = deque(maxlen=64)
+        self.last_symbol_features: dict[str, np.ndarray] | None = None
+
+    # -- reference API ------------------------------------------------------------------
+    def on_closed_candle(self, symbol: str, candle) -> dict | None:
+        history = self.state_store.update(symbol=symbol, candle=candle)
+        return self.refresh_context_for_timestamp(int(history.iloc[-1]["timestamp"]))
+
+    def on_closed_candles(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume,
+                          at: int | None = None) -> dict | None:
+        """A whole tick in one device update, then one context build (at the
+        tick's latest timestamp unless `at` is given)."""
+        self.state_store.update_batch(symbols, timestamp, open_, high, low, close, volume)
+        ts = int(np.max(np.asarray(timestamp))) if at is None else int(at)
+        return self.refresh_context_for_timestamp(ts)
+
+    def get_context(self, timestamp: int) -> dict | None:
+        return self._contexts_by_timestamp.get(timestamp)
+
+    def get_latest_context(self) -> dict | None:
+        while self._context_order:
+            ts = self._context_order[-1]
+            ctx = self._contexts_by_timestamp.get(ts)
+            if ctx is not None:
+                return ctx
+            self._context_order.pop()
+        return None
+
+    def refresh_context_for_timestamp(self, timestamp: int) -> dict | None:
+        context = self._build_context(int(timestamp))
+        if context is None:
+            return None
+        self._contexts_by_timestamp[int(timestamp)] = context
+        if int(timestamp) not in self._context_order:
+            self._context_order.append(int(timestamp))
+        return context
+
+    def _get_previous_context(self, timestamp: int) -> dict | None:
+        for known in reversed(self._context_order):
+            if known >= timestamp:
+                continue
+            ctx = self._contexts_by_timestamp.get(known)
+            if ctx is not None:
+                return ctx
+        return None
+
+    # -- the build --------------------------------------------------------------------------
+    def _sharded(self) -> bool:
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
+
+    def _build_context(self, timestamp: int) -> dict | None:
+        store = self.state_store
+        dev = store.device
+        fresh = store.fresh_slots(timestamp)
+        btc_slot = store.slot_of(self.btc_symbol)
+        # the benchmark is replicated on every rank: only rank 0 counts it
+        btc_counted = btc_slot is not None and (not self._sharded() or dist.get_rank(self.group) == 0)
+        if btc_slot is not None and not btc_counted:
+            fresh = fresh[fresh != btc_slot]
+        n_fresh = fresh.numel()
+        sel = fresh if btc_slot is None else torch.cat([fresh, torch.tensor([btc_slot], dtype=torch.int64, device=dev)])
+        feats, close = store.features(sel)
+        fz = {k: v[:n_fresh].reshape(n_fresh, 1) for k, v in feats.items()}
+        npart = len(_lib.PARTIAL_COLUMNS)
+        red = torch.zeros(npart + 2, dtype=torch.float64, device=dev)
+        if n_fresh:
+            engine.breadth_partial(close[:n_fresh].reshape(n_fresh, 1), fz, out=red[:npart].view(1, -1))
+        red[npart] = float(n_fresh)
+        red[npart + 1] = float(store.n_tracked - (0 if btc_counted or btc_slot is None else 1))
+        if self._sharded():
+            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+        red_h = red.cpu().numpy()
+        total_fresh, total_tracked = int(red_h[npart]), int(red_h[npart + 1])
+        required = max(REQUIRED_FRESH_SYMBOLS, ceil(total_tracked * MIN_COVERAGE_RATIO))
+        if total_fresh < required:
+            return None
+        if btc_slot is not None:
+            btc_ret = float(feats["return_pct"][n_fresh])
+            btc_trend = float(feats["trend_score"][n_fresh])
+        else:
+            btc_ret = btc_trend = float("nan")
+        btc_valid = not np.isnan(btc_ret)
+        batch = score_contexts(
+            red_h[None, :npart], np.array([btc_ret if btc_valid else 0.0]),
+            np.array([btc_trend if btc_valid else 0.0]), np.array([btc_valid]), total_tracked=total_tracked,
+            fresh_count=np.array([total_fresh]), timestamps=np.array([timestamp]),
+        )
+        previous = self._get_previous_context(timestamp)
+        batch = annotate_market(batch, previous)
+        ctx = batch.context_at(0)
+        if ctx is None:
+            return None
+        ctx["btc_symbol"] = self.btc_symbol
+        ctx["confidence"] = 1.0
+        ctx["is_provisional"] = False
+        # this rank's fresh symbols with relative strength + micro regime
+        # (regime_transitions.py:162-232), previous micro regime chained
+        f = {k: v[:n_fresh].cpu().numpy() for k, v in feats.items()}
+        c = close[:n_fresh].cpu().numpy()
+        ok = ~np.isnan(f["return_pct"])
+        names = [store.symbol_of(i) for i in fresh.cpu().tolist()]
+        rs = f["return_pct"] - (btc_ret if btc_valid else 0.0)
+        if not btc_valid:
+            rs[:] = 0.0
+        rs[[i for i, nme in enumerate(names) if nme == self.btc_symbol]] = 0.0
+        prev_sym = (previous or {}).get("symbol_features") or {}
+        prev_reg = np.array([prev_sym.get(nme, {}).get("micro_regime") for nme in names], dtype=object)
+        prev_str = np.array([prev_sym.get(nme, {}).get("micro_regime_strength", 0.0) or 0.0 for nme in names])
+        ann = annotate_symbols(f["trend_score"], c > f["ema20"], c > f["ema50"], rs, f["bb_width"], f["atr_pct"],
+                               f["return_pct"], prev_regime=prev_reg, prev_strength=prev_str)
+        sym = {}
+        for i in np.flatnonzero(ok):
+            d = {k: float(f[k][i]) for k in FEATURE_COLUMNS}
+            d.update(symbol=names[i], timestamp=int(timestamp), close=float(c[i]), above_ema20=bool(c[i] > f["ema20"][i]),
+                     above_ema50=bool(c[i] > f["ema50"][i]), relative_strength_vs_btc=float(rs[i]),
+                     micro_regime=ann["micro_regime"][i], micro_regime_strength=float(ann["micro_regime_strength"][i]),
+                     micro_regime_transition=ann["micro_regime_transition"][i],
+                     micro_regime_transition_strength=float(ann["micro_regime_transition_strength"][i]))
+            sym[names[i]] = d
+        ctx["symbol_features"] = sym
+        ctx["metadata"] = {
+            "btc_fresh": self.btc_symbol in set(names),
+            "btc_used_for_regime": btc_valid,
+            "fresh_symbols": sorted(sym),
+            "fresh_symbol_count": int(ctx["fresh_count"]),
+        }
+        return ctx

@@ -37,6 +37,8 @@
  *                         strategies/liquidation_sweep_pump.py:255-263
  *   bq_join_returns,   <- the inner join + rolling beta/corr of
  *   bq_beta_corr_pairs    producers/context_evaluator.py:161-194
+ *   bq_store_*         <- MarketStateStore (market_regime/market_state_store.py:14-87)
+ *                         and _compute_symbol_features on its histories
  *   bq_breadth_partial <- the per-symbol sums/counts of
  *                         LiveMarketContextAccumulator._build_context
  *                         market_regime/live_market_context_accumulator.py:135-163
@@ -303,6 +305,52 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
  */
 int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in, int32_t window,
                        double* beta, double* corr, int64_t ld_out, void* stream);
+
+/* ---- device-resident MarketStateStore -------------------------------------- */
+/*
+ * market_regime/market_state_store.py:14-87 kept in HBM: per symbol slot a
+ * ring of the last max_bars closed candles, sorted by timestamp, unique
+ * timestamps (a later update of a timestamp replaces it, keep="last").
+ * Caller-owned buffers (the library allocates nothing):
+ */
+#define BQ_STORE_MAX_BARS 512
+typedef struct bq_store_view {
+  int64_t* ts;                     /* [capacity][max_bars] candle timestamps (ms)        */
+  double*  field[BQ_NUM_INPUTS];   /* open, high, low, close, volume, same layout       */
+  int32_t* head;                   /* [capacity] ring index of the oldest candle        */
+  int32_t* count;                  /* [capacity] candles held (<= max_bars)             */
+  int64_t* last;                   /* [capacity] last closed timestamp (undefined if 0) */
+  int64_t  capacity;
+  int32_t  max_bars;               /* 2 .. BQ_STORE_MAX_BARS                            */
+  int32_t  reserved;
+} bq_store_view;
+/*
+ * MarketStateStore.update for a batch: n_seg runs of candles, run g =
+ * [seg_begin[g], seg_begin[g+1]) all for slot[seg_begin[g]], timestamps
+ * strictly ascending inside a run, one run per slot per call (the caller
+ * sorts and de-duplicates the batch, keep="last"). NaN close / timestamp rows
+ * must already be dropped (market_state_store.py:84). slot, ts, seg_begin and
+ * the five ohlcv arrays are device pointers.
+ */
+int bq_store_update(const bq_store_view* st, const int64_t* slot, const int64_t* ts, const double* const* ohlcv,
+                    const int64_t* seg_begin, int64_t n_seg, void* stream);
+/*
+ * LiveMarketContextAccumulator._compute_symbol_features
+ * (market_regime/live_market_context_accumulator.py:244-297) on the histories
+ * of n_sel slots: feat[BQ_NUM_FEATURES] arrays of n_sel doubles (NULL =
+ * skip; NaN rows where a history has < 2 candles, i.e. the reference's None)
+ * and close_out[n_sel] (latest close). pandas' ewm / roll_mean / roll_var
+ * recurrences are replayed, so values equal pandas' bit for bit.
+ */
+int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_sel, double* const* feat,
+                      double* close_out, void* stream);
+/*
+ * MarketStateStore.get_symbol_history / get_all_histories: time-ordered copy
+ * of n_sel slots into ts_out / out[BQ_NUM_INPUTS] [n_sel][ld_out]
+ * (ld_out >= max_bars; NaN / 0 past each slot's count; NULL = skip).
+ */
+int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,
+                    double* const* out, int64_t ld_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -302,3 +302,88 @@ def symbol_transition_event(prev: str, cur: str) -> str:   # regime_transitions.
     return {"TREND_UP": "ENTERED_TREND_UP", "TREND_DOWN": "ENTERED_TREND_DOWN", "RANGE": "ENTERED_RANGE"}.get(
         cur, "ENTERED_TRANSITIONAL"
     )
+
+
+def roll_mean_replay(vals, window: int, min_periods: int = 1) -> np.ndarray:
+    """pandas 2.3.3 roll_mean for a fixed window, replayed step by step:
+    Kahan add / remove with separate compensations, nobs, the same-value run
+    (result = the value) and sign (neg_ct) rules of calc_mean. The order of
+    floating-point operations is the one bq_store_features replays on the
+    device (the restatement is pinned bit-exact against pandas in
+    tests/test_oracle_golden.py)."""
+    x = np.asarray(vals, dtype=np.float64)
+    out = np.empty(x.size)
+    s = ca = cr = 0.0
+    nobs = neg = same = 0
+    prev = x[0] if x.size else 0.0
+    for i in range(x.size):
+        if i >= window and x[i - window] == x[i - window]:
+            v = x[i - window]
+            nobs -= 1
+            y = -v - cr
+            t = s + y
+            cr = t - s - y
+            s = t
+            neg -= 1 if np.signbit(v) else 0
+        v = x[i]
+        if v == v:
+            nobs += 1
+            y = v - ca
+            t = s + y
+            ca = t - s - y
+            s = t
+            neg += 1 if np.signbit(v) else 0
+            same = same + 1 if v == prev else 1
+            prev = v
+        if nobs >= min_periods and nobs > 0:
+            r = s / nobs
+            if same >= nobs:
+                r = prev
+            elif neg == 0 and r < 0:
+                r = 0.0
+            elif neg == nobs and r > 0:
+                r = 0.0
+        else:
+            r = np.nan
+        out[i] = r
+    return out
+
+
+def roll_var_replay(vals, window: int, min_periods: int = 1, ddof: int = 0) -> np.ndarray:
+    """pandas 2.3.3 roll_var for a fixed window (compensated Welford add /
+    remove, same-value rule -> 0), replayed step by step; see roll_mean_replay."""
+    x = np.asarray(vals, dtype=np.float64)
+    out = np.empty(x.size)
+    nobs = mean = ssq = ca = cr = 0.0
+    same = 0
+    prev = x[0] if x.size else np.nan
+    for i in range(x.size):
+        if i >= window and x[i - window] == x[i - window]:
+            v = x[i - window]
+            nobs -= 1
+            if nobs:
+                pm = mean - cr
+                y = v - cr
+                t = y - mean
+                cr = t + mean - y
+                mean = mean - t / nobs
+                ssq = ssq - (v - pm) * (v - mean)
+            else:
+                mean = ssq = 0.0
+        v = x[i]
+        if v == v:
+            same = same + 1 if v == prev else 1
+            prev = v
+            nobs += 1
+            pm = mean - ca
+            y = v - ca
+            t = y - mean
+            ca = t + mean - y
+            mean = mean + t / nobs if nobs else 0.0
+            ssq = ssq + (v - pm) * (v - mean)
+        if nobs >= min_periods and nobs > ddof:
+            r = 0.0 if (nobs == 1 or same >= nobs) else max(ssq / (nobs - ddof), 0.0)
+        else:
+            r = np.nan
+        out[i] = r
+    return out

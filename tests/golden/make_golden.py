@@ -422,7 +422,101 @@ def child(out_dir: Path) -> None:
         out[f"{k}__topgainer_status"] = np.array(st)
     out["topgainer_keys"] = np.array(tg_keys)
     np.savez(out_dir / "signal_helpers.npz", **out)
+
+    # ---- 9. MarketStateStore + accumulator under a scripted feed ---------------------
+    store_sequence(out_dir, context_dict)
     print("golden fixtures written to", out_dir)
+
+
+def store_sequence(out_dir: Path, context_dict) -> None:
+    """store_sequence.json: a scripted feed (REST history syncs with shuffled,
+    duplicated, NaN and string rows; live ticks with skipped symbols, late
+    corrections and out-of-order candles) replayed through the reference's
+    MarketStateStore.update (market_regime/market_state_store.py:19-31) and
+    LiveMarketContextAccumulator.on_closed_candle / refresh_context_for_timestamp
+    (live_market_context_accumulator.py:38-84). Records every context, the
+    final histories, last-closed timestamps and fresh sets."""
+    import numpy as np
+
+    from market_regime.live_market_context_accumulator import LiveMarketContextAccumulator
+    from market_regime.market_state_store import MarketStateStore
+
+    rng = np.random.default_rng(777)
+    M = 30
+    step = 900_000
+    t0 = 1_760_000_400_000
+    syms = ["BTCUSDT"] + [f"A{i:02d}USDT" for i in range(1, 50)]
+    scale = {s: float(10 ** rng.uniform(-2, 3)) for s in syms}
+    price = {s: scale[s] for s in syms}
+
+    def candle(s, k, jitter=0.0):
+        p = price[s] * float(np.exp(rng.normal(0.0004, 0.006)))
+        price[s] = p
+        o = p * float(np.exp(rng.normal(0, 0.002)))
+        return dict(timestamp=t0 + k * step, open=o, high=max(o, p) * (1 + float(rng.uniform(0, 0.003))),
+                    low=min(o, p) * (1 - float(rng.uniform(0, 0.003))), close=p * (1 + jitter),
+                    volume=float(rng.lognormal(3, 1)))
+
+    store = MarketStateStore(max_bars_per_symbol=M)
+    acc = LiveMarketContextAccumulator(store, btc_symbol="BTCUSDT")
+    ops, contexts = [], []
+    # phase 1: REST history sync, one frame per symbol
+    for s in syms:
+        rows = [candle(s, k) for k in range(45)]
+        for k in rng.choice(45, 3, replace=False):      # later copies of a timestamp win
+            r = dict(rows[k])
+            r["close"] = r["close"] * 1.01
+            rows.append(r)
+        for k in rng.choice(len(rows), 2, replace=False):   # rows without a close are dropped
+            rows[k] = dict(rows[k], close=None)
+        order = rng.permutation(len(rows))
+        rows = [rows[i] for i in order]
+        for r in rows[:5]:                               # wire-style strings
+            r.update({f: (str(v) if v is not None else v) for f, v in r.items() if f != "timestamp"})
+        if s == "A07USDT":                               # open/high/low/volume omitted
+            rows = [dict(timestamp=r["timestamp"], close=r["close"]) for r in rows]
+        ops.append(dict(op="update", symbol=s, rows=rows))
+        store.update(s, pd_frame(rows))
+    # phase 2: live ticks
+    for k in range(45, 53):
+        ts = t0 + k * step
+        active = [s for s in syms if rng.random() > 0.12 or s == "BTCUSDT"]
+        for i in rng.permutation(len(active)):
+            s = active[i]
+            c = candle(s, k)
+            ops.append(dict(op="on_closed_candle", symbol=s, rows=[c]))
+            ctx = context_dict(acc.on_closed_candle(s, c))
+            if ctx is not None:   # per-symbol rows are kept for the refresh contexts only
+                ctx.pop("symbol_features")
+            contexts.append(ctx)
+        if k == 48:   # late corrections of the current candle
+            for s in active[:5]:
+                c = dict(candle(s, k), close=price[s] * 0.97)
+                ops.append(dict(op="update", symbol=s, rows=[c]))
+                store.update(s, c)
+        if k == 50:   # out-of-order older candles (replace inside the ring)
+            for s in active[5:8]:
+                c = candle(s, k - 5)
+                ops.append(dict(op="update", symbol=s, rows=[c]))
+                store.update(s, c)
+        ops.append(dict(op="refresh", ts=ts))
+        contexts.append(context_dict(acc.refresh_context_for_timestamp(ts)))
+    final = {
+        "histories": {s: store.get_symbol_history(s).to_dict(orient="list") for s in syms},
+        "last_closed": {s: store.get_last_closed_timestamp(s) for s in syms},
+        "fresh": {str(t0 + k * step): sorted(store.get_fresh_symbols(t0 + k * step)) for k in range(40, 53)},
+        "tracked": store.get_tracked_symbols(),
+        "latest_context_ts": (acc.get_latest_context().timestamp if acc.get_latest_context() else None),
+    }
+    with open(out_dir / "store_sequence.json", "w") as f:
+        json.dump(dict(max_bars=M, btc="BTCUSDT", ops=ops, contexts=contexts, final=final), f,
+                  separators=(",", ":"), default=float)
+
+
+def pd_frame(rows):
+    import pandas as pd
+
+    return pd.DataFrame(rows)
 
 
 def main() -> None:

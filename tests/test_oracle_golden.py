@@ -91,3 +91,24 @@ def test_sma_rsi_matches_reference_helper():
         np.testing.assert_allclose(got[m], want[m], rtol=1e-13, atol=1e-12, err_msg=k)
         # the helper refuses fewer than window+1 closes; the column is NaN for < window
         assert np.isnan(ours[:13]).all()
+
+
+def test_rolling_replays_are_bit_exact_vs_pandas():
+    """The step-by-step roll_mean / roll_var restatements that bq_store_features
+    replays on the device equal pandas 2.3.3 bit for bit (random walks,
+    constant runs, rounded prices, windows 14 and 20, min_periods 1)."""
+    from oracle.market_ref import roll_mean_replay, roll_var_replay
+
+    rng = np.random.default_rng(0)
+    for trial in range(120):
+        n = int(rng.integers(1, 260))
+        x = 100 * np.exp(np.cumsum(rng.normal(0, 0.01, n)))
+        if trial % 3 == 0:
+            k = int(rng.integers(0, n))
+            x[k : k + 25] = x[k]
+        if trial % 5 == 0:
+            x = np.round(x, 2)
+        for w in (14, 20):
+            s = pd.Series(x).rolling(w, min_periods=1)
+            np.testing.assert_array_equal(roll_mean_replay(x, w), s.mean().to_numpy())
+            np.testing.assert_array_equal(roll_var_replay(x, w), s.var(ddof=0).to_numpy())
