@@ -5,7 +5,11 @@ ARCH      ?= gfx950
 HIPFLAGS  ?= -O3 --offload-arch=$(ARCH) -ffp-contract=off -fPIC -std=c++17 \
              -Iinclude -Ibinquant_amd/csrc -Wall -Wno-unused-function
 SRCS      := $(wildcard binquant_amd/csrc/*.hip)
-OBJS      := $(patsubst binquant_amd/csrc/%.hip,build/%.o,$(SRCS))
+CXXSRCS   := $(wildcard binquant_amd/csrc/*.cpp)
+OBJS      := $(patsubst binquant_amd/csrc/%.hip,build/%.o,$(SRCS)) \
+             $(patsubst binquant_amd/csrc/%.cpp,build/%.o,$(CXXSRCS))
+CXX       ?= g++
+CXXFLAGS  ?= -O3 -fPIC -std=c++17 -Iinclude -Wall
 LIB       := binquant_amd/lib/libbinquant_amd.so
 
 all: $(LIB)
@@ -13,6 +17,11 @@ all: $(LIB)
 build/%.o: binquant_amd/csrc/%.hip binquant_amd/csrc/bq_device.h include/binquant_amd.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# host-only sources (wire-format ingest)
+build/%.o: binquant_amd/csrc/%.cpp include/binquant_amd.h
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
 	@mkdir -p binquant_amd/lib

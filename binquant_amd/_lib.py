@@ -136,6 +136,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
+    "bq_parse_kline_events": (ctypes.c_int, [ctypes.c_char_p, _I64, _I64, _P, _I64, _P, _P, _PP, _P, _P, _P]),
 }
 
 

@@ -342,7 +342,12 @@ class DeviceLiveMarketContextAccumulator:
         red[npart] = float(n_fresh)
         red[npart + 1] = float(store.n_tracked - (0 if btc_counted or btc_slot is None else 1))
         if self._sharded():
-            dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
+            if dist.get_backend(self.group) == "gloo":   # CPU rehearsal of the sharded path
+                red_c = red.cpu()
+                dist.all_reduce(red_c, op=dist.ReduceOp.SUM, group=self.group)
+                red = red_c
+            else:   # RCCL over xGMI: one all-reduce of 12 doubles
+                dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
         red_h = red.cpu().numpy()
         total_fresh, total_tracked = int(red_h[npart]), int(red_h[npart + 1])
         required = max(REQUIRED_FRESH_SYMBOLS, ceil(total_tracked * MIN_COVERAGE_RATIO))

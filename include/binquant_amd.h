@@ -39,6 +39,8 @@
  *   bq_beta_corr_pairs    producers/context_evaluator.py:161-194
  *   bq_store_*         <- MarketStateStore (market_regime/market_state_store.py:14-87)
  *                         and _compute_symbol_features on its histories
+ *   bq_parse_kline_events <- json.loads + KlineProduceModel of the websocket
+ *                         frames, producers/klines_connector.py:77-164 (host)
  *   bq_breadth_partial <- the per-symbol sums/counts of
  *                         LiveMarketContextAccumulator._build_context
  *                         market_regime/live_market_context_accumulator.py:135-163
@@ -351,6 +353,21 @@ int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_s
  */
 int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,
                     double* const* out, int64_t ld_out, void* stream);
+
+/* ---- wire-format ingest (host) ------------------------------------------------ */
+/*
+ * Binance kline websocket events (one JSON object per '\n'-separated frame,
+ * as decoded at producers/klines_connector.py:77-90 and copied into a
+ * KlineProduceModel at :148-164) -> arrays, in one native pass: sym
+ * [max_rows][sym_stride] NUL-terminated symbols ("s"), open_time ("t"),
+ * close_time ("T"), ohlcv[5] ("o","h","l","c","v" via strtod: the same
+ * doubles as Python float()), closed ("x"). HOST pointers. Non-kline frames
+ * are skipped; malformed kline frames are counted in n_bad and skipped.
+ * Returns BQ_EINVAL (with n_rows filled so far) if max_rows is too small.
+ */
+int bq_parse_kline_events(const char* buf, int64_t len, int64_t max_rows, char* sym, int64_t sym_stride,
+                          int64_t* open_time, int64_t* close_time, double* const* ohlcv, uint8_t* closed,
+                          int64_t* n_rows, int64_t* n_bad);
 
 #ifdef __cplusplus
 }
