@@ -60,6 +60,8 @@ STORE_MAX_BARS = 512
 AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
+ROLL_EWM = 8
+MAX_ROLL_JOBS = 16
 
 
 class BqParams(ctypes.Structure):
@@ -94,6 +96,23 @@ class BqStoreView(ctypes.Structure):
         ("capacity", ctypes.c_int64),
         ("max_bars", ctypes.c_int32),
         ("reserved", ctypes.c_int32),
+    ]
+
+
+class BqRollJob(ctypes.Structure):
+    """Mirror of ``bq_roll_job`` (include/binquant_amd.h)."""
+
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("ld_in", ctypes.c_int64),
+        ("ld_out", ctypes.c_int64),
+        ("window", ctypes.c_int32),
+        ("min_periods", ctypes.c_int32),
+        ("shift", ctypes.c_int32),
+        ("mode", ctypes.c_int32),
+        ("q", ctypes.c_double),
+        ("alpha", ctypes.c_double),
     ]
 
 
@@ -136,6 +155,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
+    "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
     "bq_parse_kline_events": (ctypes.c_int, [ctypes.c_char_p, _I64, _I64, _P, _I64, _P, _P, _PP, _P, _P, _P]),
 }
 

@@ -228,7 +228,7 @@ __device__ __forceinline__ void stage_load(const double* __restrict__ base, int6
     const int e = lane + WAVE * k;
     const int64_t s = sym0 + e / CT;
     const int t = t0 + e % CT;
-    r[k] = (s < S && t < T) ? base[s * ld + t] : qnan();
+    r[k] = (s < S && t >= 0 && t < T) ? base[s * ld + t] : qnan();
   }
 }
 

@@ -1,39 +1,47 @@
 // Rolling-window statistics with pandas semantics, for the strategy feature
 // pipelines:
 //
-//   bq_rolling: x.shift(shift).rolling(window, min_periods).{quantile(q),
-//               median(), mean(), sum()} — NaNs are skipped and counted out
-//               of nobs, the result is NaN while nobs < min_periods.
-//     quantile: pandas roll_quantile, linear interpolation
-//               (vlow + (vhigh - vlow) * (q*(nobs-1) - idx)); q = 0 / 1 give
-//               rolling min / max;
-//     median:   pandas roll_median_c (mean of the two middle values for even
-//               nobs);
-//     mean:     sum / nobs with pandas' same-value rule;
-//     sum:      Kahan-compensated like pandas add_sum / remove_sum, same-value
-//               rule (value * nobs), 0 for an empty window when min_periods = 0;
-//     var/std:  ddof 1, pandas' compensated Welford update, same-value rule -> 0.
+//   bq_rolling: x.shift(shift).rolling(window, min_periods).<mode>()
+//     mean / sum / var / std (ddof 1 or 0): pandas' own window recurrences
+//       REPLAYED over the whole row (pandas/_libs/window/aggregations.pyx,
+//       2.3.3): roll_sum / roll_mean keep a Kahan sum with separate add and
+//       remove compensations, the signbit count (mean clamps) and the
+//       same-value run (result = the value / value * nobs); roll_var a
+//       compensated Welford mean + ssqdm with the same-value rule -> 0. Each
+//       step removes the leaving value, then adds the entering one. The
+//       outputs therefore equal pandas' bit for bit (restatement pinned in
+//       tests/test_oracle_golden.py; kernels in tests/test_strategies_gpu.py).
+//     quantile(q) (linear interpolation), median (roll_median_c), and
+//       max / min (q = 1 / 0): order statistics of the window's non-NaN
+//       values — a pure function of the window multiset, so any algorithm
+//       that selects the same ranks is exact.
 //     Used by ActivityBurstPump.compute_indicators
 //     (strategies/activity_burst_pump.py:58-63 median(19), :134-139
 //     quantile(0.92, 80), :147-152 max(3)), LiquidationSweepPump.compute_pump_score
 //     (strategies/liquidation_sweep_pump.py:218-245: mean(20), max/min(6),
-//     quantile(0.80, 48)), FailedSpikeFade (quantile(0.85, 60)).
+//     quantile(0.80, 48)), FailedSpikeFade (quantile(0.85, 60), rolling
+//     mean/std(12, 8, 20, 10), sums(2, 3, 5)).
 //
 //   bq_ewm: x.ewm(alpha, adjust=False, min_periods).mean() with
 //           ignore_na=False NaN gaps (the BTC left-merge of
 //           liquidation_sweep_pump.py:255-267 and the Wilder ATR/RSI of
-//           :215-217 and mean_reversion_fade.py:88-109).
+//           :215-217 and mean_reversion_fade.py:88-109) — pandas' exact
+//           recursion, bit for bit.
 //
-// Mapping (bq_rolling): order statistics are not prefix-able, so each lane
-// owns a run of SEG consecutive outputs of one symbol and keeps its window
-// SORTED in LDS (lane-interleaved: element j of lane l at j*64 + l, so a wave's
-// accesses hit 64 distinct banks). Per step it binary-searches the leaving and
-// the entering value and shifts only the span between them. The window is
-// rebuilt from the w values before each run (warm-up), so runs are
-// independent: S * ceil(T / SEG) lanes in flight.
-//
-// Mapping (bq_ewm): lane = symbol, one sequential pass with pandas' exact
-// update (bit-for-bit the pandas recursion).
+// Mappings (both HBM-friendly; no lane walks memory on its own):
+//   replay (mean/sum/var/std, ewm): lane = symbol, one wave per 64 symbols.
+//     Chunks of RP_CT candles are read coalesced (RP_CT lanes cover one
+//     symbol's contiguous bytes), transposed through LDS, and the next chunk
+//     is in flight while the current one is replayed; results leave through
+//     an LDS tile as coalesced row segments. The staged chunks stay in an
+//     LDS ring covering window + shift, so the value leaving the window is
+//     an LDS read and every input byte crosses HBM once.
+//   rank (quantile/median/max/min): lane = (symbol, segment of the row).
+//     Each lane keeps its window SORTED IN REGISTERS (W slots, +inf padding):
+//     a removal / insertion is a branch-free pass of compares and selects over
+//     the W slots (no LDS, no serial shift loop), so throughput scales with
+//     VALU width instead of LDS latency. A segment first rebuilds its window
+//     from the w values before it, so segments are independent.
 #include "bq_device.h"
 #include "binquant_amd.h"
 
@@ -41,270 +49,434 @@
 
 namespace bq {
 
-constexpr int RW_LANES = 64;           // one wave per workgroup
 constexpr int RW_MAXW = BQ_MAX_ROLLING_WINDOW;
-constexpr int RW_SEG = 256;            // outputs per lane
+constexpr int RW_MAXSHIFT = 32;
 
-struct RollArgs {
+constexpr int RW_MAXJOBS = BQ_MAX_ROLL_JOBS;
+
+// one series of a batch (bq_roll_job); jobs of one launch share [S][T]
+struct RollJob {
   const double* x;
   double* out;
-  int64_t S, ld_in, ld_out;
-  int T, win, minp, shift, mode, nseg;
-  double q;
+  int64_t ld_in, ld_out;
+  int win, minp, shift, mode, seg, nseg;
+  double q, alpha;
 };
 
-// lane-interleaved sorted window
-struct Win {
-  double* base;   // LDS base of this wave's windows
-  int lane, n;
-  __device__ __forceinline__ double& at(int j) const { return base[j * RW_LANES + lane]; }
-  // first index with at(i) >= v  (lower bound)
-  __device__ __forceinline__ int lower(double v) const {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (at(mid) < v) lo = mid + 1;
-      else hi = mid;
-    }
-    return lo;
-  }
-  __device__ __forceinline__ void insert(double v) {
-    const int p = lower(v);
-    for (int j = n; j > p; --j) at(j) = at(j - 1);
-    at(p) = v;
-    ++n;
-  }
-  __device__ __forceinline__ void erase(double v) {   // v is present
-    const int p = lower(v);
-    for (int j = p; j < n - 1; ++j) at(j) = at(j + 1);
-    --n;
-  }
-  // erase `old` and insert `nw` with one shift of the span between them
-  __device__ __forceinline__ void replace(double old, double nw) {
-    const int po = lower(old);
-    if (nw >= old) {
-      // move elements (po, pn) one slot down, new value at pn-1
-      int p = po;
-      while (p + 1 < n && at(p + 1) < nw) {
-        at(p) = at(p + 1);
-        ++p;
-      }
-      at(p) = nw;
-    } else {
-      int p = po;
-      while (p > 0 && at(p - 1) > nw) {
-        at(p) = at(p - 1);
-        --p;
-      }
-      at(p) = nw;
-    }
-  }
+struct RollBatch {
+  RollJob j[RW_MAXJOBS];
+  int64_t S;
+  int T;
 };
 
-__global__ __launch_bounds__(RW_LANES) void rolling_kernel(const RollArgs A) {
-  __shared__ double sw[RW_MAXW * RW_LANES];
-  const int lane = threadIdx.x;
-  const int64_t item = (int64_t)blockIdx.x * RW_LANES + lane;
-  if (item >= A.S * A.nseg) return;   // whole lane idle; no barriers below
-  const int64_t sym = item / A.nseg;
-  const int seg = (int)(item % A.nseg);
-  const int T = A.T, w = A.win, sh = A.shift;
-  const double* __restrict__ x = A.x + sym * A.ld_in;
-  double* __restrict__ out = A.out + sym * A.ld_out;
-  const int t_begin = seg * RW_SEG;
-  const int t_end = min(T, t_begin + RW_SEG);
-  // value entering the window of output t: x[t - shift] (NaN outside [0, T))
-  auto val = [&](int t) -> double {
-    const int i = t - sh;
-    return (i >= 0 && i < T) ? x[i] : qnan();
-  };
-  Win W{sw, lane, 0};
-  // Moment modes follow pandas' window aggregations update for update
-  // (pandas/_libs/window/aggregations.pyx, 2.3.3): add_sum/remove_sum and
-  // add_mean/remove_mean keep a Kahan sum with SEPARATE add and remove
-  // compensations; add_var/remove_var a compensated Welford mean + ssqdm.
-  // Each step removes the leaving value, then adds the entering one.
-  const bool welford = A.mode >= BQ_ROLL_VAR;
-  double sum = 0.0, c_add = 0.0, c_rem = 0.0, last = qnan();
-  double mean = 0.0, ssq = 0.0;
-  int neg = 0, run = 0;   // signbit count (mean clamps); same-value run
-  auto add = [&](double v) {
-    ++W.n;
+// ---- replay kernels (lane = symbol) --------------------------------------------------
+constexpr int RP_CT = 32;
+
+// pandas roll_sum / roll_mean / roll_var state, updated value by value
+struct Moments {
+  double sum, c_add, c_rem;     // Kahan sum (separate compensations)
+  double vn, mean, ssq, v_add, v_rem;   // Welford (nobs as float64, as pandas)
+  double prev;
+  int nobs, neg, same;
+  __device__ __forceinline__ void init(double first) {
+    sum = c_add = c_rem = 0.0;
+    vn = mean = ssq = v_add = v_rem = 0.0;
+    prev = first;
+    nobs = neg = same = 0;
+  }
+  __device__ __forceinline__ void add(double v, bool welford) {
+    if (v != v) return;
+    ++nobs;
     if (welford) {
-      const double prev_mean = mean - c_add;
-      const double y = v - c_add;
+      vn += 1.0;
+      const double pm = mean - v_add;
+      const double y = v - v_add;
       const double t = y - mean;
-      c_add = (t + mean) - y;
-      mean = mean + t / (double)W.n;
-      ssq = ssq + (v - prev_mean) * (v - mean);
+      v_add = t + mean - y;
+      mean = vn != 0.0 ? mean + t / vn : 0.0;
+      ssq = ssq + (v - pm) * (v - mean);
     } else {
       const double y = v - c_add;
       const double t = sum + y;
-      c_add = (t - sum) - y;
+      c_add = t - sum - y;
       sum = t;
       neg += signbit(v) ? 1 : 0;
     }
-    run = v == last ? run + 1 : 1;   // pandas counts equal values as they are added
-    last = v;
-  };
-  auto remove = [&](double v) {
-    --W.n;
+    same = (v == prev) ? same + 1 : 1;
+    prev = v;
+  }
+  __device__ __forceinline__ void remove(double v, bool welford) {
+    if (v != v) return;
+    --nobs;
     if (welford) {
-      if (W.n) {
-        const double prev_mean = mean - c_rem;
-        const double y = v - c_rem;
+      vn -= 1.0;
+      if (vn != 0.0) {
+        const double pm = mean - v_rem;
+        const double y = v - v_rem;
         const double t = y - mean;
-        c_rem = (t + mean) - y;
-        mean = mean - t / (double)W.n;
-        ssq = ssq - (v - prev_mean) * (v - mean);
+        v_rem = t + mean - y;
+        mean = mean - t / vn;
+        ssq = ssq - (v - pm) * (v - mean);
       } else {
-        mean = 0.0;
-        ssq = 0.0;
+        mean = ssq = 0.0;
       }
     } else {
       const double y = -v - c_rem;
       const double t = sum + y;
-      c_rem = (t - sum) - y;
+      c_rem = t - sum - y;
       sum = t;
       neg -= signbit(v) ? 1 : 0;
     }
-  };
-  // warm-up: window of output t_begin - 1, i.e. values of t in [t_begin - w, t_begin)
-  for (int t = t_begin - w; t < t_begin; ++t) {
-    const double v = val(t);
-    if (v == v) {
-      if (A.mode <= 1) {
-        W.insert(v);
-        run = v == last ? run + 1 : 1;
-        last = v;
-      } else {
-        add(v);
+  }
+  __device__ __forceinline__ double result(int mode, int minp) const {
+    switch (mode) {
+      case BQ_ROLL_SUM:   // calc_sum
+        if (nobs == 0 && minp == 0) return 0.0;
+        if (nobs < minp) return qnan();
+        return same >= nobs ? prev * (double)nobs : sum;
+      case BQ_ROLL_MEAN: {   // calc_mean
+        if (nobs < minp || nobs <= 0) return qnan();
+        double r = sum / (double)nobs;
+        if (same >= nobs) r = prev;
+        else if (neg == 0 && r < 0.0) r = 0.0;
+        else if (neg == nobs && r > 0.0) r = 0.0;
+        return r;
+      }
+      default: {   // calc_var (ddof 1 or 0), std = sqrt
+        const double ddof = (mode == BQ_ROLL_VAR || mode == BQ_ROLL_STD) ? 1.0 : 0.0;
+        double r;
+        if (vn >= (double)minp && vn > ddof) {
+          if (vn == 1.0 || (double)same >= vn) r = 0.0;
+          else {
+            r = ssq / (vn - ddof);
+            r = r < 0.0 ? 0.0 : r;
+          }
+        } else {
+          r = qnan();
+        }
+        return (mode == BQ_ROLL_STD || mode == BQ_ROLL_STD0) ? sqrt(r) : r;
       }
     }
   }
-  for (int t = t_begin; t < t_end; ++t) {
-    const double vn = val(t), vo = val(t - w);
-    const bool in = vn == vn, outv = vo == vo;
-    if (A.mode <= 1) {
-      if (in && outv) W.replace(vo, vn);
-      else if (in) W.insert(vn);
-      else if (outv) W.erase(vo);
-    } else {
-      if (outv) remove(vo);
-      if (in) add(vn);
-    }
-    const int n = W.n;
-    double r;
-    if (n == 0 && A.minp == 0 && A.mode == BQ_ROLL_SUM) r = 0.0;
-    else if (n < A.minp || n == 0) r = qnan();
-    else if (A.mode == BQ_ROLL_QUANTILE) {
-      if (n == 1) r = W.at(0);
-      else {
-        const double idxf = A.q * (double)(n - 1);
-        const int idx = (int)idxf;
-        if ((double)idx == idxf) r = W.at(idx);
-        else {
-          const double lo = W.at(idx), hi = W.at(idx + 1);
-          r = lo + (hi - lo) * (idxf - (double)idx);
+};
+
+// LDS: a ring of the last `ring` (a power of two) input chunks, x-index
+// aligned, + one result
+// tile; the ring covers window + shift, so the leaving value is an LDS read
+// and every input byte crosses HBM once.
+__global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int ring) {
+  const RollJob& A = B.j[blockIdx.y];   // wave-uniform: scalar kernarg loads
+  const bool EWM = A.mode == BQ_ROLL_EWM;
+  extern __shared__ double smem[];
+  constexpr int TILE = RP_CT * STG_PITCH;
+  double* sRes = smem + ring * TILE;
+  const int lane = threadIdx.x;
+  const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
+  const int64_t S = B.S;
+  const int T = B.T, w = A.win, sh = A.shift;
+  const bool welford = A.mode >= BQ_ROLL_VAR;
+  auto xval = [&](int i) -> double {   // x[i] of this lane's symbol, i within the ring
+    return i < 0 ? qnan() : smem[((i / RP_CT) & (ring - 1)) * TILE + (i % RP_CT) * STG_PITCH + lane];
+  };
+  double ri[RP_CT];
+  stage_load<RP_CT>(A.x, A.ld_in, sym0, S, 0, T, lane, ri);
+  Moments m;
+  m.init(0.0);
+  // ewm state (pandas ewm, adjust=False, ignore_na=False)
+  double weighted = qnan(), old_wt = 1.0;
+  int nobs = 0;
+  const double alpha = A.alpha, om = 1.0 - alpha;
+  for (int t0 = 0; t0 < T; t0 += RP_CT) {
+    stage_put<RP_CT>(smem + ((t0 / RP_CT) & (ring - 1)) * TILE, lane, ri);
+    __syncthreads();
+    if (t0 + RP_CT < T)   // next chunk in flight during this one's replay
+      stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT, T, lane, ri);
+    auto step = [&](int j) {
+      const int t = t0 + j;
+      const int x = j * STG_PITCH + lane;
+      const double v_in = xval(t - sh);
+      double res;
+      if (EWM) {
+        if (t == 0) {
+          weighted = v_in;
+          nobs = v_in == v_in;
+        } else {
+          const bool obs = v_in == v_in;
+          nobs += obs;
+          if (weighted == weighted) {
+            old_wt *= om;
+            if (obs) {
+              if (weighted != v_in) {
+                weighted = old_wt * weighted + alpha * v_in;
+                weighted /= old_wt + alpha;
+              }
+              old_wt = 1.0;
+            }
+          } else if (obs) {
+            weighted = v_in;
+          }
         }
+        res = nobs >= A.minp ? weighted : qnan();
+      } else {
+        if (t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
+        if (t >= w) m.remove(xval(t - sh - w), welford);
+        m.add(v_in, welford);
+        res = m.result(A.mode, A.minp);
       }
-    } else if (A.mode == BQ_ROLL_MEDIAN) {
-      r = (n & 1) ? W.at(n >> 1) : (W.at((n >> 1) - 1) + W.at(n >> 1)) / 2.0;
-    } else if (A.mode == BQ_ROLL_MEAN) {
-      r = run >= n ? last : sum / (double)n;   // same-value rule
-      if (neg == 0 && r < 0.0) r = 0.0;        // pandas calc_mean sign clamps
-      else if (neg == n && r > 0.0) r = 0.0;
-    } else if (A.mode == BQ_ROLL_SUM) {
-      r = run >= n ? last * (double)n : sum;   // same-value rule
-    } else {   // var / std (pandas calc_var), ddof 1 or 0
-      const int ddof = (A.mode == BQ_ROLL_VAR || A.mode == BQ_ROLL_STD) ? 1 : 0;
-      double var;
-      if (n <= ddof) var = qnan();
-      else if (n == 1 || run >= n) var = 0.0;
+      sRes[x] = res;
+    };
+    if (t0 + RP_CT <= T) {
+      // full chunk: unrolled, so each step's result / LDS traffic overlaps
+      // the next step's (short) dependent state update
+#pragma unroll
+      for (int j = 0; j < RP_CT; ++j) step(j);
+    } else {
+      for (int j = 0; j < T - t0; ++j) step(j);
+    }
+    __syncthreads();
+    stage_store<RP_CT>(sRes, A.out, A.ld_out, sym0, S, t0, T, lane);
+  }
+}
+
+// ---- rank kernels (lane = symbol x segment, sorted window in registers) -----------
+template <int W>
+struct SortedWin {
+  double a[W];
+  int n;
+  __device__ __forceinline__ void clear() {
+#pragma unroll
+    for (int i = 0; i < W; ++i) a[i] = __builtin_inf();
+    n = 0;
+  }
+  // number of stored values < v (padding is +inf, never counted for finite v)
+  __device__ __forceinline__ int rank(double v) const {
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) p += a[i] < v ? 1 : 0;
+    return p;
+  }
+  __device__ __forceinline__ void insert(double v) {
+    const int p = rank(v);
+#pragma unroll
+    for (int i = W - 1; i > 0; --i) a[i] = i > p ? a[i - 1] : (i == p ? v : a[i]);
+    a[0] = p == 0 ? v : a[0];
+    ++n;
+  }
+  __device__ __forceinline__ void erase(double v) {   // v is stored
+    const int p = rank(v);
+#pragma unroll
+    for (int i = 0; i < W - 1; ++i) a[i] = i >= p ? a[i + 1] : a[i];
+    a[W - 1] = __builtin_inf();
+    --n;
+  }
+  // a[k] for a run-time k: a masked OR over the slots (a select chain here is
+  // folded by the compiler into one dynamically indexed load, which would
+  // push the whole window out of registers into scratch)
+  __device__ __forceinline__ double get(int k) const {
+    unsigned long long r = 0;
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      const unsigned long long m = 0ull - (unsigned long long)(i == k);
+      r |= m & (unsigned long long)__double_as_longlong(a[i]);
+    }
+    return __longlong_as_double((long long)r);
+  }
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
+  const RollJob& A = B.j[blockIdx.y];
+  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  // consecutive lanes: consecutive symbols of one segment
+  const int64_t sym = item % B.S;
+  const int seg = (int)(item / B.S);
+  if (seg >= A.nseg) return;
+  const double* __restrict__ x = A.x + sym * A.ld_in;
+  double* __restrict__ out = A.out + sym * A.ld_out;
+  const int T = B.T, w = A.win, sh = A.shift;
+  const int t_begin = seg * A.seg, t_end = min(T, t_begin + A.seg);
+  auto val = [&](int t) -> double {
+    const int i = t - sh;
+    return (i >= 0 && i < T) ? x[i] : qnan();
+  };
+  SortedWin<W> win;
+  win.clear();
+  const int t_start = max(0, t_begin - w + 1);   // rebuild the window of t_begin
+  // values leave only once they were inserted by this lane (t - w >= t_start)
+  double nx_in = val(t_start), nx_out = qnan();
+  for (int t = t_start; t < t_end; ++t) {
+    const double vin = nx_in, vout = nx_out;
+    nx_in = val(t + 1);   // next step's values, in flight
+    nx_out = t + 1 - w >= t_start ? val(t + 1 - w) : qnan();
+    if (vout == vout) win.erase(vout);
+    if (vin == vin) win.insert(vin);
+    if (t < t_begin) continue;
+    const int n = win.n;
+    double r;
+    if (n < A.minp || n == 0) r = qnan();
+    else if (A.mode == BQ_ROLL_MEDIAN) {
+      const int h = n >> 1;
+      if (n & 1) r = win.get(h);
       else {
-        var = ssq / (double)(n - ddof);
-        var = var < 0.0 ? 0.0 : var;
+        r = (win.get(h - 1) + win.get(h)) / 2.0;
       }
-      r = (A.mode == BQ_ROLL_VAR || A.mode == BQ_ROLL_VAR0) ? var : sqrt(var);
+    } else if (n == 1) {
+      r = win.a[0];
+    } else {   // roll_quantile, linear interpolation
+      const double idxf = A.q * (double)(n - 1);
+      const int idx = (int)idxf;
+      if ((double)idx == idxf) r = win.get(idx);
+      else {
+        const double lo = win.get(idx), hi = win.get(idx + 1);
+        r = lo + (hi - lo) * (idxf - (double)idx);
+      }
     }
     out[t] = r;
   }
 }
 
-// ---- ewm(alpha, adjust=False, ignore_na=False, min_periods) ---------------------
-__global__ __launch_bounds__(256) void ewm_kernel(const double* __restrict__ x, double* __restrict__ out, int64_t S,
-                                                  int T, int64_t ld_in, int64_t ld_out, double alpha, int minp) {
-  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (s >= S) return;
-  const double* r = x + s * ld_in;
-  double* o = out + s * ld_out;
-  const double om = 1.0 - alpha;
-  double weighted = r[0];
-  int nobs = weighted == weighted;
-  double old_wt = 1.0;
-  o[0] = nobs >= minp ? weighted : qnan();
-  for (int i = 1; i < T; ++i) {
-    const double cur = r[i];
-    const bool obs = cur == cur;
-    nobs += obs;
-    if (weighted == weighted) {
-      old_wt *= om;
-      if (obs) {
-        if (weighted != cur) {
-          weighted = old_wt * weighted + alpha * cur;
-          weighted /= old_wt + alpha;
-        }
-        old_wt = 1.0;
-      }
-    } else if (obs) {
-      weighted = cur;
-    }
-    o[i] = nobs >= minp ? weighted : qnan();
-  }
+}  // namespace bq
+
+namespace {
+
+bool job_ok(const bq_roll_job& j, int64_t T) {
+  if (!j.x || !j.out || j.ld_in < T || j.ld_out < T || j.min_periods < 0) return false;
+  if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
+  return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
+         j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0 && j.q >= 0.0 && j.q <= 1.0;
 }
 
-}  // namespace bq
+int rank_bucket(int w) {
+  return w <= 8 ? 0 : w <= 24 ? 1 : w <= 48 ? 2 : w <= 64 ? 3 : w <= 80 ? 4 : 5;
+}
+
+template <int W>
+void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t st) {
+  const unsigned blocks = (unsigned)((max_items + 255) / 256);
+  hipLaunchKernelGGL(bq::rank_kernel<W>, dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+}
+
+}  // namespace
 
 extern "C" {
 
+int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream) {
+  using namespace bq;
+  if (!jobs || n_jobs < 0 || S < 0 || T < 0 || T > 0x7fffffff) return BQ_EINVAL;
+  for (int i = 0; i < n_jobs; ++i)
+    if (!job_ok(jobs[i], T)) return BQ_EINVAL;
+  if (S == 0 || T == 0 || n_jobs == 0) return BQ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // replay jobs (moments, ewm): lane = symbol; rank jobs grouped by window size
+  RollBatch rep;
+  memset(&rep, 0, sizeof(rep));
+  rep.S = S;
+  rep.T = (int)T;
+  int nrep = 0;
+  RollBatch rank[6];
+  int nrank[6] = {0, 0, 0, 0, 0, 0};
+  int64_t rank_items[6] = {0, 0, 0, 0, 0, 0};
+  for (int b = 0; b < 6; ++b) {
+    memset(&rank[b], 0, sizeof(RollBatch));
+    rank[b].S = S;
+    rank[b].T = (int)T;
+  }
+  int max_back = 0;   // window + shift of the replay jobs in the batch
+  auto flush_rep = [&]() {
+    if (!nrep) return;
+    int ring = 1;
+    while (ring < (max_back + RP_CT - 1) / RP_CT + 1) ring <<= 1;
+    const size_t lds = (size_t)(ring + 1) * RP_CT * STG_PITCH * sizeof(double);
+    static bool lds_opt_in = false;   // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+    if (!lds_opt_in) {
+      hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      lds_opt_in = true;
+    }
+    hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
+                       rep, ring);
+    nrep = 0;
+    max_back = 0;
+  };
+  auto flush_rank = [&](int b) {
+    if (!nrank[b]) return;
+    switch (b) {
+      case 0: launch_rank<8>(rank[b], nrank[b], rank_items[b], st); break;
+      case 1: launch_rank<24>(rank[b], nrank[b], rank_items[b], st); break;
+      case 2: launch_rank<48>(rank[b], nrank[b], rank_items[b], st); break;
+      case 3: launch_rank<64>(rank[b], nrank[b], rank_items[b], st); break;
+      case 4: launch_rank<80>(rank[b], nrank[b], rank_items[b], st); break;
+      default: launch_rank<96>(rank[b], nrank[b], rank_items[b], st);
+    }
+    nrank[b] = 0;
+    rank_items[b] = 0;
+  };
+  for (int i = 0; i < n_jobs; ++i) {
+    const bq_roll_job& in = jobs[i];
+    RollJob J;
+    memset(&J, 0, sizeof(J));
+    J.x = in.x;
+    J.out = in.out;
+    J.ld_in = in.ld_in;
+    J.ld_out = in.ld_out;
+    J.win = in.window;
+    J.minp = in.min_periods;
+    J.shift = in.shift;
+    J.mode = in.mode;
+    J.q = in.q;
+    J.alpha = in.alpha;
+    if (in.mode >= BQ_ROLL_MEAN) {   // moments / ewm: exact replay
+      const int back = in.mode == BQ_ROLL_EWM ? 0 : in.window + in.shift;
+      max_back = back > max_back ? back : max_back;
+      rep.j[nrep++] = J;
+      if (nrep == RW_MAXJOBS) flush_rep();
+    } else {
+      // segments: enough lanes to fill the chip (~32k), each >= 4 windows long
+      const int64_t want = (32768 + S - 1) / S;
+      int seg = (int)((T + want - 1) / want);
+      seg = seg < 4 * in.window ? 4 * in.window : seg;
+      J.seg = seg;
+      J.nseg = (int)((T + seg - 1) / seg);
+      const int b = rank_bucket(in.window);
+      rank[b].j[nrank[b]++] = J;
+      const int64_t items = S * (int64_t)J.nseg;
+      rank_items[b] = items > rank_items[b] ? items : rank_items[b];
+      if (nrank[b] == RW_MAXJOBS) flush_rank(b);
+    }
+  }
+  flush_rep();
+  for (int b = 0; b < 6; ++b) flush_rank(b);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
 int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream) {
-  using namespace bq;
-  if (!x || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || window < 1 || window > RW_MAXW ||
-      min_periods < 0 || shift < 0 || mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0 || !(q >= 0.0 && q <= 1.0) ||
-      T > 0x7fffffff)
-    return BQ_EINVAL;
-  if (S == 0 || T == 0) return BQ_OK;
-  RollArgs A;
-  A.x = x;
-  A.out = out;
-  A.S = S;
-  A.ld_in = ld_in;
-  A.ld_out = ld_out;
-  A.T = (int)T;
-  A.win = window;
-  A.minp = min_periods;
-  A.shift = shift;
-  A.mode = mode;
-  A.q = q;
-  A.nseg = (int)((T + RW_SEG - 1) / RW_SEG);
-  const int64_t items = S * (int64_t)A.nseg;
-  const unsigned blocks = (unsigned)((items + RW_LANES - 1) / RW_LANES);
-  hipLaunchKernelGGL(rolling_kernel, dim3(blocks), dim3(RW_LANES), 0, (hipStream_t)stream, A);
-  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+  if (mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0) return BQ_EINVAL;
+  bq_roll_job j;
+  memset(&j, 0, sizeof(j));
+  j.x = x;
+  j.out = out;
+  j.ld_in = ld_in;
+  j.ld_out = ld_out;
+  j.window = window;
+  j.min_periods = min_periods;
+  j.shift = shift;
+  j.mode = mode;
+  j.q = q;
+  return bq_rolling_batch(&j, 1, S, T, stream);
 }
 
 int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, int32_t min_periods, double* out,
            int64_t ld_out, void* stream) {
-  using namespace bq;
-  if (!x || !out || S < 0 || T < 0 || ld_in < T || ld_out < T || !(alpha > 0.0 && alpha <= 1.0) ||
-      min_periods < 0 || T > 0x7fffffff)
-    return BQ_EINVAL;
-  if (S == 0 || T == 0) return BQ_OK;
-  const unsigned blocks = (unsigned)((S + 255) / 256);
-  hipLaunchKernelGGL(ewm_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, out, S, (int)T, ld_in, ld_out,
-                     alpha, (int)min_periods);
-  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+  bq_roll_job j;
+  memset(&j, 0, sizeof(j));
+  j.x = x;
+  j.out = out;
+  j.ld_in = ld_in;
+  j.ld_out = ld_out;
+  j.min_periods = min_periods;
+  j.mode = BQ_ROLL_EWM;
+  j.alpha = alpha;
+  return bq_rolling_batch(&j, 1, S, T, stream);
 }
 
 }  // extern "C"

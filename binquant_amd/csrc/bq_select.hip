@@ -147,21 +147,39 @@ __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __res
   }
 }
 
+// One wave per symbol row: 64 candles per step are read as one coalesced
+// 64-byte load, the labels of the step become one ballot mask, and the greedy
+// (keep a label iff it is more than `bars` after the last kept one) walks only
+// the set bits of the mask with wave-uniform scalar arithmetic — labels are
+// sparse, so a row costs ~T/64 steps instead of T dependent byte loads.
 __global__ __launch_bounds__(256) void cooldown_kernel(const uint8_t* __restrict__ label, int64_t S, int T,
                                                        int64_t ld_in, int bars, uint8_t* __restrict__ kept,
                                                        uint8_t* __restrict__ suppressed, int64_t ld_out) {
-  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (s >= S) return;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t s = (int64_t)blockIdx.x * (256 / WAVE) + threadIdx.x / WAVE;
+  if (s >= S) return;   // whole wave
   const uint8_t* __restrict__ l = label + s * ld_in;
   uint8_t* __restrict__ k = kept + s * ld_out;
   uint8_t* __restrict__ u = suppressed + s * ld_out;
   int last = -0x40000000;   // "None": never within reach
-  for (int i = 0; i < T; ++i) {
-    const bool on = l[i] != 0;
-    const bool sup = on && (i - last) <= bars;
-    if (on && !sup) last = i;
-    k[i] = (uint8_t)(on && !sup);
-    u[i] = (uint8_t)sup;
+  for (int t0 = 0; t0 < T; t0 += WAVE) {
+    const int t = t0 + lane;
+    const bool on = t < T && l[t] != 0;
+    uint64_t m = __ballot(on);
+    uint64_t keep = 0;
+    while (m) {
+      const int i = __builtin_ctzll(m);
+      m &= m - 1;
+      if (t0 + i - last > bars) {
+        keep |= 1ull << i;
+        last = t0 + i;
+      }
+    }
+    if (t < T) {
+      const bool kb = (keep >> lane) & 1ull;
+      k[t] = (uint8_t)kb;
+      u[t] = (uint8_t)(on && !kb);
+    }
   }
 }
 
@@ -186,7 +204,7 @@ int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32
       T > 0x7fffffff)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;
-  hipLaunchKernelGGL(cooldown_kernel, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, (hipStream_t)stream, label, S,
+  hipLaunchKernelGGL(cooldown_kernel, dim3((unsigned)((S + 3) / 4)), dim3(256), 0, (hipStream_t)stream, label, S,
                      (int)T, ld_in, (int)bars, kept, suppressed, ld_out);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }

@@ -349,6 +349,71 @@ def ewm(
     return out
 
 
+@dataclass
+class Roll:
+    """One x.shift(shift).rolling(window, min_periods).<stat>() series of a
+    rolling_many batch (stat as in rolling())."""
+
+    x: torch.Tensor
+    window: int
+    stat: str = "mean"
+    q: float = 0.5
+    min_periods: int | None = None
+    shift: int = 0
+
+
+@dataclass
+class Ewm:
+    """One x.ewm(alpha|span, adjust=False, min_periods).mean() series of a batch."""
+
+    x: torch.Tensor
+    alpha: float | None = None
+    span: float | None = None
+    min_periods: int = 0
+
+
+def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
+    """Independent Roll / Ewm series over one [S, T] shape in as few launches
+    as the kernel families allow (bq_rolling_batch): the lane-per-symbol
+    replays of different series run side by side instead of one launch each."""
+    if not specs:
+        return []
+    x0 = _check_panel(specs[0].x, "x")
+    S, T = x0.shape
+    outs: list[torch.Tensor] = []
+    jobs = []
+    keep = []
+    for sp in specs:
+        x = _check_panel(sp.x, "x", (S, T))
+        out = torch.empty((S, T), dtype=torch.float64, device=x.device)
+        j = _lib.BqRollJob()
+        j.x, j.out, j.ld_in, j.ld_out = x.data_ptr(), out.data_ptr(), _row_stride(x), T
+        if isinstance(sp, Ewm):
+            if (sp.alpha is None) == (sp.span is None):
+                raise ValueError("give exactly one of alpha / span")
+            com = (float(sp.span) - 1.0) / 2.0 if sp.span is not None else 1.0 / float(sp.alpha) - 1.0
+            j.alpha, j.mode, j.min_periods = 1.0 / (1.0 + com), _lib.ROLL_EWM, int(sp.min_periods)
+        else:
+            stat, q = sp.stat, sp.q
+            if stat == "max":
+                stat, q = "quantile", 1.0
+            elif stat == "min":
+                stat, q = "quantile", 0.0
+            if stat not in _lib.ROLL_MODES:
+                raise ValueError(f"unknown rolling statistic {stat!r}")
+            j.window, j.shift, j.mode, j.q = int(sp.window), int(sp.shift), _lib.ROLL_MODES[stat], float(q)
+            j.min_periods = int(sp.window if sp.min_periods is None else sp.min_periods)
+        jobs.append(j)
+        outs.append(out)
+        keep.append(x)
+    L = _lib.load()
+    for i in range(0, len(jobs), _lib.MAX_ROLL_JOBS):
+        chunk = jobs[i : i + _lib.MAX_ROLL_JOBS]
+        arr = (_lib.BqRollJob * len(chunk))(*chunk)
+        _lib.check(L.bq_rolling_batch(arr, len(chunk), S, T, _stream_handle(stream)), "bq_rolling_batch")
+    return outs
+
+
 def row_quantile(x: torch.Tensor, q: float, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """numpy.quantile(row[~isnan(row)], q) per row (numpy 'linear' method), as
     FailedSpikeFade.auto_calibrate (strategies/failed_spike_fade.py:229-257)

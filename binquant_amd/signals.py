@@ -51,16 +51,15 @@ def wilder_rsi(close: torch.Tensor, window: int = 14) -> torch.Tensor:
     delta = _diff(close, 1)
     gain = _clip_lower(delta, 0.0)
     loss = -torch.where(delta > 0, torch.zeros_like(delta), delta)   # -delta.clip(upper=0), NaN stays
-    ag = engine.ewm(gain, alpha=1 / window, min_periods=window)
-    al = engine.ewm(loss, alpha=1 / window, min_periods=window)
+    ag, al = engine.rolling_many(engine.Ewm(gain, alpha=1 / window, min_periods=window),
+                                 engine.Ewm(loss, alpha=1 / window, min_periods=window))
     den = ag + al
     return torch.where(den != 0, 100 * ag / den, torch.full_like(den, 50.0))
 
 
 def trend_score(close: torch.Tensor, fast: int = 20, slow: int = 50) -> torch.Tensor:
     """(ema_fast - ema_slow) / |ema_slow|, 0 where ema_slow == 0."""
-    f = ema(close, fast)
-    s = ema(close, slow)
+    f, s = engine.rolling_many(engine.Ewm(close, span=fast), engine.Ewm(close, span=slow))
     return torch.where(s == 0, torch.zeros_like(s), (f - s) / s.abs())
 
 
@@ -74,9 +73,10 @@ def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int 
     minus_dm = torch.where((ld > hd) & (ld > 0), ld, zero)
     pc = _shift(close, 1)
     tr = torch.fmax(torch.fmax(high - low, (high - pc).abs()), (low - pc).abs())   # max(axis=1) skips NaN
-    atr_sum = engine.rolling(tr, window, "sum")
-    plus_di = 100.0 * engine.rolling(plus_dm, window, "sum") / atr_sum
-    minus_di = 100.0 * engine.rolling(minus_dm, window, "sum") / atr_sum
+    atr_sum, plus_sum, minus_sum = engine.rolling_many(
+        engine.Roll(tr, window, "sum"), engine.Roll(plus_dm, window, "sum"), engine.Roll(minus_dm, window, "sum"))
+    plus_di = 100.0 * plus_sum / atr_sum
+    minus_di = 100.0 * minus_sum / atr_sum
     total = plus_di + minus_di
     dx = 100.0 * (plus_di - minus_di).abs() / torch.where(total != 0, total, torch.full_like(total, NAN))
     dx = torch.nan_to_num(dx, nan=0.0, posinf=torch.inf, neginf=-torch.inf)   # fillna(0.0)
@@ -87,8 +87,7 @@ def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int 
 def zscore(close: torch.Tensor, window: int = 20) -> torch.Tensor:
     """_compute_zscore at every t: (c - mean) / std(ddof=0); 0 where std is 0
     or NaN."""
-    mean = engine.rolling(close, window, "mean")
-    std = engine.rolling(close, window, "std0")
+    mean, std = engine.rolling_many(engine.Roll(close, window, "mean"), engine.Roll(close, window, "std0"))
     bad = (std == 0) | torch.isnan(std)
     return torch.where(bad, torch.zeros_like(std), (close - mean) / std)
 
@@ -104,15 +103,20 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     eps = 1e-6
     vals: dict[str, torch.Tensor] = {}
     vals["close"], vals["open"], vals["high"], vals["low"], vals["volume"] = c, o, h, l, v
-    vma = engine.rolling(v, volume_window, "mean")
+    R, E = engine.Roll, engine.Ewm
+    # df["high"].iloc[-49:-1].max(): the 48 highs before t (fewer when short; nan-skipping)
+    specs = [R(v, volume_window, "mean"), R(h, lookback_high, "max", min_periods=1, shift=1), E(c, span=20),
+             E(c, span=50)]
+    if qv is not None:
+        specs.append(R(qv, volume_window, "mean"))
+    res = engine.rolling_many(*specs)
+    vma, vals["previous_high"], e20, e50 = res[:4]
     if qv is not None:
         vals["quote_volume"] = qv
-        qvma = engine.rolling(qv, volume_window, "mean")
+        qvma = res[4]
     else:
         vals["quote_volume"] = v * c
         qvma = vma * c
-    # df["high"].iloc[-49:-1].max(): the 48 highs before t (fewer when short; nan-skipping)
-    vals["previous_high"] = engine.rolling(h, lookback_high, "max", min_periods=1, shift=1)
     t = torch.arange(T, device=dev, dtype=torch.int64)
 
     def back(k):
@@ -136,8 +140,8 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     rng = h - l
     vals["range_position"] = (c - l) / (rng + eps)
     vals["upper_wick_fraction"] = (h - torch.maximum(o, c)) / (rng + eps)
-    vals["ema20"] = ema(c, 20)
-    vals["ema50"] = ema(c, 50)
+    vals["ema20"] = e20
+    vals["ema50"] = e50
     vals["atr"] = atr if atr is not None else torch.zeros_like(c)
     status = torch.full((S, T), TG_READY, dtype=torch.int8, device=dev)
     finite = torch.ones((S, T), dtype=torch.bool, device=dev)
@@ -159,11 +163,12 @@ def mean_reversion_features(o, h, l, c, v, atr, rsi_window: int = 14, volume_ma_
     ratio of _resolve_entry (:124-134)."""
     rsi = wilder_rsi(c, rsi_window)
     rng = h - l
+    vma, ama = engine.rolling_many(engine.Roll(v, volume_ma_window, "mean"), engine.Roll(atr, atr_ma_window, "mean"))
     return {
         "rsi": rsi,
         "previous_rsi": _shift(rsi, 1),
-        "volume_ma": engine.rolling(v, volume_ma_window, "mean"),
-        "atr_ma": engine.rolling(atr, atr_ma_window, "mean"),
+        "volume_ma": vma,
+        "atr_ma": ama,
         "trend_score": trend_score(c, fast, slow),
         "upper_rejection_ratio": torch.where(rng > 0, (h - torch.maximum(o, c)) / rng, torch.full_like(c, NAN)),
     }

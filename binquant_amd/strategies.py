@@ -104,11 +104,17 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     bw = max(p.lookback_window, 2)
     out: dict[str, torch.Tensor] = {}
     # volume.shift(2).rolling(bw - 1, min_periods=bw - 1).median()   (:58-63)
-    out["baseline_volume"] = engine.rolling(v, bw - 1, "median", min_periods=bw - 1, shift=2)
+    R = engine.Roll
+    up = (c > _shift(c, 1)).to(torch.float64)
+    specs = [R(v, bw - 1, "median", min_periods=bw - 1, shift=2), R(up, 3, "sum", min_periods=3)]
+    if has_q:
+        specs.append(R(qv, bw - 1, "median", min_periods=bw - 1, shift=2))
+    res = engine.rolling_many(*specs)
+    out["baseline_volume"] = res[0]
     out["baseline_volume_safe"] = _clip_lower(out["baseline_volume"], p.min_baseline_volume)
     out["volume_ratio"] = v / out["baseline_volume_safe"]
     if has_q:
-        out["baseline_quote_volume"] = engine.rolling(qv, bw - 1, "median", min_periods=bw - 1, shift=2)
+        out["baseline_quote_volume"] = res[2]
         out["baseline_quote_volume_safe"] = _clip_lower(out["baseline_quote_volume"], p.min_baseline_volume)
         out["quote_volume_ratio"] = qv / out["baseline_quote_volume_safe"]
     else:
@@ -123,8 +129,7 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     out["body_frac"] = candle_body / candle_range
     out["close_to_high"] = (h - c) / candle_range
     out["is_bullish"] = c > o
-    up = (c > _shift(c, 1)).to(torch.float64)
-    out["recent_up_closes"] = engine.rolling(up, 3, "sum", min_periods=3)
+    out["recent_up_closes"] = res[1]
     out["vol_spike"] = v > (p.volume_multiplier * out["baseline_volume_safe"])
     if has_q:
         out["quote_vol_spike"] = qv > (p.quote_volume_multiplier * out["baseline_quote_volume_safe"])
@@ -179,32 +184,35 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -
     out: dict[str, torch.Tensor] = {}
     prev = _shift(c, 1)
     tr = torch.fmax(torch.fmax(h - l, (h - prev).abs()), (l - prev).abs())   # concat(...).max(axis=1) skips NaN
-    out["candidate_atr"] = engine.ewm(tr, alpha=1 / 14, min_periods=14)
+    R, E = engine.Roll, engine.Ewm
+    atr, vmean, hmax, lmin, e20, e50 = engine.rolling_many(
+        E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
+        R(h, p.compression_bars, "max", shift=1), R(l, p.compression_bars, "min", shift=1),
+        E(c, span=20), E(c, span=50),
+    )
+    out["candidate_atr"] = atr
     out["momentum_3"] = _pct_change(c, p.momentum_bars)
-    out["relative_volume"] = v / engine.rolling(v, p.volume_lookback, "mean", shift=1)
-    out["pre_breakout_compression"] = (
-        engine.rolling(h, p.compression_bars, "max", shift=1) - engine.rolling(l, p.compression_bars, "min", shift=1)
-    ) / prev
+    out["relative_volume"] = v / vmean
+    out["pre_breakout_compression"] = (hmax - lmin) / prev
     out["pump_score"] = (
         out["relative_volume"] * _clip_lower(out["momentum_3"], 0.0) / _replace0(out["pre_breakout_compression"])
     )
-    out["score_threshold"] = engine.rolling(out["pump_score"], p.score_lookback, "quantile", q=p.score_quantile,
-                                            shift=1)
+    out["score_threshold"], out["volume_threshold"] = engine.rolling_many(
+        R(out["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+        R(out["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+    )
     out["score_cross"] = (out["pump_score"] >= out["score_threshold"]) & (
         _shift(out["pump_score"], 1) < _shift(out["score_threshold"], 1)
     )
-    out["volume_threshold"] = engine.rolling(out["relative_volume"], p.score_lookback, "quantile",
-                                             q=p.score_quantile, shift=1)
-    out["prior_high"] = engine.rolling(h, p.compression_bars, "max", shift=1)
+    out["prior_high"] = hmax
     out["close_location"] = (c - l) / _replace0(h - l)
-    out["ema20"] = engine.ewm(c, span=20)
-    out["ema50"] = engine.ewm(c, span=50)
+    out["ema20"] = e20
+    out["ema50"] = e50
     out["trend_score"] = (out["ema20"] - out["ema50"]) / out["ema50"]
     out["momentum_atr"] = out["momentum_3"] / (out["candidate_atr"] / c)
     bench = btc_close.reshape(1, -1)
     out["btc_momentum_3"] = _pct_change(bench, p.momentum_bars).expand_as(c)
-    be20 = engine.ewm(bench.contiguous(), span=20)
-    be50 = engine.ewm(bench.contiguous(), span=50)
+    be20, be50 = engine.rolling_many(E(bench.contiguous(), span=20), E(bench.contiguous(), span=50))
     out["btc_trend_score"] = ((be20 - be50) / be50).expand_as(c)
     out["relative_strength"] = out["momentum_3"] - out["btc_momentum_3"]
     return out
@@ -265,14 +273,32 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
     out["range_pct"] = out["total_range"] / (o + eps)
     out["is_bullish"] = c > o
     out["close_open_ratio"] = (c - o) / (o + eps)
-    out["price_ma"] = engine.rolling(c, w, "mean")
-    out["price_std"] = engine.rolling(c, w, "std")
+    # every rolling series that depends only on the inputs: ONE batched call
+    R, E = engine.Roll, engine.Ewm  # noqa: F841
+    bsp = out["body_size_pct"]
+    cw, n = p.cumulative_price_window, p.streak_length
+    neg_pc = torch.where(pc > 0, torch.zeros_like(pc), pc).abs()   # clip(upper=0).abs(), NaN stays
+    specs = [R(c, w, "mean"), R(c, w, "std"), R(v, w, "mean"), R(v, w, "std"), R(qv, w, "mean"),
+             R(c, 8, "std"), R(c, 20, "std"), R(pc, 2, "sum"), R(pc, 3, "sum"),
+             R((pc > 0).to(torch.float64), 5, "sum"), R(pca, 5, "sum"), R(bsp, 10, "mean"), R(bsp, 10, "std"),
+             R((c > o).to(torch.float64), n, "sum"), R((c < o).to(torch.float64), n, "sum")]
+    if cw > 1:
+        specs += [R(_clip_lower(pc, 0.0), cw, "sum"), R(neg_pc, cw, "sum")]
+    if p.price_break_use_dynamic:
+        specs.append(R(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20))
+    res = engine.rolling_many(*specs)
+    (price_ma, price_std, volume_ma, volume_std, qv_ma, s8, s20, pc2, pc3, pos5, abs5, bsp_ma, bsp_sd, green,
+     red) = res[:15]
+    cum_pos, cum_neg = (res[15], res[16]) if cw > 1 else (None, None)
+    dyn = res[-1] if p.price_break_use_dynamic else None
+    out["price_ma"] = price_ma
+    out["price_std"] = price_std
     out["price_zscore"] = (c - out["price_ma"]) / (out["price_std"] + eps)
-    out["volume_ma"] = engine.rolling(v, w, "mean")
+    out["volume_ma"] = volume_ma
     vr = v / (out["volume_ma"] + eps)
     out["volume_ratio"] = vr
-    out["volume_zscore"] = (v - out["volume_ma"]) / (engine.rolling(v, w, "std") + eps)
-    out["quote_volume_ma"] = engine.rolling(qv, w, "mean")
+    out["volume_zscore"] = (v - out["volume_ma"]) / (volume_std + eps)
+    out["quote_volume_ma"] = qv_ma
     out["quote_volume_ratio"] = qv / (out["quote_volume_ma"] + eps)
     out["momentum_3"] = _pct_change(c, 3)
     out["momentum_5"] = _pct_change(c, 5)
@@ -291,26 +317,27 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
     out["volume_cluster_min_ratio"] = vcmr.squeeze(1)
     out["price_break_base_threshold"] = pbbt.squeeze(1)
     # ---- compute_early_features (:324-357) ----
-    s8 = engine.rolling(c, 8, "std")
-    s20 = engine.rolling(c, 20, "std")
     out["rolling_price_std_8"] = s8
     out["rolling_price_std_20"] = s20
     out["std_ratio_8_20"] = s8 / (s20 + eps)
     out["vol_ratio_slope_3"] = _diff(vr, 3)
     out["vol_ratio_accel"] = _diff(out["vol_ratio_slope_3"], 1)
     out["pc_1"] = pc
-    out["pc_2c"] = engine.rolling(pc, 2, "sum")
-    out["pc_3c"] = engine.rolling(pc, 3, "sum")
-    out["pc_pos_count_5"] = engine.rolling((pc > 0).to(torch.float64), 5, "sum")
-    out["pc_abs_sum_5"] = engine.rolling(pca, 5, "sum")
-    bsp = out["body_size_pct"]
-    out["body_size_pct_ma_10"] = engine.rolling(bsp, 10, "mean")
-    out["body_size_pct_std_10"] = engine.rolling(bsp, 10, "std")
+    out["pc_2c"] = pc2
+    out["pc_3c"] = pc3
+    out["pc_pos_count_5"] = pos5
+    out["pc_abs_sum_5"] = abs5
+    out["body_size_pct_ma_10"] = bsp_ma
+    out["body_size_pct_std_10"] = bsp_sd
     out["body_size_pct_z"] = (bsp - out["body_size_pct_ma_10"]) / (out["body_size_pct_std_10"] + eps)
     out["vol_compression_flag"] = s8 < s20 * 0.6
     # ---- volume_cluster_flag (:360-370) ----
     cond = vr >= vcmr
-    cnt = engine.rolling(cond.to(torch.float64), p.volume_cluster_window, "sum", min_periods=1)
+    # the two series that need the calibrated ratio: one more batched call
+    cnt, vmax = engine.rolling_many(
+        R(cond.to(torch.float64), p.volume_cluster_window, "sum", min_periods=1),
+        R((vr >= vcmr * 0.8).to(torch.float64), max(cw, 1), "max"),
+    )
     base = (cnt >= p.volume_cluster_min_count) & cond
     if p.volume_cluster_label_mode == "last":
         nxt = torch.zeros_like(base)
@@ -325,7 +352,6 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
     out["volume_cluster_flag"] = vcf
     # ---- price_break_flag (:372-400), auto_tune off ----
     if p.price_break_use_dynamic:
-        dyn = engine.rolling(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20)
         thr = _ffill(torch.where(torch.isnan(dyn), dyn, torch.maximum(pbbt.expand_as(dyn), dyn)))
     else:
         thr = pbbt.expand_as(pca).clone()
@@ -337,10 +363,6 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
         cum_f = torch.zeros_like(cond)
         cum_s = torch.zeros_like(cond)
     else:
-        cum_pos = engine.rolling(_clip_lower(pc, 0.0), cw, "sum")
-        neg_pc = torch.where(pc > 0, torch.zeros_like(pc), pc).abs()   # clip(upper=0).abs(), NaN stays
-        cum_neg = engine.rolling(neg_pc, cw, "sum")
-        vmax = engine.rolling((vr >= vcmr * 0.8).to(torch.float64), cw, "max")
         vol_cond = torch.isnan(vmax) | (vmax != 0)          # .astype(bool): NaN -> True
         cum_f = (cum_pos >= p.cumulative_price_threshold) & vol_cond
         cum_s = (cum_neg >= p.cumulative_price_threshold) & vol_cond
@@ -378,9 +400,6 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
         out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_pre,
                                                                             p.post_spike_cooldown_bars)
     # ---- detect_streaks (:522-531) ----
-    n = p.streak_length
-    green = engine.rolling((c > o).to(torch.float64), n, "sum")
-    red = engine.rolling((c < o).to(torch.float64), n, "sum")
     out["upward"] = green >= n
     out["downward"] = red >= n
     return out

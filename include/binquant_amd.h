@@ -208,7 +208,8 @@ enum bq_roll_mode {
   BQ_ROLL_VAR = 4,   /* ddof 1 */
   BQ_ROLL_STD = 5,   /* ddof 1 */
   BQ_ROLL_VAR0 = 6,  /* ddof 0 */
-  BQ_ROLL_STD0 = 7   /* ddof 0 */
+  BQ_ROLL_STD0 = 7,  /* ddof 0 */
+  BQ_ROLL_EWM = 8    /* bq_rolling_batch only: ewm(alpha, adjust=False, min_periods) */
 };
 /*
  * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,
@@ -222,6 +223,24 @@ enum bq_roll_mode {
  */
 int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream);
+
+/*
+ * Many independent rolling / ewm series over one [S][T] shape in one call
+ * (the strategy pipelines issue 5-18 of them per frame batch, e.g.
+ * strategies/failed_spike_fade.py:260-357): one launch per kernel family
+ * instead of one per series, so lane-per-symbol replays of different series
+ * run side by side. Jobs are read from HOST memory (copied into the launch).
+ */
+#define BQ_MAX_ROLL_JOBS 16
+typedef struct bq_roll_job {
+  const double* x;         /* [S][ld_in] device pointer                        */
+  double* out;             /* [S][ld_out] device pointer                       */
+  int64_t ld_in, ld_out;
+  int32_t window, min_periods, shift, mode;   /* mode: bq_roll_mode            */
+  double q;                /* quantile                                         */
+  double alpha;            /* BQ_ROLL_EWM                                      */
+} bq_roll_job;
+int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream);
 
 /*
  * out = x.ewm(alpha=alpha, adjust=False, min_periods=min_periods).mean()

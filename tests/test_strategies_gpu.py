@@ -65,7 +65,7 @@ def test_rolling_primitive_vs_pandas(cuda, stat, window, minp, shift, q):
     from binquant_amd import engine
     from binquant_amd.synth import numpy_panel
 
-    S, T = 9, 1300
+    S, T = 70, 1300   # 70 rows: a full and a partial wave of the lane-per-symbol replay
     x = numpy_panel(S, T, seed0=window + shift, edges=True)["volume"]
     x[:, 100:110] = np.nan   # NaN gaps are skipped (nobs)
     x[2, 500:700] = 3.25     # constant run (same-value rule for mean)
@@ -74,10 +74,8 @@ def test_rolling_primitive_vs_pandas(cuda, stat, window, minp, shift, q):
         r = pd.Series(x[s]).shift(shift).rolling(window, min_periods=minp)
         want = {"median": r.median, "mean": r.mean, "sum": r.sum, "max": r.max, "min": r.min,
                 "var": r.var, "std": r.std}.get(stat, lambda: r.quantile(q))()
-        # var/std: pandas' Welford update vs the kernel's shifted sums -> last-bit noise
-        rtol = 1e-10 if stat in ("var", "std") else 1e-12
-        np.testing.assert_allclose(got[s], want.to_numpy(), rtol=rtol, atol=1e-12, equal_nan=True,
-                                   err_msg=f"{stat} row {s}")
+        # bit-exact: moments replay pandas' recurrences, order statistics are exact
+        np.testing.assert_array_equal(got[s], want.to_numpy(), err_msg=f"{stat} row {s}")
 
 
 @pytest.mark.parametrize("alpha,minp", [(1 / 14, 14), (2 / 21, 0), (0.5, 3)])
@@ -113,7 +111,7 @@ def test_rolling_signed_series_vs_pandas(cuda, stat, window, minp):
     for s in range(6):
         r = pd.Series(x[s]).rolling(window, min_periods=minp)
         want = getattr(r, stat)().to_numpy()
-        np.testing.assert_allclose(got[s], want, rtol=1e-10, atol=1e-15, equal_nan=True, err_msg=f"{stat} {s}")
+        np.testing.assert_array_equal(got[s], want, err_msg=f"{stat} {s}")
 
 
 def test_row_quantile_is_numpy_bitwise(cuda):
