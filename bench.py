@@ -14,7 +14,13 @@ Also reported (same JSON line):
                  pattern) on the host cores, rank 0 at N=1, time-bounded sample;
   tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
                  latency p50/p99;
-  breadth      — C5 leg (market features + breadth partials + RCCL all-reduce).
+  breadth      — C5 leg (market features + breadth partials + RCCL all-reduce);
+  rows         — every other SURVEY §8 row on the device at 12 500 x 2 000
+                 (HIP-event time per call, algorithmic bytes -> GB/s and
+                 fraction of HBM peak) with a bounded CPU timing of the
+                 oracle's per-symbol path where the oracle restates the row;
+  store        — §8f row 1: device MarketStateStore + live context at 10k
+                 symbols x 400-bar histories, per-tick latency p50/p99.
 """
 
 from __future__ import annotations
@@ -55,6 +61,10 @@ def parse():
     ap.add_argument("--no-tick", action="store_true")
     ap.add_argument("--no-breadth", action="store_true")
     ap.add_argument("--breadth-steps", type=int, default=5)
+    ap.add_argument("--no-rows", action="store_true")
+    ap.add_argument("--row-symbols", type=int, default=12_500)
+    ap.add_argument("--row-candles", type=int, default=2_000)
+    ap.add_argument("--store-ticks", type=int, default=50)
     return ap.parse_args()
 
 
@@ -203,6 +213,141 @@ def bench_breadth(args, panel, world, dev):
     }
 
 
+def _time_call(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def _cpu_rate(fn, candles_per_call, budget=1.0):
+    """Candles/s of a single-core oracle call pattern, time-bounded."""
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget:
+        fn()
+        n += 1
+    return n * candles_per_call / (time.perf_counter() - t0)
+
+
+def bench_rows(args, dev):
+    """Per-row device timings (SURVEY §8a/§8f rows beyond the headline)."""
+    import pandas as pd
+
+    from binquant_amd import signals, strategies
+    from binquant_amd.synth import numpy_symbol
+    from oracle import frame_ref, indicators_ref, market_ref
+
+    S, T = args.row_symbols, args.row_candles
+    p = device_panel(S, T, device=dev, seed=99)
+    o, h, l, c, v = (p[k] for k in ("open", "high", "low", "close", "volume"))
+    qv = v * c
+    btc = c[0].clone()
+    ts = (1_700_000_000_000 + 900_000 * torch.arange(T, device=dev, dtype=torch.int64)).expand(S, T).contiguous()
+    atr = engine.enrich(o, h, l, c, v, columns=("ATR",))["ATR"]
+    agg = {"open": "first", "high": "max", "low": "min", "close": "last", "volume": "sum"}
+    # name -> (device call, algorithmic bytes per candle, row reference)
+    rows = {
+        "a11_beta_corr": (lambda: engine.beta_corr(c, btc, 50), 8 + 16, "producers/context_evaluator.py:154-194"),
+        "a13_market_features": (lambda: engine.market_features(h, l, c, max_bars=400), 24 + 48,
+                                "live_market_context_accumulator.py:244-297"),
+        "a17_activity_burst": (lambda: strategies.activity_burst_features(o, h, l, c, v, qv), 48 + 8 * 23,
+                               "strategies/activity_burst_pump.py:51-158"),
+        "a18_pump_score": (lambda: strategies.pump_score_features(o, h, l, c, v, btc), 40 + 8 * 17,
+                           "strategies/liquidation_sweep_pump.py:195-269"),
+        "a19_failed_spike": (lambda: strategies.failed_spike_features(o, h, l, c, v, qv), 48 + 8 * 56,
+                             "strategies/failed_spike_fade.py:260-544"),
+        "a20_wilder_rsi": (lambda: signals.wilder_rsi(c), 16, "strategies/mean_reversion_fade.py:88-109"),
+        "a20_adx": (lambda: signals.adx(h, l, c), 32, "strategies/range_bb_rsi_mean_reversion.py:101-122"),
+        "a20_zscore": (lambda: signals.zscore(c), 16, "strategies/range_bb_rsi_mean_reversion.py:124-138"),
+        "supertrend": (lambda: engine.supertrend(h, l, c, atr=atr), 4 * 8 + 1 + 16, "strategies/coinrule/coinrule.py:143"),
+        "a9_resample_1h": (lambda: engine.resample(ts, {"open": o, "high": h, "low": l, "close": c, "volume": v},
+                                                   agg, 3_600_000), 48 + 48 / 4, "producers/context_evaluator.py:403-407"),
+        "f4_btc_join_returns": (lambda: engine.join_returns(ts, c, ts[0], btc), 16 + 16,
+                                "producers/context_evaluator.py:161-177"),
+    }
+    out = {"workload": f"{S} symbols x {T} candles (synthetic, HBM-resident)"}
+    for name, (fn, bpc, ref) in rows.items():
+        ms = _time_call(fn)
+        gbs = S * T * bpc / (ms * 1e-3) / 1e9
+        out[name] = {"ms": ms, "value": S * T / (ms * 1e-3), "unit": "symbol-candles/s", "GBps": gbs,
+                     "frac": gbs / HBM_PEAK_GBS, "bytes_per_candle": bpc, "reference": ref}
+    del p, o, h, l, c, v, qv, ts, atr
+    torch.cuda.empty_cache()
+    if args.no_cpu_baseline:
+        return out
+    # bounded single-core CPU timings of the oracle restatements (pandas, the reference's library)
+    sym = numpy_symbol(400, 1)
+    df = pd.DataFrame(sym)
+    bc = numpy_symbol(400, 2)["close"]
+    tsv = 1_700_000_000_000 + 900_000 * np.arange(400)
+    df_r = df.assign(open_time=tsv)
+    cpu = {
+        "a11_beta_corr": lambda: indicators_ref.beta_corr_series(sym["close"], bc, 50),
+        "a13_market_features": lambda: market_ref.symbol_features(sym["high"], sym["low"], sym["close"]),
+        "supertrend": lambda: indicators_ref.supertrend(df.copy(), 3.0, 10),
+        "a9_resample_1h": lambda: frame_ref.resample(df_r, "1h", agg),
+        "f4_btc_join_returns": lambda: frame_ref.joined_returns(tsv, sym["close"], tsv, bc),
+    }
+    for name, fn in cpu.items():
+        rate = _cpu_rate(fn, 400 if name != "a13_market_features" else 1)
+        out[name]["cpu_oracle"] = {"value": rate, "unit": "symbol-candles/s" if name != "a13_market_features"
+                                   else "symbol-features/s (one latest-candle feature row per call)",
+                                   "cores": 1, "sample": "one 400-candle frame per call, ~1 s"}
+    return out
+
+
+def bench_store(args, dev):
+    """§8f row 1: DeviceMarketStateStore at 10k symbols x 400-bar histories;
+    one tick = a new closed candle per symbol (host arrays, one device update)
+    + the live context build (fresh slots, features, breadth, scoring)."""
+    from binquant_amd.market_regime.store import DeviceLiveMarketContextAccumulator, DeviceMarketStateStore
+
+    S, M = args.tick_symbols, 400
+    syms = ["BTCUSDT"] + [f"S{i:05d}USDT" for i in range(1, S)]
+    store = DeviceMarketStateStore(max_bars_per_symbol=M, capacity=S)
+    acc = DeviceLiveMarketContextAccumulator(store, "BTCUSDT")
+    rng = np.random.default_rng(0)
+    price = 10 ** rng.uniform(-2, 3, S)
+    t0 = 1_700_000_000_000
+    hist = device_panel(S, M, device=dev, seed=5)
+    slots = torch.arange(S, dtype=torch.int64, device=dev).repeat_interleave(M)
+    for s in syms:
+        store._slot(s)
+    tsh = (t0 + 900_000 * torch.arange(M, device=dev, dtype=torch.int64)).repeat(S)
+    store.update_slots(slots, tsh, [hist[k].reshape(-1) for k in ("open", "high", "low", "close", "volume")])
+    del hist, slots, tsh
+    lat = []
+    vol = np.ones(S)
+    for k in range(args.store_ticks + 5):
+        ts = t0 + 900_000 * (M + k)
+        price *= np.exp(rng.normal(0, 0.002, S))
+        c = price
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        ctx = acc.on_closed_candles(syms, np.full(S, ts), c, c * 1.001, c * 0.999, c, vol, at=ts)
+        torch.cuda.synchronize()
+        if k >= 5:
+            lat.append(time.perf_counter() - a)
+    sl = store.fresh_slots(ts)
+    fms = _time_call(lambda: store.features(sl), reps=5)
+    lat = np.array(lat) * 1e3
+    return {
+        "symbols": S, "max_bars": M, "ticks": len(lat),
+        "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)),
+        "features_kernel_ms": fms,
+        "features_GBps": S * M * 24 / (fms * 1e-3) / 1e9,
+        "context_valid": ctx is not None,
+        "includes": "host candle arrays -> one bq_store_update + fresh slots + bq_store_features + breadth + "
+                    "host scoring/annotation, synchronized",
+    }
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -274,6 +419,9 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_tick:
         result["tick"] = bench_tick(args, dev)
+        result["store"] = bench_store(args, dev)
+    if rank == 0 and world == 1 and not args.no_rows:
+        result["rows"] = bench_rows(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, T)
     else:

@@ -295,11 +295,11 @@ def annotate_symbols(
     if prev_regime is not None:
         trans = np.full(ts.shape, None, dtype=object)
         tstr = np.zeros(ts.shape)
-        for i in range(ts.size):
-            p = prev_regime[i]
-            if p is not None and p != regime[i]:
-                trans[i] = symbol_transition_event(p, regime[i])
-                tstr[i] = min(1.0, max(0.0, strength[i] + abs(strength[i] - prev_strength[i]) - 0.25))
+        prev_regime = np.asarray(prev_regime, dtype=object)
+        changed = np.array([p is not None for p in prev_regime], dtype=bool) & (prev_regime != regime)
+        for i in np.flatnonzero(changed):
+            trans[i] = symbol_transition_event(prev_regime[i], regime[i])
+            tstr[i] = min(1.0, max(0.0, strength[i] + abs(strength[i] - prev_strength[i]) - 0.25))
         out.update(micro_regime_transition=trans, micro_regime_transition_strength=tstr)
     return out
 

@@ -76,6 +76,56 @@ def _device(device) -> torch.device:
     return torch.device("cuda")
 
 
+class SortedNames(Sequence):
+    """sorted(names), computed on first access (metadata["fresh_symbols"])."""
+
+    def __init__(self, names: np.ndarray):
+        self._names, self._sorted = names, None
+
+    def _get(self) -> list[str]:
+        if self._sorted is None:
+            self._sorted = sorted(self._names.tolist())
+        return self._sorted
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __len__(self) -> int:
+        return int(self._names.size)
+
+    def __eq__(self, other) -> bool:
+        return list(self._get()) == list(other)
+
+
+class SymbolFeatureRows(Mapping):
+    """LiveMarketContext.symbol_features as a read-only mapping symbol -> dict
+    (the SymbolMarketFeatures fields of market_regime/models.py:53-83 plus the
+    micro-regime annotation), backed by column arrays (`.arrays`, `.slots`,
+    `.names`): the per-symbol dict is only built when a symbol is looked up."""
+
+    def __init__(self, names: np.ndarray, slots: np.ndarray, arrays: dict[str, np.ndarray], timestamp: int):
+        self.names, self.slots, self.arrays, self.timestamp = names, slots, arrays, timestamp
+        self._row: dict[str, int] | None = None
+
+    def _index(self) -> dict[str, int]:
+        if self._row is None:
+            self._row = {n: i for i, n in enumerate(self.names.tolist())}
+        return self._row
+
+    def __getitem__(self, symbol: str) -> dict:
+        i = self._index()[symbol]
+        d = {k: (v[i].item() if hasattr(v[i], "item") else v[i]) for k, v in self.arrays.items()}
+        d["symbol"] = symbol
+        d["timestamp"] = self.timestamp
+        return d
+
+    def __iter__(self):
+        return iter(self.names.tolist())
+
+    def __len__(self) -> int:
+        return int(self.names.size)
+
+
 class DeviceMarketStateStore:
     """MarketStateStore with the histories in HBM (one ring per symbol slot)."""
 
@@ -129,6 +179,22 @@ class DeviceMarketStateStore:
     def symbol_of(self, slot: int) -> str:
         return self._names[slot]
 
+    def names_array(self) -> np.ndarray:
+        if getattr(self, "_names_np", None) is None or self._names_np.size != len(self._names):
+            self._names_np = np.array(self._names, dtype=object)
+        return self._names_np
+
+    def slots_for(self, symbols: Sequence[str]) -> torch.Tensor:
+        """Device slot ids of `symbols` (registering new ones); cached for a
+        repeated symbol list, so a steady feed pays the lookup once."""
+        key = tuple(symbols)
+        cached = getattr(self, "_slot_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        t = torch.tensor([self._slot(s) for s in symbols], dtype=torch.int64, device=self.device)
+        self._slot_cache = (key, t)
+        return t
+
     @property
     def n_tracked(self) -> int:
         return len(self._names)
@@ -169,9 +235,10 @@ class DeviceMarketStateStore:
 
     def update_batch(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume) -> None:
         """Many symbols' candles (host arrays, arrival order) in one launch."""
-        slots = torch.tensor([self._slot(s) for s in symbols], dtype=torch.int64)
-        cols = [torch.as_tensor(np.asarray(x, dtype=np.float64)) for x in (open_, high, low, close, volume)]
-        self.update_slots(slots, torch.as_tensor(np.asarray(timestamp, dtype=np.int64)), cols)
+        slots = self.slots_for(symbols)
+        cols = torch.from_numpy(np.stack([np.asarray(x, dtype=np.float64) for x in (open_, high, low, close, volume)]))
+        cols = cols.to(self.device)
+        self.update_slots(slots, torch.as_tensor(np.asarray(timestamp, dtype=np.int64)), list(cols))
 
     # -- reference API ----------------------------------------------------------------
     def update(self, symbol: str, candle: Mapping[str, Any] | pd.Series | pd.DataFrame) -> pd.DataFrame:
@@ -327,6 +394,7 @@ class DeviceLiveMarketContextAccumulator:
         dev = store.device
         fresh = store.fresh_slots(timestamp)
         btc_slot = store.slot_of(self.btc_symbol)
+        btc_fresh = btc_slot is not None and bool((fresh == btc_slot).any())
         # the benchmark is replicated on every rank: only rank 0 counts it
         btc_counted = btc_slot is not None and (not self._sharded() or dist.get_rank(self.group) == 0)
         if btc_slot is not None and not btc_counted:
@@ -373,34 +441,37 @@ class DeviceLiveMarketContextAccumulator:
         ctx["confidence"] = 1.0
         ctx["is_provisional"] = False
         # this rank's fresh symbols with relative strength + micro regime
-        # (regime_transitions.py:162-232), previous micro regime chained
-        f = {k: v[:n_fresh].cpu().numpy() for k, v in feats.items()}
-        c = close[:n_fresh].cpu().numpy()
+        # (regime_transitions.py:162-232), previous micro regime chained by
+        # slot; everything vectorised, per-symbol dicts built on access only
+        stacked = torch.stack([feats[k][:n_fresh] for k in FEATURE_COLUMNS] + [close[:n_fresh]]).cpu().numpy()
+        f = dict(zip(FEATURE_COLUMNS, stacked[:-1]))
+        c = stacked[-1]
+        slots = fresh.cpu().numpy()
         ok = ~np.isnan(f["return_pct"])
-        names = [store.symbol_of(i) for i in fresh.cpu().tolist()]
-        rs = f["return_pct"] - (btc_ret if btc_valid else 0.0)
-        if not btc_valid:
-            rs[:] = 0.0
-        rs[[i for i, nme in enumerate(names) if nme == self.btc_symbol]] = 0.0
-        prev_sym = (previous or {}).get("symbol_features") or {}
-        prev_reg = np.array([prev_sym.get(nme, {}).get("micro_regime") for nme in names], dtype=object)
-        prev_str = np.array([prev_sym.get(nme, {}).get("micro_regime_strength", 0.0) or 0.0 for nme in names])
-        ann = annotate_symbols(f["trend_score"], c > f["ema20"], c > f["ema50"], rs, f["bb_width"], f["atr_pct"],
-                               f["return_pct"], prev_regime=prev_reg, prev_strength=prev_str)
-        sym = {}
-        for i in np.flatnonzero(ok):
-            d = {k: float(f[k][i]) for k in FEATURE_COLUMNS}
-            d.update(symbol=names[i], timestamp=int(timestamp), close=float(c[i]), above_ema20=bool(c[i] > f["ema20"][i]),
-                     above_ema50=bool(c[i] > f["ema50"][i]), relative_strength_vs_btc=float(rs[i]),
-                     micro_regime=ann["micro_regime"][i], micro_regime_strength=float(ann["micro_regime_strength"][i]),
-                     micro_regime_transition=ann["micro_regime_transition"][i],
-                     micro_regime_transition_strength=float(ann["micro_regime_transition_strength"][i]))
-            sym[names[i]] = d
+        slots, c = slots[ok], c[ok]
+        f = {k: v[ok] for k, v in f.items()}
+        rs = f["return_pct"] - btc_ret if btc_valid else np.zeros_like(f["return_pct"])
+        if btc_slot is not None:
+            rs[slots == btc_slot] = 0.0
+        prev_sf = (previous or {}).get("symbol_features")
+        prev_reg = np.full(slots.size, None, dtype=object)
+        prev_str = np.zeros(slots.size)
+        if isinstance(prev_sf, SymbolFeatureRows) and prev_sf.slots.size:
+            j = np.minimum(np.searchsorted(prev_sf.slots, slots), prev_sf.slots.size - 1)
+            hit = prev_sf.slots[j] == slots
+            prev_reg[hit] = prev_sf.arrays["micro_regime"][j[hit]]
+            prev_str[hit] = prev_sf.arrays["micro_regime_strength"][j[hit]]
+        a20, a50 = c > f["ema20"], c > f["ema50"]
+        ann = annotate_symbols(f["trend_score"], a20, a50, rs, f["bb_width"], f["atr_pct"], f["return_pct"],
+                               prev_regime=prev_reg, prev_strength=prev_str)
+        arrays = dict(f, close=c, above_ema20=a20, above_ema50=a50, relative_strength_vs_btc=rs, **ann)
+        names = store.names_array()[slots]
+        sym = SymbolFeatureRows(names, slots, arrays, int(timestamp))
         ctx["symbol_features"] = sym
         ctx["metadata"] = {
-            "btc_fresh": self.btc_symbol in set(names),
+            "btc_fresh": btc_fresh,
             "btc_used_for_regime": btc_valid,
-            "fresh_symbols": sorted(sym),
+            "fresh_symbols": SortedNames(sym.names),
             "fresh_symbol_count": int(ctx["fresh_count"]),
         }
         return ctx

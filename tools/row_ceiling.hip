@@ -1,0 +1,112 @@
+// What limits the one-workgroup-per-symbol streaming structure of the enrich
+// kernel? Variants of a no-arithmetic kernel with the enrich traffic mix
+// (5 fp64 inputs read, 14 written, [S][ld] rows, 1024-candle tiles per WG):
+// allocation stagger between arrays, padded row pitch, swizzled symbol order,
+// workgroup size, register prefetch of the next tile.
+// Build: hipcc -O3 --offload-arch=gfx950 tools/row_ceiling.hip -o tools/row_ceiling
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+constexpr int NIN = 5, NOUT = 14, K = 4;
+
+struct Args {
+  const double* in[NIN];
+  double* out[NOUT];
+  long S, T, ld;
+  int swz;
+};
+
+template <int NT, bool PREFETCH>
+__global__ __launch_bounds__(NT) void row_tiles(Args a) {
+  long sym = blockIdx.x;
+  if (a.swz) sym = (sym * 7919) % a.S;   // scatter concurrently running rows
+  const long base = sym * a.ld;
+  constexpr int TILE = NT * K;
+  dbl2 nx[NIN][2];
+  long tb = threadIdx.x * K;
+  if (PREFETCH && tb < a.T)
+    for (int f = 0; f < NIN; ++f) {
+      const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb);
+      nx[f][0] = p[0];
+      nx[f][1] = p[1];
+    }
+  for (; tb < a.T; tb += TILE) {
+    dbl2 cu[NIN][2];
+    for (int f = 0; f < NIN; ++f) {
+      if (PREFETCH) {
+        cu[f][0] = nx[f][0];
+        cu[f][1] = nx[f][1];
+      } else {
+        const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb);
+        cu[f][0] = p[0];
+        cu[f][1] = p[1];
+      }
+    }
+    if (PREFETCH && tb + TILE < a.T)
+      for (int f = 0; f < NIN; ++f) {
+        const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb + TILE);
+        nx[f][0] = p[0];
+        nx[f][1] = p[1];
+      }
+    dbl2 acc0 = {0, 0}, acc1 = {0, 0};
+    for (int f = 0; f < NIN; ++f) {
+      acc0 += cu[f][0];
+      acc1 += cu[f][1];
+    }
+    for (int o = 0; o < NOUT; ++o) {
+      dbl2* q = reinterpret_cast<dbl2*>(a.out[o] + base + tb);
+      q[0] = acc0 + (double)o;
+      q[1] = acc1;
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  const long S = 12500, T = 10000;
+  const int reps = 10;
+  struct V { const char* name; long pad; long stagger; int swz; int nt; int pf; };
+  const V vs[] = {
+      {"base", 0, 0, 0, 256, 0},        {"prefetch", 0, 0, 0, 256, 1},   {"stagger4k", 0, 4096 + 256, 0, 256, 0},
+      {"stagger64k", 0, 65536 + 1024, 0, 256, 0}, {"pad256B", 32, 0, 0, 256, 0}, {"pad2k", 256, 0, 0, 256, 0},
+      {"swizzle", 0, 0, 1, 256, 0},     {"nt512", 0, 0, 0, 512, 0},      {"nt128", 0, 0, 0, 128, 0},
+      {"stagger+pf", 0, 65536 + 1024, 0, 256, 1},
+  };
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (const V& v : vs) {
+    const long ld = T + v.pad;
+    const size_t arr = (size_t)S * ld * sizeof(double);
+    const size_t slot = arr + v.stagger;   // one allocation, arrays staggered
+    char* buf;
+    CK(hipMalloc(&buf, slot * (NIN + NOUT) + 4096));
+    CK(hipMemset(buf, 0, slot * (NIN + NOUT)));
+    Args a;
+    for (int f = 0; f < NIN; ++f) a.in[f] = (const double*)(buf + slot * f);
+    for (int o = 0; o < NOUT; ++o) a.out[o] = (double*)(buf + slot * (NIN + o));
+    a.S = S;
+    a.T = T;
+    a.ld = ld;
+    a.swz = v.swz;
+    for (int r = 0; r < reps + 2; ++r) {
+      if (r == 2) CK(hipEventRecord(e0));
+      if (v.nt == 512) row_tiles<512, false><<<S, 512>>>(a);
+      else if (v.nt == 128) row_tiles<128, false><<<S, 128>>>(a);
+      else if (v.pf) row_tiles<256, true><<<S, 256>>>(a);
+      else row_tiles<256, false><<<S, 256>>>(a);
+    }
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    const double gb = (double)S * T * 8.0 * (NIN + NOUT) / 1e9;
+    printf("{\"variant\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", v.name, ms, gb / ms * 1e3);
+    CK(hipFree(buf));
+  }
+  return 0;
+}
