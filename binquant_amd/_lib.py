@@ -57,6 +57,12 @@ PARTIAL_COLUMNS = (
 MAX_WINDOW = 126
 MAX_RESAMPLE_FIELDS = 12
 STORE_MAX_BARS = 512
+MICRO_REGIMES = ("TREND_UP", "TREND_DOWN", "RANGE", "VOLATILE", "TRANSITIONAL")
+MICRO_TRANSITIONS = ("VOLATILITY_EXPANSION", "BREAKOUT_UP", "BREAKDOWN", "RECOVERY", "MEAN_REVERSION",
+                     "ENTERED_TREND_UP", "ENTERED_TREND_DOWN", "ENTERED_RANGE", "ENTERED_TRANSITIONAL")
+SCORE_FIELDS = ("confidence", "breadth_score", "btc_alignment_score", "cross_asset_confirmation",
+                "followthrough_score", "adverse_excursion_risk", "override_strength", "supportiveness_score",
+                "adjusted_score")
 AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
@@ -116,6 +122,17 @@ class BqRollJob(ctypes.Structure):
     ]
 
 
+class BqContextScalars(ctypes.Structure):
+    _fields_ = [("confidence", ctypes.c_double), ("long_tailwind", ctypes.c_double),
+                ("short_tailwind", ctypes.c_double), ("btc_regime_score", ctypes.c_double),
+                ("market_stress_score", ctypes.c_double), ("present", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class BqScorerWeights(ctypes.Structure):
+    _fields_ = [("context_weight", ctypes.c_double), ("risk_weight", ctypes.c_double),
+                ("support_weight", ctypes.c_double)]
+
+
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _I32 = ctypes.c_int32
@@ -156,6 +173,10 @@ SIGNATURES: dict[str, tuple] = {
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
     "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
+    "bq_micro_regime": (ctypes.c_int, [_I64] + [_P] * 13 + [_P]),
+    "bq_context_score": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.POINTER(BqContextScalars),
+                                        ctypes.POINTER(BqScorerWeights), _P, _I64, _P]),
+    "bq_cohort_select": (ctypes.c_int, [_I64, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "bq_parse_kline_events": (ctypes.c_int, [ctypes.c_char_p, _I64, _I64, _P, _I64, _P, _P, _PP, _P, _P, _P]),
 }
 

@@ -389,7 +389,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     const size_t lds = (size_t)(ring + 1) * RP_CT * STG_PITCH * sizeof(double);
     static bool lds_opt_in = false;   // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     if (!lds_opt_in) {
-      hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       lds_opt_in = true;
     }
     hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,

@@ -36,7 +36,9 @@ import torch.distributed as dist
 
 from .. import _lib, engine
 from .._lib import FEATURE_COLUMNS, INPUT_FIELDS
-from .regime import MIN_COVERAGE_RATIO, REQUIRED_FRESH_SYMBOLS, annotate_market, annotate_symbols, score_contexts
+from .._lib import MICRO_TRANSITIONS
+from .regime import MIN_COVERAGE_RATIO, REQUIRED_FRESH_SYMBOLS, annotate_market, score_contexts
+from .scoring import labels, micro_regime
 
 STORE_COLUMNS = ["timestamp", "open", "high", "low", "close", "volume"]
 
@@ -103,8 +105,10 @@ class SymbolFeatureRows(Mapping):
     micro-regime annotation), backed by column arrays (`.arrays`, `.slots`,
     `.names`): the per-symbol dict is only built when a symbol is looked up."""
 
-    def __init__(self, names: np.ndarray, slots: np.ndarray, arrays: dict[str, np.ndarray], timestamp: int):
+    def __init__(self, names: np.ndarray, slots: np.ndarray, arrays: dict[str, np.ndarray], timestamp: int,
+                 codes: np.ndarray | None = None):
         self.names, self.slots, self.arrays, self.timestamp = names, slots, arrays, timestamp
+        self.codes = codes   # int8 micro-regime codes (bq_micro_regime), chained into the next context
         self._row: dict[str, int] | None = None
 
     def _index(self) -> dict[str, int]:
@@ -443,30 +447,40 @@ class DeviceLiveMarketContextAccumulator:
         # this rank's fresh symbols with relative strength + micro regime
         # (regime_transitions.py:162-232), previous micro regime chained by
         # slot; everything vectorised, per-symbol dicts built on access only
-        stacked = torch.stack([feats[k][:n_fresh] for k in FEATURE_COLUMNS] + [close[:n_fresh]]).cpu().numpy()
-        f = dict(zip(FEATURE_COLUMNS, stacked[:-1]))
-        c = stacked[-1]
+        # micro regime of every fresh symbol on the device (bq_micro_regime);
+        # the previous context's regimes are matched by slot on the host
         slots = fresh.cpu().numpy()
-        ok = ~np.isnan(f["return_pct"])
-        slots, c = slots[ok], c[ok]
-        f = {k: v[ok] for k, v in f.items()}
-        rs = f["return_pct"] - btc_ret if btc_valid else np.zeros_like(f["return_pct"])
-        if btc_slot is not None:
-            rs[slots == btc_slot] = 0.0
         prev_sf = (previous or {}).get("symbol_features")
-        prev_reg = np.full(slots.size, None, dtype=object)
+        prev_code = np.full(slots.size, -1, dtype=np.int8)
         prev_str = np.zeros(slots.size)
         if isinstance(prev_sf, SymbolFeatureRows) and prev_sf.slots.size:
             j = np.minimum(np.searchsorted(prev_sf.slots, slots), prev_sf.slots.size - 1)
             hit = prev_sf.slots[j] == slots
-            prev_reg[hit] = prev_sf.arrays["micro_regime"][j[hit]]
+            prev_code[hit] = prev_sf.codes[j[hit]]
             prev_str[hit] = prev_sf.arrays["micro_regime_strength"][j[hit]]
-        a20, a50 = c > f["ema20"], c > f["ema50"]
-        ann = annotate_symbols(f["trend_score"], a20, a50, rs, f["bb_width"], f["atr_pct"], f["return_pct"],
-                               prev_regime=prev_reg, prev_strength=prev_str)
-        arrays = dict(f, close=c, above_ema20=a20, above_ema50=a50, relative_strength_vs_btc=rs, **ann)
+        fd = {k: v[:n_fresh] for k, v in feats.items()}
+        cd = close[:n_fresh]
+        rs_d = fd["return_pct"] - btc_ret if btc_valid else torch.zeros_like(fd["return_pct"])
+        if btc_slot is not None:
+            rs_d = torch.where(fresh == btc_slot, torch.zeros_like(rs_d), rs_d)
+        a20, a50 = cd > fd["ema20"], cd > fd["ema50"]
+        ann = micro_regime(fd["trend_score"], a20, a50, rs_d, fd["bb_width"], fd["atr_pct"], fd["return_pct"],
+                           prev_regime=prev_code, prev_strength=prev_str, device=dev)
+        stacked = torch.stack([fd[k] for k in FEATURE_COLUMNS] + [
+            cd, rs_d, a20.double(), a50.double(), ann["micro_regime"].double(), ann["micro_regime_strength"],
+            ann["micro_regime_transition"].double(), ann["micro_regime_transition_strength"]]).cpu().numpy()
+        nf = len(FEATURE_COLUMNS)
+        ok = ~np.isnan(stacked[0])
+        stacked, slots = stacked[:, ok], slots[ok]
+        codes = stacked[nf + 4].astype(np.int8)
+        arrays = dict(zip(FEATURE_COLUMNS, stacked[:nf]))
+        arrays.update(close=stacked[nf], relative_strength_vs_btc=stacked[nf + 1], above_ema20=stacked[nf + 2] > 0,
+                      above_ema50=stacked[nf + 3] > 0, micro_regime=labels(codes),
+                      micro_regime_strength=stacked[nf + 5],
+                      micro_regime_transition=labels(stacked[nf + 6].astype(np.int8), MICRO_TRANSITIONS),
+                      micro_regime_transition_strength=stacked[nf + 7])
         names = store.names_array()[slots]
-        sym = SymbolFeatureRows(names, slots, arrays, int(timestamp))
+        sym = SymbolFeatureRows(names, slots, arrays, int(timestamp), codes)
         ctx["symbol_features"] = sym
         ctx["metadata"] = {
             "btc_fresh": btc_fresh,

@@ -41,6 +41,10 @@
  *                         and _compute_symbol_features on its histories
  *   bq_parse_kline_events <- json.loads + KlineProduceModel of the websocket
  *                         frames, producers/klines_connector.py:77-164 (host)
+ *   bq_micro_regime    <- regime_transitions.py:162-232 (per-symbol micro regime)
+ *   bq_context_score   <- context_scoring.py:13-114 + signal_context_scorer.py:15-55
+ *   bq_cohort_select   <- the portfolio selectors' winner pick
+ *                         (liquidation_sweep_pump.py:38-87, gradual_gainer_retest.py:33-70)
  *   bq_breadth_partial <- the per-symbol sums/counts of
  *                         LiveMarketContextAccumulator._build_context
  *                         market_regime/live_market_context_accumulator.py:135-163
@@ -372,6 +376,61 @@ int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_s
  */
 int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,
                     double* const* out, int64_t ld_out, void* stream);
+
+/* ---- regime annotation, candidate scoring, portfolio selection -------------- */
+enum bq_micro_regime_code {   /* models.py:15-21 MicroRegime; -1 = None */
+  BQ_MICRO_TREND_UP = 0, BQ_MICRO_TREND_DOWN = 1, BQ_MICRO_RANGE = 2, BQ_MICRO_VOLATILE = 3,
+  BQ_MICRO_TRANSITIONAL = 4
+};
+enum bq_micro_transition_code {   /* models.py:32-42 MicroRegimeTransition; -1 = None */
+  BQ_MT_VOLATILITY_EXPANSION = 0, BQ_MT_BREAKOUT_UP, BQ_MT_BREAKDOWN, BQ_MT_RECOVERY, BQ_MT_MEAN_REVERSION,
+  BQ_MT_ENTERED_TREND_UP, BQ_MT_ENTERED_TREND_DOWN, BQ_MT_ENTERED_RANGE, BQ_MT_ENTERED_TRANSITIONAL
+};
+/*
+ * RegimeTransitionDetector._annotate_symbol_regime (market_regime/regime_transitions.py:162-232)
+ * for n symbols: device arrays of the SymbolMarketFeatures fields; prev_regime
+ * (int8, -1 = None; NULL = no previous context) / prev_strength chain the
+ * transition. Outputs regime/strength (+ transition / transition_strength,
+ * NULL = skip). Bit-exact with the Python floats.
+ */
+int bq_micro_regime(int64_t n, const double* trend, const uint8_t* above_ema20, const uint8_t* above_ema50,
+                    const double* rs, const double* bb_width, const double* atr_pct, const double* return_pct,
+                    const int8_t* prev_regime, const double* prev_strength, int8_t* regime, double* strength,
+                    int8_t* transition, double* transition_strength, void* stream);
+
+enum bq_direction { BQ_DIR_LONG = 0, BQ_DIR_SHORT = 1, BQ_DIR_OTHER = 2 };   /* direction.upper().strip() */
+typedef struct bq_context_scalars {   /* the LiveMarketContext fields the scorer reads */
+  double confidence, long_tailwind, short_tailwind, btc_regime_score, market_stress_score;
+  int32_t present;                    /* 0: no context (None) */
+  int32_t reserved;
+} bq_context_scalars;
+typedef struct bq_scorer_weights {    /* SignalContextScorer (signal_context_scorer.py:10-13) */
+  double context_weight, risk_weight, support_weight;
+} bq_scorer_weights;
+enum bq_score_field {   /* MarketContextScore fields + the adjusted score; out[field][ld_out] */
+  BQ_SC_CONFIDENCE = 0, BQ_SC_BREADTH, BQ_SC_BTC_ALIGNMENT, BQ_SC_CROSS_ASSET, BQ_SC_FOLLOWTHROUGH,
+  BQ_SC_ADVERSE, BQ_SC_OVERRIDE, BQ_SC_SUPPORTIVENESS, BQ_SC_ADJUSTED, BQ_NUM_SCORE_FIELDS
+};
+/*
+ * RuleBasedMarketContextModel.evaluate (market_regime/context_scoring.py:13-114)
+ * + SignalContextScorer.adjust_score (signal_context_scorer.py:15-28) for n
+ * candidates against one context: direction (bq_direction), rs / trend (the
+ * candidate's local_features or its snapshot row, resolved by the caller),
+ * local_score (NULL = 0). out: BQ_NUM_SCORE_FIELDS x ld_out doubles.
+ */
+int bq_context_score(int64_t n, const int8_t* direction, const double* rs, const double* trend,
+                     const double* local_score, const bq_context_scalars* ctx, const bq_scorer_weights* weights,
+                     double* out, int64_t ld_out, void* stream);
+/*
+ * Portfolio winners (strategies/liquidation_sweep_pump.py:38-87,
+ * strategies/gradual_gainer_retest.py:33-70): per cohort (dense ids
+ * 0..n_cohorts-1) the accepted candidate (accepted NULL = all) with the
+ * largest (score, symbol_rank), the latest submission on a full tie.
+ * winner[n_cohorts]: candidate index or -1. scratch: 2*n_cohorts u64 (device).
+ */
+int bq_cohort_select(int64_t n, const int32_t* cohort, const uint8_t* accepted, const double* score,
+                     const int32_t* symbol_rank, int32_t n_cohorts, unsigned long long* scratch, int64_t* winner,
+                     void* stream);
 
 /* ---- wire-format ingest (host) ------------------------------------------------ */
 /*

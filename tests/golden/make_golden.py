@@ -425,7 +425,116 @@ def child(out_dir: Path) -> None:
 
     # ---- 9. MarketStateStore + accumulator under a scripted feed ---------------------
     store_sequence(out_dir, context_dict)
+    # ---- 10. candidate scoring and portfolio selection ------------------------------
+    scoring_and_selection(out_dir)
     print("golden fixtures written to", out_dir)
+
+
+def scoring_and_selection(out_dir: Path) -> None:
+    """context_scoring.json: RuleBasedMarketContextModel.evaluate
+    (market_regime/context_scoring.py:13-114) + SignalContextScorer
+    (market_regime/signal_context_scorer.py:15-55) and
+    score_signal_candidate_with_context's emit gate on random contexts and
+    candidates (LONG/SHORT, in/out of the snapshot, local_features overrides,
+    no context, zero confidence).
+    portfolio.json: LiquidationSweepPortfolioSelector
+    (strategies/liquidation_sweep_pump.py:38-87) and
+    GradualGainerPortfolioSelector (strategies/gradual_gainer_retest.py:33-70)
+    driven with asyncio on random submission streams (late candidates, ties,
+    re-submissions of a symbol); records submit() results and the dispatch order."""
+    import asyncio
+
+    import numpy as np
+
+    from market_regime.models import LiveMarketContext, SymbolMarketFeatures
+    from market_regime.score_signal_candidate_with_context import score_signal_candidate_with_context
+    from market_regime.signal_context_scorer import SignalContextScorer
+    from strategies.gradual_gainer_retest import GradualGainerCandidate, GradualGainerPortfolioSelector
+    from strategies.liquidation_sweep_pump import LiquidationSweepCandidate, LiquidationSweepPortfolioSelector
+
+    rng = np.random.default_rng(4242)
+    syms = [f"C{i:02d}USDT" for i in range(30)]
+    cases = []
+    for k in range(40):
+        feats = {}
+        for s in syms[: int(rng.integers(0, 30))]:
+            feats[s] = SymbolMarketFeatures(
+                symbol=s, timestamp=1000, close=1.0, return_pct=float(rng.normal(0, 0.02)), ema20=1.0, ema50=1.0,
+                above_ema20=bool(rng.random() < 0.5), above_ema50=bool(rng.random() < 0.5),
+                trend_score=float(rng.normal(0, 0.03)), relative_strength_vs_btc=float(rng.normal(0, 0.03)),
+                atr_pct=0.01, bb_width=0.05)
+        ctx = None
+        if k % 9 != 0:
+            ctx = LiveMarketContext(
+                timestamp=1000 + k, fresh_count=40, total_tracked_symbols=50, coverage_ratio=0.8, btc_symbol="BTCUSDT",
+                btc_present=True, confidence=float(0.0 if k % 13 == 0 else rng.uniform(0.2, 1.0)),
+                is_provisional=False, advancers=20, decliners=20, advancers_ratio=0.5, decliners_ratio=0.5,
+                advancers_decliners_ratio=1.0, average_return=0.0, average_relative_strength_vs_btc=0.0,
+                pct_above_ema20=0.5, pct_above_ema50=0.5, average_trend_score=0.0, average_atr_pct=0.01,
+                average_bb_width=0.05, btc_return=0.0, btc_trend_score=0.0,
+                btc_regime_score=float(rng.uniform(-1, 1)), market_stress_score=float(rng.uniform(0, 1)),
+                long_tailwind=float(rng.uniform(-1, 1)), short_tailwind=float(rng.uniform(-1, 1)),
+                symbol_features=feats)
+        weights = dict(context_weight=float(rng.uniform(0, 1.5)), risk_weight=float(rng.uniform(0, 1)),
+                       support_weight=float(rng.uniform(0, 1)))
+        scorer = SignalContextScorer(**weights)
+        cands = []
+        for j in range(12):
+            sym = syms[int(rng.integers(0, 30))]
+            direction = ["LONG", "SHORT", " long ", "short"][int(rng.integers(0, 4))]
+            local = {}   # SignalContextEvaluation rejects None (models.py)
+            if rng.random() < 0.4:
+                if rng.random() < 0.7:
+                    local["relative_strength_vs_btc"] = float(rng.normal(0, 0.05))
+                if rng.random() < 0.7:
+                    local["trend_score"] = float(rng.normal(0, 0.05))
+            score = float(rng.uniform(-1, 2))
+            thr = None if rng.random() < 0.3 else float(rng.uniform(0, 1.5))
+            ev = score_signal_candidate_with_context(sym, direction, score, ctx, scorer, local_features=local,
+                                                     emit_threshold=thr)
+            cs = ev.context_score
+            cands.append(dict(symbol=sym, direction=direction, local_score=score, local_features=local,
+                              emit_threshold=thr, adjusted_score=ev.adjusted_score, emit=ev.emit,
+                              score={k2: getattr(cs, k2) for k2 in (
+                                  "direction", "confidence", "breadth_score", "btc_alignment_score",
+                                  "cross_asset_confirmation", "followthrough_score", "adverse_excursion_risk",
+                                  "override_strength", "supportiveness_score")}))
+        cases.append(dict(weights=weights, context=None if ctx is None else dict(
+            confidence=ctx.confidence, long_tailwind=ctx.long_tailwind, short_tailwind=ctx.short_tailwind,
+            btc_regime_score=ctx.btc_regime_score, market_stress_score=ctx.market_stress_score, timestamp=ctx.timestamp,
+            symbol_features={s: dict(relative_strength_vs_btc=f.relative_strength_vs_btc, trend_score=f.trend_score)
+                             for s, f in feats.items()}), candidates=cands))
+    with open(out_dir / "context_scoring.json", "w") as f:
+        json.dump(cases, f, separators=(",", ":"))
+
+    async def drive(selector_cls, cand_cls, stream):
+        sel = selector_cls()
+        dispatched, accepted = [], []
+        for i, (t, s, sc) in enumerate(stream):
+            async def disp(i=i):
+                dispatched.append(i)
+            accepted.append(await sel.submit(cand_cls(candle_open_time=t, symbol=s, rank_score=sc, dispatch=disp)))
+        await sel.flush()
+        return accepted, dispatched
+
+    runs = {}
+    for name, sel_cls, cand_cls, step in (("liquidation", LiquidationSweepPortfolioSelector, LiquidationSweepCandidate,
+                                           900_000),
+                                          ("gradual", GradualGainerPortfolioSelector, GradualGainerCandidate, 900_000)):
+        streams = []
+        for k in range(6):
+            n = int(rng.integers(20, 400))
+            base = 1_760_000_000_000
+            t = base + step * np.cumsum(rng.integers(0, 2, n) * (rng.random(n) < 0.3))
+            late = rng.random(n) < 0.1
+            t = np.where(late, t - step * rng.integers(1, 4, n), t)
+            st = [(int(t[i]), syms[int(rng.integers(0, 12))],
+                   float(np.round(rng.normal(0, 1), 1 if k % 2 else 6))) for i in range(n)]
+            acc, disp = asyncio.run(drive(sel_cls, cand_cls, st))
+            streams.append(dict(stream=st, accepted=acc, dispatched=disp))
+        runs[name] = streams
+    with open(out_dir / "portfolio.json", "w") as f:
+        json.dump(runs, f, separators=(",", ":"))
 
 
 def store_sequence(out_dir: Path, context_dict) -> None:
