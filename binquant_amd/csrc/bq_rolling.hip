@@ -70,7 +70,7 @@ struct RollBatch {
 };
 
 // ---- replay kernels (lane = symbol) --------------------------------------------------
-constexpr int RP_CT = 32;
+constexpr int RP_CT = 16;
 
 // pandas roll_sum / roll_mean / roll_var state, updated value by value
 struct Moments {
@@ -160,24 +160,29 @@ struct Moments {
   }
 };
 
-// LDS: a ring of the last `ring` (a power of two) input chunks, x-index
-// aligned, + one result
-// tile; the ring covers window + shift, so the leaving value is an LDS read
-// and every input byte crosses HBM once.
+// LDS: a ring of the last `ring` input chunks (RL = ring * RP_CT candles per
+// lane, lane-interleaved); the ring covers window + shift, so the leaving
+// value is an LDS read and every input byte crosses HBM once. Results go
+// straight from each lane to its row (consecutive steps fill a cache line
+// in L2 before it is written back), which keeps the LDS per wave small
+// enough for several waves per CU.
 __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int ring) {
   const RollJob& A = B.j[blockIdx.y];   // wave-uniform: scalar kernarg loads
   const bool EWM = A.mode == BQ_ROLL_EWM;
   extern __shared__ double smem[];
   constexpr int TILE = RP_CT * STG_PITCH;
-  double* sRes = smem + ring * TILE;
+  const int RL = ring * RP_CT;
   const int lane = threadIdx.x;
   const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
   const int64_t S = B.S;
   const int T = B.T, w = A.win, sh = A.shift;
   const bool welford = A.mode >= BQ_ROLL_VAR;
-  auto xval = [&](int i) -> double {   // x[i] of this lane's symbol, i within the ring
-    return i < 0 ? qnan() : smem[((i / RP_CT) & (ring - 1)) * TILE + (i % RP_CT) * STG_PITCH + lane];
-  };
+  const bool live = sym0 + lane < S;
+  double* __restrict__ orow = A.out + (live ? sym0 + lane : 0) * A.ld_out;
+  // ring positions of the entering (t - sh) and leaving (t - sh - w) values,
+  // advanced by one per step (no division in the loop)
+  auto wrap = [&](int i) { return ((i % RL) + RL) % RL; };
+  int pin = wrap(-sh), pout = wrap(-sh - w);
   double ri[RP_CT];
   stage_load<RP_CT>(A.x, A.ld_in, sym0, S, 0, T, lane, ri);
   Moments m;
@@ -187,14 +192,14 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
   int nobs = 0;
   const double alpha = A.alpha, om = 1.0 - alpha;
   for (int t0 = 0; t0 < T; t0 += RP_CT) {
-    stage_put<RP_CT>(smem + ((t0 / RP_CT) & (ring - 1)) * TILE, lane, ri);
+    stage_put<RP_CT>(smem + ((t0 / RP_CT) % ring) * TILE, lane, ri);
     __syncthreads();
     if (t0 + RP_CT < T)   // next chunk in flight during this one's replay
       stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT, T, lane, ri);
     auto step = [&](int j) {
       const int t = t0 + j;
-      const int x = j * STG_PITCH + lane;
-      const double v_in = xval(t - sh);
+      const double v_in = t - sh < 0 ? qnan() : smem[pin * STG_PITCH + lane];
+      pin = pin + 1 == RL ? 0 : pin + 1;
       double res;
       if (EWM) {
         if (t == 0) {
@@ -219,11 +224,12 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
         res = nobs >= A.minp ? weighted : qnan();
       } else {
         if (t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
-        if (t >= w) m.remove(xval(t - sh - w), welford);
+        if (t >= w && t - sh - w >= 0) m.remove(smem[pout * STG_PITCH + lane], welford);
+        pout = pout + 1 == RL ? 0 : pout + 1;
         m.add(v_in, welford);
         res = m.result(A.mode, A.minp);
       }
-      sRes[x] = res;
+      if (live) orow[t] = res;
     };
     if (t0 + RP_CT <= T) {
       // full chunk: unrolled, so each step's result / LDS traffic overlaps
@@ -233,8 +239,7 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
     } else {
       for (int j = 0; j < T - t0; ++j) step(j);
     }
-    __syncthreads();
-    stage_store<RP_CT>(sRes, A.out, A.ld_out, sym0, S, t0, T, lane);
+    __syncthreads();   // the ring slot of this chunk is reused RL candles later
   }
 }
 
@@ -384,9 +389,8 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   int max_back = 0;   // window + shift of the replay jobs in the batch
   auto flush_rep = [&]() {
     if (!nrep) return;
-    int ring = 1;
-    while (ring < (max_back + RP_CT - 1) / RP_CT + 1) ring <<= 1;
-    const size_t lds = (size_t)(ring + 1) * RP_CT * STG_PITCH * sizeof(double);
+    const int ring = (max_back + RP_CT - 1) / RP_CT + 1;
+    const size_t lds = (size_t)ring * RP_CT * STG_PITCH * sizeof(double);
     static bool lds_opt_in = false;   // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     if (!lds_opt_in) {
       (void)hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -430,10 +434,20 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       rep.j[nrep++] = J;
       if (nrep == RW_MAXJOBS) flush_rep();
     } else {
-      // segments: enough lanes to fill the chip (~32k), each >= 4 windows long
-      const int64_t want = (32768 + S - 1) / S;
-      int seg = (int)((T + want - 1) / want);
-      seg = seg < 4 * in.window ? 4 * in.window : seg;
+      // segments: lanes = (symbol, segment). Enough lanes to fill the SIMDs to
+      // the kernel's occupancy (waves per SIMD set by the window's register
+      // footprint), but no more than ~80k-130k: every lane streams its own
+      // row lines through L2, and beyond that the lines are evicted before
+      // their 16 values are used (measured: tools/segx.py sweep). Each
+      // segment re-reads one window of warm-up values.
+      static const int occ[6] = {8, 6, 3, 2, 2, 1};   // rank_kernel<8,24,48,64,80,96>
+      static const int64_t cap[6] = {80000, 80000, 100000, 131072, 131072, 65536};
+      const int b0 = rank_bucket(in.window);
+      int64_t lanes = (int64_t)1024 * occ[b0] * WAVE;
+      lanes = lanes < cap[b0] ? lanes : cap[b0];
+      const int64_t nseg_t = lanes / S > 1 ? lanes / S : 1;
+      int seg = (int)((T + nseg_t - 1) / nseg_t);
+      seg = seg < in.window ? in.window : seg;
       J.seg = seg;
       J.nseg = (int)((T + seg - 1) / seg);
       const int b = rank_bucket(in.window);

@@ -22,6 +22,8 @@ struct Args {
 
 template <int NT, bool PREFETCH>
 __global__ __launch_bounds__(NT) void row_tiles(Args a) {
+  extern __shared__ double occupancy_limiter[];   // dynamic LDS only limits WGs/CU
+  if (a.S < 0) occupancy_limiter[threadIdx.x] = 0.0;
   long sym = blockIdx.x;
   if (a.swz) sym = (sym * 7919) % a.S;   // scatter concurrently running rows
   const long base = sym * a.ld;
@@ -68,12 +70,13 @@ __global__ __launch_bounds__(NT) void row_tiles(Args a) {
 int main(int argc, char** argv) {
   const long S = 12500, T = 10000;
   const int reps = 10;
-  struct V { const char* name; long pad; long stagger; int swz; int nt; int pf; };
+  struct V { const char* name; long pad; long stagger; int swz; int nt; int pf; int lds; };
   const V vs[] = {
-      {"base", 0, 0, 0, 256, 0},        {"prefetch", 0, 0, 0, 256, 1},   {"stagger4k", 0, 4096 + 256, 0, 256, 0},
-      {"stagger64k", 0, 65536 + 1024, 0, 256, 0}, {"pad256B", 32, 0, 0, 256, 0}, {"pad2k", 256, 0, 0, 256, 0},
-      {"swizzle", 0, 0, 1, 256, 0},     {"nt512", 0, 0, 0, 512, 0},      {"nt128", 0, 0, 0, 128, 0},
-      {"stagger+pf", 0, 65536 + 1024, 0, 256, 1},
+      {"base", 0, 0, 0, 256, 0, 0},          {"prefetch", 0, 0, 0, 256, 1, 0},
+      {"base_3wg", 0, 0, 0, 256, 0, 52000},  {"prefetch_3wg", 0, 0, 0, 256, 1, 52000},
+      {"prefetch_4wg", 0, 0, 0, 256, 1, 39000}, {"prefetch_2wg", 0, 0, 0, 256, 1, 78000},
+      {"swizzle_pf_3wg", 0, 0, 1, 256, 1, 52000}, {"stagger+pf", 0, 65536 + 1024, 0, 256, 1, 0},
+      {"stagger+pf_3wg", 0, 65536 + 1024, 0, 256, 1, 52000}, {"prefetch_again", 0, 0, 0, 256, 1, 0},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -94,10 +97,8 @@ int main(int argc, char** argv) {
     a.swz = v.swz;
     for (int r = 0; r < reps + 2; ++r) {
       if (r == 2) CK(hipEventRecord(e0));
-      if (v.nt == 512) row_tiles<512, false><<<S, 512>>>(a);
-      else if (v.nt == 128) row_tiles<128, false><<<S, 128>>>(a);
-      else if (v.pf) row_tiles<256, true><<<S, 256>>>(a);
-      else row_tiles<256, false><<<S, 256>>>(a);
+      if (v.pf) row_tiles<256, true><<<S, 256, v.lds>>>(a);
+      else row_tiles<256, false><<<S, 256, v.lds>>>(a);
     }
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
