@@ -10,7 +10,9 @@
 //     candle of that window. Computed from the full-history EMA Y (affine scan,
 //     as in bq_enrich) with the exact windowing identity
 //       y_t = Y_t - a^(M-1) * (Y_s - c_s),  s = t - M + 1,
-//     which needs Y and close M-1 candles back: the LDS halo is 512 candles.
+//     which needs Y_s - c_s M-1 candles back: that difference is kept in
+//     LDS with a 512-candle halo; close and the prefix sums only need the
+//     short windows' 32-candle halo (LDS 50 KB: 3 workgroups per CU).
 //   * ATR = TR.rolling(14, min_periods=1).mean(); BB mid/std(ddof=0) over
 //     rolling(20, min_periods=1): compensated prefix-sum differences with the
 //     pandas constant-window rules, two-pass variance.
@@ -30,8 +32,10 @@ constexpr int MF_NT = 256;
 constexpr int MF_NW = MF_NT / WAVE;
 constexpr int MF_K = 4;
 constexpr int MF_TT = MF_NT * MF_K;
-constexpr int MF_H = BQ_MAX_HISTORY;
+constexpr int MF_H = BQ_MAX_HISTORY;   // halo of the window-seeded EMA terms
 constexpr int MF_R = MF_H + MF_TT;
+constexpr int MF_HS = 32;              // halo of the short windows (ATR 14, BB 20)
+constexpr int MF_RS = MF_HS + MF_TT;
 constexpr int ATR_W = 14;   // live_market_context_accumulator.py:268
 constexpr int BB_W = 20;    // :269-270
 
@@ -76,8 +80,8 @@ __device__ __forceinline__ void mf_store(double* __restrict__ row, int tb, int T
 }
 
 __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int vec_in, int vec_out) {
-  __shared__ double sPc[MF_R], sPt[MF_R], sC[MF_R];
-  __shared__ double sY[2][MF_R];
+  __shared__ double sPc[MF_RS], sPt[MF_RS], sC[MF_RS];
+  __shared__ double sD[2][MF_R];   // Y_e - close (EMA window identity)
   __shared__ double sX[4][MF_NW + 1];   // c, c[-2], h, l of each wave's last candle
   __shared__ double sWh[2][MF_NW], sWl[2][MF_NW], sWe[2][MF_NW];
   __shared__ int sWlc[2][MF_NW];
@@ -98,17 +102,20 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
   }
   if (tid < 4) sX[tid][0] = qnan();
   for (int i = tid; i < MF_H; i += MF_NT) {
-    sPc[i] = 0.0;
-    sPt[i] = 0.0;
-    sC[i] = qnan();
-    sY[0][i] = qnan();
-    sY[1][i] = qnan();
+    sD[0][i] = qnan();
+    sD[1][i] = qnan();
+  }
+  if (tid < MF_HS) {
+    sPc[tid] = 0.0;
+    sPt[tid] = 0.0;
+    sC[tid] = qnan();
   }
   __syncthreads();
 
   for (int t0 = 0; t0 < T; t0 += MF_TT) {
     const int tb = t0 + MF_K * tid;
-    const int pb = MF_H + MF_K * tid;
+    const int pb = MF_H + MF_K * tid;     // position in the long-halo arrays
+    const int qb = MF_HS + MF_K * tid;    // position in the short-halo arrays
     double h[MF_K], l[MF_K], c[MF_K];
     mf_load(rH, tb, T, vin, h);
     mf_load(rL, tb, T, vin, l);
@@ -125,7 +132,7 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       sX[3][w + 1] = l[MF_K - 1];
     }
 #pragma unroll
-    for (int k = 0; k < MF_K; ++k) sC[pb + k] = c[k];
+    for (int k = 0; k < MF_K; ++k) sC[qb + k] = c[k];
     __syncthreads();   // B1
     if (lane == 0) {
       pc1 = sX[0][w];
@@ -208,8 +215,8 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       for (int k = 0; k < MF_K; ++k) {
         bc = dd_add1(bc, c[k]);
         bt = dd_add1(bt, tr[k]);
-        sPc[pb + k] = dd_round(bc);
-        sPt[pb + k] = dd_round(bt);
+        sPc[qb + k] = dd_round(bc);
+        sPt[qb + k] = dd_round(bt);
       }
       int cc = sLcar[0], ct = sLcar[1];
       for (int u = 0; u < w; ++u) {
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
         if (tb + k == 0) y = x;
         else if (y != x) y = (om * y + al * x) / dn;
         Y[e][k] = y;
-        sY[e][pb + k] = y;
+        sD[e][pb + k] = y - x;
       }
     }
     __syncthreads();   // B3
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
     double fr[MF_K], fe20[MF_K], fe50[MF_K], ftr[MF_K], fap[MF_K], fbw[MF_K];
 #pragma unroll
     for (int k = 0; k < MF_K; ++k) {
-      const int t = tb + k, p = pb + k;
+      const int t = tb + k, p = pb + k, q = qb + k;
       const int n = min(t + 1, M);
       if (n < 2) {   // history.empty or len < 2 -> None (:248-249)
         fr[k] = fe20[k] = fe50[k] = ftr[k] = fap[k] = fbw[k] = qnan();
@@ -257,16 +264,15 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       double e20 = Y[0][k], e50 = Y[1][k];
       if (t + 1 > M) {   // history window starts at s = t - M + 1 > 0
         const int ps = p - M + 1;
-        const double cs = sC[ps];
-        e20 = e20 - A.corr[0] * (sY[0][ps] - cs);
-        e50 = e50 - A.corr[1] * (sY[1][ps] - cs);
+        e20 = e20 - A.corr[0] * sD[0][ps];
+        e50 = e50 - A.corr[1] * sD[1][ps];
       }
       // ATR: TR.rolling(14, min_periods=1).mean() at the last row (:268)
       const int ma = min(ATR_W, n);
       double atr;
       if (lct[k] <= t - ma + 1) atr = tr[k];
       else {
-        double S = sPt[p] - sPt[p - ma];
+        double S = sPt[q] - sPt[q - ma];
         atr = (S < 0.0 ? 0.0 : S) / (double)ma;
       }
       // BB: rolling(20, min_periods=1) mean / std(ddof=0).fillna(0) (:269-272)
@@ -276,9 +282,9 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
         mid = cl;
         sd = 0.0;
       } else {
-        mid = (sPc[p] - sPc[p - mb]) / (double)mb;
+        mid = (sPc[q] - sPc[q - mb]) / (double)mb;
         double acc = 0.0;
-        for (int i = p - mb + 1; i <= p; ++i) {
+        for (int i = q - mb + 1; i <= q; ++i) {
           const double d = sC[i] - mid;
           acc = fma(d, d, acc);
         }
@@ -303,12 +309,14 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
     if (t0 + MF_TT >= T) break;
     __syncthreads();   // B4
     for (int i = tid; i < MF_H; i += MF_NT) {
-      const int src = MF_TT + i;
-      sPc[i] = sPc[src] - sPc[MF_R - 1];
-      sPt[i] = sPt[src] - sPt[MF_R - 1];
-      sC[i] = sC[src];
-      sY[0][i] = sY[0][src];
-      sY[1][i] = sY[1][src];
+      sD[0][i] = sD[0][MF_TT + i];
+      sD[1][i] = sD[1][MF_TT + i];
+    }
+    if (tid < MF_HS) {   // short halos; prefixes re-based to the tile end
+      const int src = MF_TT + tid;
+      sPc[tid] = sPc[src] - sPc[MF_RS - 1];
+      sPt[tid] = sPt[src] - sPt[MF_RS - 1];
+      sC[tid] = sC[src];
     }
     if (tid < 4) sX[tid][0] = sX[tid][MF_NW];
     if (tid == MF_NT - 1) {
