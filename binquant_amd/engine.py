@@ -603,3 +603,14 @@ def beta_corr_pairs(x: torch.Tensor, y: torch.Tensor, window: int = 50,
                                         _stream_handle(stream))
     _lib.check(st, "bq_beta_corr_pairs")
     return {"beta": beta, "corr": corr}
+
+
+def pct_change(x: torch.Tensor, periods: int = 1) -> torch.Tensor:
+    """x.pct_change(periods) along T of a [S, T] panel (pandas:
+    x / x.shift(periods) - 1; NaN for the first `periods` rows). Device
+    element-wise, same IEEE operations as pandas."""
+    x = _check_panel(x, "x")
+    out = torch.full_like(x, float("nan"))
+    if periods < x.shape[1]:
+        out[:, periods:] = x[:, periods:] / x[:, :-periods] - 1
+    return out

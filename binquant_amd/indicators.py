@@ -277,8 +277,10 @@ def dynamic_btc_beta_corr_frames(frames: Sequence[pd.DataFrame], df_btc: pd.Data
 
 def btc_price_change(df_btc: pd.DataFrame, periods: int = 96) -> float:
     """BTC 24h change of ContextEvaluator.process_data (producers/context_evaluator.py:427-430):
-    close.pct_change(periods=96) * 100 at the last row (scalar; host arithmetic)."""
+    close.pct_change(periods=96) * 100 at the last row, on the device
+    (engine.pct_change); NaN when the frame is too short."""
     c = pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)
     if len(c) <= periods:
         return float("nan")
-    return float((c[-1] / c[-1 - periods] - 1.0) * 100)
+    x = torch.from_numpy(c[-periods - 1 :]).to(_device())[None, :]
+    return float(engine.pct_change(x, periods)[0, -1] * 100)

@@ -134,3 +134,47 @@ def test_row_stride_and_rejects_bad_input(cuda):
     with pytest.raises(ValueError):
         engine.enrich(t["open"], t["high"], t["low"], t["close"], t["volume"],
                       params=engine.IndicatorParams(ma_periods=(7, 25, 500)))
+
+
+def test_c2_batch_matches_oracle(cuda):
+    """BASELINE config C2: 1k symbols x 1k candles (per-symbol price scales
+    10^U(-4,4), constant runs, zero-volume bars) against the per-symbol pandas
+    oracle, every column, every candle."""
+    panel = numpy_panel(1000, 1000, seed0=2026)
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    compare(got, want, panel)
+
+
+def test_c4_shard_size_properties(cuda):
+    """At the C4 shard (12 500 x 10 000, generated in HBM): a sample of rows
+    equals the oracle, the NaN warm-up pattern is exact for every row, and
+    size-independent identities hold everywhere: bb_mid == ma_20-equivalent
+    mean (bb_upper + bb_lower) / 2, macd == ema12 - ema26 sign structure,
+    0 <= rsi, mfi <= 100."""
+    from binquant_amd.synth import device_panel
+
+    S, T = 12_500, 10_000
+    p = device_panel(S, T, seed=77)
+    out = engine.enrich(p["open"], p["high"], p["low"], p["close"], p["volume"])
+    torch.cuda.synchronize()
+    # warm-up NaN prefixes (pandas rolling(w) / min_periods semantics)
+    for k, w in (("ma_7", 7), ("ma_25", 25), ("ma_100", 100), ("bb_mid", 20), ("ATR", 14), ("twap", 12),
+                 ("rsi", 14), ("mfi", 14)):   # delta.where(...) turns the first NaN into 0
+        col = out[k]
+        assert torch.isnan(col[:, : w - 1]).all(), k
+        assert not torch.isnan(col[:, w:]).any(), k
+    for k in ("macd", "macd_signal", "ema20", "ema50"):
+        assert not torch.isnan(out[k]).any(), k
+    for k in ("rsi", "mfi"):
+        v = out[k][:, 20:]
+        assert bool(((v >= 0) & (v <= 100)).all()), k
+    mid2 = (out["bb_upper"] + out["bb_lower"]) / 2
+    rel = ((mid2 - out["bb_mid"]).abs() / out["bb_mid"].abs())[:, 20:]
+    assert float(rel.max()) < 1e-12
+    # a spread sample of rows against the per-symbol pandas path
+    rows = torch.linspace(0, S - 1, 6).long()
+    host = {k: v[rows].cpu().numpy() for k, v in p.items()}
+    want = ref.enrich_panel(host["open"], host["high"], host["low"], host["close"], host["volume"])
+    got = {k: v[rows].cpu().numpy() for k, v in out.items()}
+    compare(got, want, host)

@@ -67,16 +67,60 @@ __global__ __launch_bounds__(NT) void row_tiles(Args a) {
   }
 }
 
+// register prefetch two tiles ahead
+__global__ __launch_bounds__(256) void row_tiles_pf2(Args a) {
+  extern __shared__ double occupancy_limiter[];
+  if (a.S < 0) occupancy_limiter[threadIdx.x] = 0.0;
+  const long base = (long)blockIdx.x * a.ld;
+  constexpr int TILE = 256 * K;
+  dbl2 n1[NIN][2], n2[NIN][2];
+  long tb = threadIdx.x * K;
+  for (int f = 0; f < NIN; ++f) {
+    const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb);
+    n1[f][0] = p[0];
+    n1[f][1] = p[1];
+    if (tb + TILE < a.T) {
+      const dbl2* q = reinterpret_cast<const dbl2*>(a.in[f] + base + tb + TILE);
+      n2[f][0] = q[0];
+      n2[f][1] = q[1];
+    }
+  }
+  for (; tb < a.T; tb += TILE) {
+    dbl2 cu[NIN][2];
+    for (int f = 0; f < NIN; ++f) {
+      cu[f][0] = n1[f][0];
+      cu[f][1] = n1[f][1];
+      n1[f][0] = n2[f][0];
+      n1[f][1] = n2[f][1];
+    }
+    if (tb + 2 * TILE < a.T)
+      for (int f = 0; f < NIN; ++f) {
+        const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb + 2 * TILE);
+        n2[f][0] = p[0];
+        n2[f][1] = p[1];
+      }
+    dbl2 acc0 = {0, 0}, acc1 = {0, 0};
+    for (int f = 0; f < NIN; ++f) {
+      acc0 += cu[f][0];
+      acc1 += cu[f][1];
+    }
+    for (int o = 0; o < NOUT; ++o) {
+      dbl2* q = reinterpret_cast<dbl2*>(a.out[o] + base + tb);
+      q[0] = acc0 + (double)o;
+      q[1] = acc1;
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const long S = 12500, T = 10000;
   const int reps = 10;
   struct V { const char* name; long pad; long stagger; int swz; int nt; int pf; int lds; };
   const V vs[] = {
-      {"base", 0, 0, 0, 256, 0, 0},          {"prefetch", 0, 0, 0, 256, 1, 0},
-      {"base_3wg", 0, 0, 0, 256, 0, 52000},  {"prefetch_3wg", 0, 0, 0, 256, 1, 52000},
-      {"prefetch_4wg", 0, 0, 0, 256, 1, 39000}, {"prefetch_2wg", 0, 0, 0, 256, 1, 78000},
-      {"swizzle_pf_3wg", 0, 0, 1, 256, 1, 52000}, {"stagger+pf", 0, 65536 + 1024, 0, 256, 1, 0},
-      {"stagger+pf_3wg", 0, 65536 + 1024, 0, 256, 1, 52000}, {"prefetch_again", 0, 0, 0, 256, 1, 0},
+      {"pf1_3wg", 0, 0, 0, 256, 1, 52000},  {"pf2_2wg", 0, 0, 0, 256, 2, 78000},
+      {"pf2_3wg", 0, 0, 0, 256, 2, 52000},  {"pf1_2wg", 0, 0, 0, 256, 1, 78000},
+      {"pf1_3wg_b", 0, 0, 0, 256, 1, 52000}, {"pf2_2wg_b", 0, 0, 0, 256, 2, 78000},
+      {"pf2_3wg_b", 0, 0, 0, 256, 2, 52000}, {"pf1_4wg", 0, 0, 0, 256, 1, 39000},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -97,7 +141,8 @@ int main(int argc, char** argv) {
     a.swz = v.swz;
     for (int r = 0; r < reps + 2; ++r) {
       if (r == 2) CK(hipEventRecord(e0));
-      if (v.pf) row_tiles<256, true><<<S, 256, v.lds>>>(a);
+      if (v.pf == 2) row_tiles_pf2<<<S, 256, v.lds>>>(a);
+      else if (v.pf) row_tiles<256, true><<<S, 256, v.lds>>>(a);
       else row_tiles<256, false><<<S, 256, v.lds>>>(a);
     }
     CK(hipEventRecord(e1));
