@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--row-symbols", type=int, default=12_500)
     ap.add_argument("--row-candles", type=int, default=2_000)
     ap.add_argument("--store-ticks", type=int, default=50)
+    ap.add_argument("--live-symbols", type=int, default=1000)
     return ap.parse_args()
 
 
@@ -302,6 +303,34 @@ def bench_rows(args, dev):
     return out
 
 
+def bench_live(args, dev):
+    """Live-path strategy pipelines: S symbols x 400-bar frames per message
+    (SURVEY §3.2), eager launches vs one hipGraph replay (binquant_amd.graphs).
+    reference_cpu_ms: the reference's per-symbol pandas cost x S (SURVEY §8a,
+    measured in the build container through the real modules)."""
+    from binquant_amd import signals, strategies
+    from binquant_amd.graphs import CapturedPipeline
+
+    S, T = args.live_symbols, 400
+    p = device_panel(S, T, device=dev, seed=31)
+    ins = [p[k] for k in ("open", "high", "low", "close", "volume")]
+    pipes = {
+        "a17_activity_burst": (lambda o, h, l, c, v: strategies.activity_burst_features(o, h, l, c, v, v * c), 9.1),
+        "a18_pump_score": (lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0]), 9.8),
+        "a19_failed_spike": (lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c), 24.3),
+        "a20_top_gainer": (lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c), None),
+    }
+    out = {"workload": f"{S} symbols x {T}-bar frames (one message cohort)"}
+    for name, (fn, ref_ms) in pipes.items():
+        eager = _time_call(lambda: fn(*ins), reps=5)
+        g = CapturedPipeline(fn, *ins)
+        graph = _time_call(lambda: g(*ins), reps=5)
+        out[name] = {"eager_ms": eager, "graph_ms": graph,
+                     "reference_cpu_ms": None if ref_ms is None else ref_ms * S}
+        del g
+    return out
+
+
 def bench_store(args, dev):
     """§8f row 1: DeviceMarketStateStore at 10k symbols x 400-bar histories;
     one tick = a new closed candle per symbol (host arrays, one device update)
@@ -422,6 +451,7 @@ def main():
         result["store"] = bench_store(args, dev)
     if rank == 0 and world == 1 and not args.no_rows:
         result["rows"] = bench_rows(args, dev)
+        result["live"] = bench_live(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, T)
     else:

@@ -391,11 +391,12 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     if (!nrep) return;
     const int ring = (max_back + RP_CT - 1) / RP_CT + 1;
     const size_t lds = (size_t)ring * RP_CT * STG_PITCH * sizeof(double);
-    static bool lds_opt_in = false;   // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    if (!lds_opt_in) {
-      (void)hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      lds_opt_in = true;
-    }
+    // > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU): set once, before
+    // any graph capture can be active (first call of the process)
+    static const bool lds_opt_in =
+        hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
+        hipSuccess;
+    (void)lds_opt_in;
     hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
                        rep, ring);
     nrep = 0;

@@ -67,8 +67,8 @@ def _pct_change(x: torch.Tensor, periods: int) -> torch.Tensor:
 
 
 def _ffill(x: torch.Tensor) -> torch.Tensor:
-    if not torch.isnan(x).any():
-        return x
+    """Forward fill along T, sync-free (no data-dependent host branch, so a
+    pipeline using it can be captured in a hipGraph)."""
     T = x.shape[-1]
     idx = torch.arange(T, device=x.device).expand_as(x)
     valid = ~torch.isnan(x)
