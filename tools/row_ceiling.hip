@@ -67,47 +67,44 @@ __global__ __launch_bounds__(NT) void row_tiles(Args a) {
   }
 }
 
-// register prefetch two tiles ahead
+// register prefetch two tiles ahead: the loop is unrolled by two so the two
+// buffers alternate roles without register moves (a move would wait for the
+// load in flight)
+__device__ __forceinline__ void load_tile2(const Args& a, long base, long tb, dbl2 (&r)[NIN][2]) {
+  if (tb < a.T)
+    for (int f = 0; f < NIN; ++f) {
+      const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb);
+      r[f][0] = p[0];
+      r[f][1] = p[1];
+    }
+}
+__device__ __forceinline__ void emit_tile(const Args& a, long base, long tb, const dbl2 (&cu)[NIN][2]) {
+  dbl2 acc0 = {0, 0}, acc1 = {0, 0};
+  for (int f = 0; f < NIN; ++f) {
+    acc0 += cu[f][0];
+    acc1 += cu[f][1];
+  }
+  for (int o = 0; o < NOUT; ++o) {
+    dbl2* q = reinterpret_cast<dbl2*>(a.out[o] + base + tb);
+    q[0] = acc0 + (double)o;
+    q[1] = acc1;
+  }
+}
 __global__ __launch_bounds__(256) void row_tiles_pf2(Args a) {
   extern __shared__ double occupancy_limiter[];
   if (a.S < 0) occupancy_limiter[threadIdx.x] = 0.0;
   const long base = (long)blockIdx.x * a.ld;
   constexpr int TILE = 256 * K;
-  dbl2 n1[NIN][2], n2[NIN][2];
+  dbl2 A[NIN][2], B[NIN][2];
   long tb = threadIdx.x * K;
-  for (int f = 0; f < NIN; ++f) {
-    const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb);
-    n1[f][0] = p[0];
-    n1[f][1] = p[1];
+  load_tile2(a, base, tb, A);
+  load_tile2(a, base, tb + TILE, B);
+  for (; tb < a.T; tb += 2 * TILE) {
+    emit_tile(a, base, tb, A);
+    load_tile2(a, base, tb + 2 * TILE, A);
     if (tb + TILE < a.T) {
-      const dbl2* q = reinterpret_cast<const dbl2*>(a.in[f] + base + tb + TILE);
-      n2[f][0] = q[0];
-      n2[f][1] = q[1];
-    }
-  }
-  for (; tb < a.T; tb += TILE) {
-    dbl2 cu[NIN][2];
-    for (int f = 0; f < NIN; ++f) {
-      cu[f][0] = n1[f][0];
-      cu[f][1] = n1[f][1];
-      n1[f][0] = n2[f][0];
-      n1[f][1] = n2[f][1];
-    }
-    if (tb + 2 * TILE < a.T)
-      for (int f = 0; f < NIN; ++f) {
-        const dbl2* p = reinterpret_cast<const dbl2*>(a.in[f] + base + tb + 2 * TILE);
-        n2[f][0] = p[0];
-        n2[f][1] = p[1];
-      }
-    dbl2 acc0 = {0, 0}, acc1 = {0, 0};
-    for (int f = 0; f < NIN; ++f) {
-      acc0 += cu[f][0];
-      acc1 += cu[f][1];
-    }
-    for (int o = 0; o < NOUT; ++o) {
-      dbl2* q = reinterpret_cast<dbl2*>(a.out[o] + base + tb);
-      q[0] = acc0 + (double)o;
-      q[1] = acc1;
+      emit_tile(a, base, tb + TILE, B);
+      load_tile2(a, base, tb + 3 * TILE, B);
     }
   }
 }
