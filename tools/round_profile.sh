@@ -14,7 +14,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAILED; tail $O/bench.err; exit 1; }
 cat $O/bench.json
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-rows --ticks 500 > $O/trace_bench.json 2> $O/trace.err || { echo TRACE_FAILED; tail $O/trace.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --no-cpu-baseline --no-rows --ticks 200 --store-ticks 10 > $O/trace_bench.json 2> $O/trace.err || { echo TRACE_FAILED; tail $O/trace.err; exit 1; }
+rm -f $O/trace/run_kernel_trace.csv   # per-dispatch rows: large; the stats summary is what is kept
 cd $R
 bash tools/pmc_profile.sh gpurun_out/$TAG/pmc || exit 1
 python tools/pmc_summary.py $O/pmc enrich_kernel $O/pmc_traffic.json $TAG > /dev/null
