@@ -45,36 +45,120 @@ def _device(device):
     return torch.device("cuda")
 
 
+def _cohort_winners(keys: torch.Tensor, sc: torch.Tensor, ranks: torch.Tensor, acc: torch.Tensor, stream=None):
+    """Device segmented arg-max of (score, symbol rank, index) per cohort key
+    over the accepted entries -> (sorted unique keys, winner index or -1)."""
+    uniq, dense = torch.unique(keys, sorted=True, return_inverse=True)
+    dense32 = dense.to(torch.int32).contiguous()
+    acc8 = acc.to(torch.uint8).contiguous()
+    sc = sc.contiguous()
+    ranks = ranks.to(torch.int32).contiguous()
+    nc = uniq.numel()
+    scratch = torch.empty(2 * nc, dtype=torch.int64, device=keys.device)
+    win = torch.empty(nc, dtype=torch.int64, device=keys.device)
+    status = _lib.load().bq_cohort_select(
+        keys.numel(), ctypes.c_void_p(dense32.data_ptr()), ctypes.c_void_p(acc8.data_ptr()),
+        ctypes.c_void_p(sc.data_ptr()), ctypes.c_void_p(ranks.data_ptr()), nc, ctypes.c_void_p(scratch.data_ptr()),
+        ctypes.c_void_p(win.data_ptr()), engine._stream_handle(stream))
+    _lib.check(status, "bq_cohort_select")
+    return uniq, win
+
+
+def _accepted(keys: torch.Tensor) -> torch.Tensor:
+    """submit() accepts a candidate unless its cohort is older than the latest seen."""
+    run = torch.cummax(keys, 0).values
+    prev = torch.cat([keys[:1], run[:-1]])
+    return keys >= prev
+
+
 def select_winners(cohort_keys, scores, symbols: Sequence[str], device=None, stream=None) -> Winners:
     """Submissions in arrival order -> accepted flags and each cohort's winner."""
     dev = _device(device)
     n = len(symbols)
-    keys = torch.as_tensor(np.asarray(cohort_keys, dtype=np.int64)).to(dev)
-    sc = torch.as_tensor(np.asarray(scores, dtype=np.float64)).to(dev)
     if n == 0:
         return Winners(np.zeros(0, bool), np.zeros(0, np.int64), np.zeros(0, np.int64))
-    # a submission is accepted unless its cohort is older than the latest seen
-    run = torch.cummax(keys, 0).values
-    prev = torch.cat([keys[:1], run[:-1]])
-    acc = keys >= prev
-    uniq, dense = torch.unique(keys, sorted=True, return_inverse=True)
+    keys = torch.as_tensor(np.asarray(cohort_keys, dtype=np.int64)).to(dev)
+    sc = torch.as_tensor(np.asarray(scores, dtype=np.float64)).to(dev)
+    acc = _accepted(keys)
     # symbol strings -> ranks in Python's str order
     names = sorted(set(symbols))
     rank_of = {s: i for i, s in enumerate(names)}
     ranks = torch.tensor([rank_of[s] for s in symbols], dtype=torch.int32, device=dev)
-    dense32 = dense.to(torch.int32).contiguous()
-    acc8 = acc.to(torch.uint8).contiguous()
-    nc = uniq.numel()
-    scratch = torch.empty(2 * nc, dtype=torch.int64, device=dev)
-    win = torch.empty(nc, dtype=torch.int64, device=dev)
-    status = _lib.load().bq_cohort_select(
-        n, ctypes.c_void_p(dense32.data_ptr()), ctypes.c_void_p(acc8.data_ptr()), ctypes.c_void_p(sc.data_ptr()),
-        ctypes.c_void_p(ranks.data_ptr()), nc, ctypes.c_void_p(scratch.data_ptr()), ctypes.c_void_p(win.data_ptr()),
-        engine._stream_handle(stream))
-    _lib.check(status, "bq_cohort_select")
+    uniq, win = _cohort_winners(keys, sc, ranks, acc, stream)
     w = win.cpu().numpy()
     keep = w >= 0
     return Winners(acc.cpu().numpy(), uniq.cpu().numpy()[keep], w[keep])
+
+
+def _all_gather_rows(rows: torch.Tensor, group) -> torch.Tensor:
+    """all_gather of a variable number of int64 rows [n, k] -> [sum n, k]
+    (counts first, then one padded gather; RCCL on device tensors, gloo
+    through host memory)."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    on_host = dist.get_backend(group) == "gloo"
+    xfer = rows.cpu() if on_host else rows
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=xfer.device)
+    counts = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts)
+    pad = torch.zeros((m, rows.shape[1]), dtype=torch.int64, device=xfer.device)
+    pad[:rows.shape[0]] = xfer
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    out = torch.cat([p[:c] for p, c in zip(parts, counts)])
+    return out.to(rows.device)
+
+
+def select_winners_sharded(cohort_keys, scores, symbol_ids, seq, group=None, device=None, stream=None,
+                           cohort_winners=None) -> Winners:
+    """The portfolio decision when the symbols are sharded over ranks (SURVEY
+    §8e): each rank holds the submissions of its own symbols; ``seq`` is the
+    global arrival order and ``symbol_ids`` a global id in the symbols' str
+    order (both shared by every rank, e.g. from the shard plan). Two
+    exchanges: an all-gather of the (seq, key) pairs, from which each rank
+    derives its submissions' acceptance (the running max of the key in
+    arrival order), and an all-gather of each rank's per-cohort winners
+    (key, score bits, symbol id, seq), merged by the same device arg-max.
+    Every rank returns the same cohorts and winners (winner = global seq);
+    ``accepted`` is per local submission. Equal to ``select_winners`` over
+    the union of the submissions in seq order."""
+    import torch.distributed as dist
+
+    dev = _device(device)
+    pick = cohort_winners or _cohort_winners
+    keys = torch.as_tensor(np.asarray(cohort_keys, dtype=np.int64)).to(dev)
+    sc = torch.as_tensor(np.asarray(scores, dtype=np.float64)).to(dev)
+    sid = torch.as_tensor(np.asarray(symbol_ids, dtype=np.int64)).to(dev)
+    sq = torch.as_tensor(np.asarray(seq, dtype=np.int64)).to(dev)
+    # (1) acceptance needs the global arrival order of the cohort keys
+    pairs = _all_gather_rows(torch.stack([sq, keys], 1), group)
+    order = torch.argsort(pairs[:, 0])
+    gk = pairs[order, 1]
+    excl = torch.cat([gk[:1], torch.cummax(gk, 0).values[:-1]])   # running max before each arrival
+    pos = torch.searchsorted(pairs[order, 0].contiguous(), sq)
+    acc = keys >= excl[pos] if keys.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
+    # (2) local winners per cohort (ties inside one symbol resolved by arrival order)
+    local_order = torch.argsort(sq)
+    k_l, s_l, i_l, q_l, a_l = keys[local_order], sc[local_order], sid[local_order], sq[local_order], acc[local_order]
+    if k_l.numel():
+        uniq, win = pick(k_l, s_l, i_l, a_l, stream)
+        ok = win >= 0
+        w = win[ok]
+        rows = torch.stack([uniq[ok], s_l[w].view(torch.int64), i_l[w], q_l[w]], 1)
+    else:
+        rows = torch.zeros((0, 4), dtype=torch.int64, device=dev)
+    # (3) merge the ranks' winners: sorted by seq so that index order is arrival order
+    allw = _all_gather_rows(rows, group)
+    allw = allw[torch.argsort(allw[:, 3])]
+    if allw.shape[0] == 0:
+        return Winners(acc.cpu().numpy(), np.zeros(0, np.int64), np.zeros(0, np.int64))
+    uniq, win = pick(allw[:, 0].contiguous(), allw[:, 1].contiguous().view(torch.float64), allw[:, 2].contiguous(),
+                     torch.ones(allw.shape[0], dtype=torch.bool, device=dev), stream)
+    ok = win >= 0
+    return Winners(acc.cpu().numpy(), uniq[ok].cpu().numpy(), allw[win[ok], 3].cpu().numpy())
 
 
 class _CohortSelector:

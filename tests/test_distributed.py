@@ -102,3 +102,78 @@ def test_shard_bounds_cover_exactly():
             assert spans[0][0] == 0 and spans[-1][1] == S
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+# ---- sharded portfolio selection (all-gather of per-cohort winners)
+
+def _np_cohort_winners(keys, sc, ranks, acc, stream=None):
+    """Stand-in for the device arg-max on CPU ranks: max (score, symbol, index)
+    per cohort over the accepted entries (what bq_cohort_select computes)."""
+    k, s, r, a = (t.numpy() for t in (keys, sc, ranks, acc))
+    uniq = np.unique(k)
+    win = np.full(len(uniq), -1, dtype=np.int64)
+    for j, key in enumerate(uniq):
+        idx = [i for i in range(len(k)) if k[i] == key and a[i]]
+        if idx:
+            win[j] = max(idx, key=lambda i: (s[i] + 0.0, r[i], i))
+    return torch.from_numpy(uniq), torch.from_numpy(win)
+
+
+def portfolio_shards(stream, world, rank, hourly):
+    names = sorted({sym for _, sym, _ in stream})
+    sid = {s: i for i, s in enumerate(names)}
+    from binquant_amd.market_regime.batch import shard_bounds
+
+    lo, hi = shard_bounds(len(names), world, rank)
+    mine = [i for i, (_, sym, _) in enumerate(stream) if lo <= sid[sym] < hi]
+    key = (lambda t: t // 3_600_000) if hourly else (lambda t: t)
+    return (mine, [key(stream[i][0]) for i in mine], [stream[i][2] for i in mine],
+            [sid[stream[i][1]] for i in mine])
+
+
+def _portfolio_worker(rank, world, port, q, device):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from binquant_amd import portfolio
+
+        runs = json.loads((G / "portfolio.json").read_text())
+        pick = _np_cohort_winners if device == "cpu" else None
+        out = []
+        for name, rr in runs.items():
+            for run in rr:
+                stream = [tuple(x) for x in run["stream"]]
+                mine, keys, scores, sids = portfolio_shards(stream, world, rank, name == "gradual")
+                w = portfolio.select_winners_sharded(keys, scores, sids, mine, device=device, cohort_winners=pick)
+                out.append((mine, w.accepted.tolist(), w.winner.tolist()))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_sharded_portfolio(world, device):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_portfolio_worker, args=(r, world, port, q, device)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    runs = json.loads((G / "portfolio.json").read_text())
+    want = [run for name in runs for run in runs[name]]
+    for j, run in enumerate(want):
+        acc = [None] * len(run["stream"])
+        for r in range(world):
+            mine, a, winners = res[r][j]
+            assert winners == run["dispatched"], (r, j)   # every rank agrees on the winners
+            for i, x in zip(mine, a):
+                acc[i] = x
+        assert acc == run["accepted"], j
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_portfolio_selection_equals_reference(world):
+    run_sharded_portfolio(world, "cpu")

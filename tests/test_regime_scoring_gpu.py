@@ -107,3 +107,12 @@ def test_portfolio_selection_matches_reference(cuda, name):
 
         acc, disp = asyncio.run(drive())
         assert acc == run["accepted"] and disp == run["dispatched"]
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_portfolio_selection_on_device(cuda, world):
+    """Symbols sharded over 2 ranks (both on this GPU, gloo for the two
+    all-gathers): per-rank device arg-max + merge == the reference's picks."""
+    from test_distributed import run_sharded_portfolio
+
+    run_sharded_portfolio(world, "cuda")
