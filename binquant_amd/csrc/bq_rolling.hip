@@ -166,12 +166,59 @@ struct Moments {
   }
 };
 
+__host__ __device__ __forceinline__ int replay_class(int mode) {
+  return mode == BQ_ROLL_EWM ? 0 : mode >= BQ_ROLL_VAR ? 2 : 1;
+}
+
+// one lane's replay state: pandas' window recurrences (Moments) or the ewm
+// recursion (adjust=False, ignore_na=False), advanced one candle per call
+struct ReplayLane {
+  Moments m;
+  double weighted, old_wt;
+  int nobs;
+  __device__ __forceinline__ void init() {
+    m.init(0.0);
+    weighted = qnan();
+    old_wt = 1.0;
+    nobs = 0;
+  }
+  // v_in = x[t - shift] (NaN before the row), v_out = x[t - shift - w]
+  __device__ __forceinline__ double step(const RollJob& A, bool EWM, bool welford, int t, double v_in, double v_out) {
+    if (EWM) {
+      const double alpha = A.alpha, om = 1.0 - alpha;
+      if (t == 0) {
+        weighted = v_in;
+        nobs = v_in == v_in;
+      } else {
+        const bool obs = v_in == v_in;
+        nobs += obs;
+        if (weighted == weighted) {
+          old_wt *= om;
+          if (obs) {
+            if (weighted != v_in) {
+              weighted = old_wt * weighted + alpha * v_in;
+              weighted /= old_wt + alpha;
+            }
+            old_wt = 1.0;
+          }
+        } else if (obs) {
+          weighted = v_in;
+        }
+      }
+      return nobs >= A.minp ? weighted : qnan();
+    }
+    if (t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
+    if (t >= A.win && t - A.shift - A.win >= 0) m.remove(v_out, welford);
+    m.add(v_in, welford);
+    return m.result(A.mode, A.minp);
+  }
+};
+
 // LDS: a ring of the last `ring` input chunks (RL = ring * RP_CT candles per
 // lane, lane-interleaved); the ring covers window + shift, so the leaving
 // value is an LDS read and every input byte crosses HBM once. Results go
 // straight from each lane to its row (consecutive steps fill a cache line
-// in L2 before it is written back), which keeps the LDS per wave small
-// enough for several waves per CU.
+// in L2 before it is written back).
 __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int ring) {
   const RollJob& A = B.j[blockIdx.y];   // wave-uniform: scalar kernarg loads
   const bool EWM = A.mode == BQ_ROLL_EWM;
@@ -191,12 +238,8 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
   int pin = wrap(-sh), pout = wrap(-sh - w);
   double ri[RP_CT];
   stage_load<RP_CT>(A.x, A.ld_in, sym0, S, 0, T, lane, ri);
-  Moments m;
-  m.init(0.0);
-  // ewm state (pandas ewm, adjust=False, ignore_na=False)
-  double weighted = qnan(), old_wt = 1.0;
-  int nobs = 0;
-  const double alpha = A.alpha, om = 1.0 - alpha;
+  ReplayLane st;
+  st.init();
   for (int t0 = 0; t0 < T; t0 += RP_CT) {
     stage_put<RP_CT>(smem + ((t0 / RP_CT) % ring) * TILE, lane, ri);
     __syncthreads();
@@ -205,36 +248,10 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
     auto step = [&](int j) {
       const int t = t0 + j;
       const double v_in = t - sh < 0 ? qnan() : smem[pin * STG_PITCH + lane];
+      const double v_out = EWM ? 0.0 : smem[pout * STG_PITCH + lane];
       pin = pin + 1 == RL ? 0 : pin + 1;
-      double res;
-      if (EWM) {
-        if (t == 0) {
-          weighted = v_in;
-          nobs = v_in == v_in;
-        } else {
-          const bool obs = v_in == v_in;
-          nobs += obs;
-          if (weighted == weighted) {
-            old_wt *= om;
-            if (obs) {
-              if (weighted != v_in) {
-                weighted = old_wt * weighted + alpha * v_in;
-                weighted /= old_wt + alpha;
-              }
-              old_wt = 1.0;
-            }
-          } else if (obs) {
-            weighted = v_in;
-          }
-        }
-        res = nobs >= A.minp ? weighted : qnan();
-      } else {
-        if (t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
-        if (t >= w && t - sh - w >= 0) m.remove(smem[pout * STG_PITCH + lane], welford);
-        pout = pout + 1 == RL ? 0 : pout + 1;
-        m.add(v_in, welford);
-        res = m.result(A.mode, A.minp);
-      }
+      pout = pout + 1 == RL ? 0 : pout + 1;
+      const double res = st.step(A, EWM, welford, t, v_in, v_out);
       if (live) orow[t] = res;
     };
     if (t0 + RP_CT <= T) {
@@ -247,6 +264,64 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
     }
     __syncthreads();   // the ring slot of this chunk is reused RL candles later
   }
+}
+
+// Same replay with a fixed 2-tile LDS footprint (16.9 KB per wave instead of
+// the ring's ceil((w + shift) / 16) + 1 tiles, up to 59 KB at w = 80): the
+// leaving values are staged from the input again (chunk t0 - shift - w, an
+// L2 / MALL hit: it was read w candles earlier), so up to 9 waves per CU fit
+// instead of 2-6. Costs one more read of the input (from cache).
+// CLS: 0 = ewm, 1 = Kahan sum / mean, 2 = Welford var / std — the body is
+// specialised per class (shorter dependent chain per step, and a per-class
+// launch keeps the registers to that class's state: 107 / 166 / 186 VGPRs).
+template <int CLS>
+__device__ __forceinline__ void replay_restage_body(const RollJob& A, const RollBatch& B, double* s_in,
+                                                    double* s_out) {
+  constexpr bool EWM = CLS == 0;
+  constexpr bool welford = CLS == 2;
+  const int lane = threadIdx.x;
+  const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
+  const int64_t S = B.S;
+  const int T = B.T, w = A.win, sh = A.shift;
+  const bool live = sym0 + lane < S;
+  double* __restrict__ orow = A.out + (live ? sym0 + lane : 0) * A.ld_out;
+  double ri[RP_CT], ro[RP_CT];
+  stage_load<RP_CT>(A.x, A.ld_in, sym0, S, -sh, T, lane, ri);
+  if (!EWM) stage_load<RP_CT>(A.x, A.ld_in, sym0, S, -sh - w, T, lane, ro);
+  ReplayLane st;
+  st.init();
+  for (int t0 = 0; t0 < T; t0 += RP_CT) {
+    stage_put<RP_CT>(s_in, lane, ri);
+    if (!EWM) stage_put<RP_CT>(s_out, lane, ro);
+    __syncthreads();
+    if (t0 + RP_CT < T) {   // next chunks in flight during this one's replay
+      stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT - sh, T, lane, ri);
+      if (!EWM) stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT - sh - w, T, lane, ro);
+    }
+    auto step = [&](int j) {
+      const int t = t0 + j;
+      const double v_in = s_in[j * STG_PITCH + lane];
+      const double v_out = EWM ? 0.0 : s_out[j * STG_PITCH + lane];
+      const double res = st.step(A, EWM, welford, t, v_in, v_out);
+      if (live) orow[t] = res;
+    };
+    if (t0 + RP_CT <= T) {
+#pragma unroll
+      for (int j = 0; j < RP_CT; ++j) step(j);
+    } else {
+      for (int j = 0; j < T - t0; ++j) step(j);
+    }
+    __syncthreads();   // both tiles are rewritten by the next chunk
+  }
+}
+
+
+// every job of the batch is of class CLS
+template <int CLS>
+__global__ __launch_bounds__(WAVE) void replay_restage_kernel(const RollBatch B) {
+  __shared__ double s_in[RP_CT * STG_PITCH];
+  __shared__ double s_out[RP_CT * STG_PITCH];
+  replay_restage_body<CLS>(B.j[blockIdx.y], B, s_in, s_out);
 }
 
 // ---- rank kernels (lane = symbol x segment, sorted window in registers) -----------
@@ -565,6 +640,17 @@ void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
+// which replay kernel: 0 = LDS ring over the window, 1 = re-staged leaving
+// values (fixed LDS). BQ_REPLAY_IMPL=ring|restage forces one (measurement).
+int replay_impl(int nclasses, int64_t waves) {
+  static const int forced = [] {
+    const char* e = getenv("BQ_REPLAY_IMPL");
+    return !e ? -1 : (strcmp(e, "ring") == 0 ? 0 : strcmp(e, "restage") == 0 ? 1 : -1);
+  }();
+  if (forced >= 0) return forced;
+  return nclasses > 1 && waves <= 4096 ? 0 : 1;
+}
+
 // which order-statistic kernel: 0 = lane (sorted window per lane), 1 = tile
 // (sorted union per wave). BQ_RANK_IMPL=lane|tile forces one (measurement).
 int rank_impl(int w, int64_t S, int64_t T) {
@@ -619,8 +705,34 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
         hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
         hipSuccess;
     (void)lds_opt_in;
-    hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
-                       rep, ring);
+    // few waves (live shapes) with mixed classes: per-class launches would
+    // run one after the other, each latency-bound, so the ring kernel takes
+    // the whole batch in one launch; otherwise the class-specialised
+    // re-staging kernels (measured: tools/replay_ab.py, identical outputs)
+    int ncls[3] = {0, 0, 0};
+    for (int i = 0; i < nrep; ++i) ++ncls[replay_class(rep.j[i].mode)];
+    const int nclasses = (ncls[0] > 0) + (ncls[1] > 0) + (ncls[2] > 0);
+    const int64_t waves = (S + WAVE - 1) / WAVE * nrep;
+    if (replay_impl(nclasses, waves)) {
+      RollBatch cls[3];
+      for (int c = 0; c < 3; ++c) {
+        memset(&cls[c], 0, sizeof(RollBatch));
+        cls[c].S = S;
+        cls[c].T = (int)T;
+        ncls[c] = 0;
+      }
+      for (int i = 0; i < nrep; ++i) {
+        const int c = replay_class(rep.j[i].mode);
+        cls[c].j[ncls[c]++] = rep.j[i];
+      }
+      const unsigned gx = (unsigned)((S + WAVE - 1) / WAVE);
+      if (ncls[0]) hipLaunchKernelGGL(replay_restage_kernel<0>, dim3(gx, (unsigned)ncls[0]), dim3(WAVE), 0, st, cls[0]);
+      if (ncls[1]) hipLaunchKernelGGL(replay_restage_kernel<1>, dim3(gx, (unsigned)ncls[1]), dim3(WAVE), 0, st, cls[1]);
+      if (ncls[2]) hipLaunchKernelGGL(replay_restage_kernel<2>, dim3(gx, (unsigned)ncls[2]), dim3(WAVE), 0, st, cls[2]);
+    } else {
+      hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
+                         rep, ring);
+    }
     nrep = 0;
     max_back = 0;
   };
