@@ -105,6 +105,38 @@ class BqStoreView(ctypes.Structure):
     ]
 
 
+FUSED_MAX_INS = 192
+FUSED_MAX_CONST = 32
+FUSED_MAX_IN = 16
+FUSED_MAX_OUT = 24
+FUSED_MAX_REGS = 20
+FUSED_MAX_LOADS = 16
+FUSED_F64, FUSED_U8 = 0, 1
+FUSED_OPS = {name: i for i, name in enumerate(
+    ["LD", "CONST", "INRANGE", "ADD", "SUB", "MUL", "DIV", "FMAX", "FMIN", "MAXIMUM", "MINIMUM", "GT", "GE", "LT",
+     "LE", "EQ", "NE", "AND", "OR", "NOT", "ABS", "NEG", "ISNAN", "SQRT", "LOG", "WHERE", "ST"], start=1)}
+
+
+class BqFusedOperand(ctypes.Structure):
+    """Mirror of ``bq_fused_operand``."""
+
+    _fields_ = [("ptr", ctypes.c_void_p), ("stride_s", ctypes.c_int64), ("stride_t", ctypes.c_int64),
+                ("dtype", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class BqFusedProgram(ctypes.Structure):
+    """Mirror of ``bq_fused_program``."""
+
+    _fields_ = [
+        ("n_ins", ctypes.c_int32), ("n_loads", ctypes.c_int32), ("n_regs", ctypes.c_int32),
+        ("n_in", ctypes.c_int32), ("n_out", ctypes.c_int32), ("n_const", ctypes.c_int32),
+        ("ins", ctypes.c_uint64 * FUSED_MAX_INS),
+        ("consts", ctypes.c_double * FUSED_MAX_CONST),
+        ("inp", BqFusedOperand * FUSED_MAX_IN),
+        ("out", BqFusedOperand * FUSED_MAX_OUT),
+    ]
+
+
 class BqRollJob(ctypes.Structure):
     """Mirror of ``bq_roll_job`` (include/binquant_amd.h)."""
 
@@ -173,6 +205,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
     "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
+    "bq_fused_eval": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), _I64, _I64, _P]),
     "bq_micro_regime": (ctypes.c_int, [_I64] + [_P] * 13 + [_P]),
     "bq_context_score": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.POINTER(BqContextScalars),
                                         ctypes.POINTER(BqScorerWeights), _P, _I64, _P]),

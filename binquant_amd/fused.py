@@ -1,0 +1,482 @@
+"""Fused element-wise stages of the strategy pipelines (bq_fused_eval).
+
+The strategies' element-wise glue — ratios, clips, flags, shifted differences,
+where-selections between rolling series (activity_burst_pump.py:64-152,
+liquidation_sweep_pump.py:205-269, failed_spike_fade.py:260-493, the a20
+helpers) — is written with ``Ex`` values that record the operations instead of
+running them. ``run`` turns the requested outputs into one straight-line
+program per stage (common subexpressions shared, registers allocated by
+liveness, the loads issued first) and evaluates it in ONE launch of
+bq_fused_eval over the [S, T] panel. The kernel applies the same IEEE fp64
+operations in the same order as the torch expressions they replace, so the
+outputs are bit-identical; only the intermediates no longer travel through HBM.
+
+    from binquant_amd import fused as F
+    c, o = F.inp(close), F.inp(open_)
+    res = F.run({"body": (c - o).abs(), "bull": c > o, "jump": c / F.shift(c, 1) - 1})
+
+A shift of a computed value is evaluated by shifting its leaves (every
+operation is element-wise, so f(x)[t - n] = f(x[t - n])), masked with pandas'
+fill (NaN, or False for booleans) where t - n falls outside the row.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import struct
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib, engine
+
+_OPS = _lib.FUSED_OPS
+NAN = float("nan")
+
+
+class _Node:
+    __slots__ = ("op", "args", "tensor", "shift", "value", "key")
+
+    def __init__(self, op, args=(), tensor=None, shift=0, value=None):
+        self.op, self.args, self.tensor, self.shift, self.value = op, tuple(args), tensor, shift, value
+        if op == "LD":
+            self.key = ("LD", _operand_key(tensor), shift, _bits(value))
+        elif op == "CONST":
+            self.key = ("CONST", _bits(value))
+        elif op == "INRANGE":
+            self.key = ("INRANGE", shift)
+        else:
+            self.key = None   # inner nodes are deduplicated by their canonical arguments
+
+
+def _bits(v):
+    return None if v is None else struct.pack("<d", float(v))
+
+
+def _operand_key(t: torch.Tensor):
+    return (t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype)
+
+
+class Ex:
+    """A lazily evaluated element of an [S, T] panel: kind 'f' (fp64) or 'b' (bool)."""
+
+    __slots__ = ("node", "kind")
+    __hash__ = object.__hash__
+
+    def __init__(self, node: _Node, kind: str):
+        self.node, self.kind = node, kind
+
+    # ---- arithmetic (fp64) ----
+    def _bin(self, op, other, kind="f", rev=False):
+        o = _as_ex(other)
+        a, b = (o, self) if rev else (self, o)
+        return Ex(_Node(op, (a.node, b.node)), kind)
+
+    def __add__(self, o): return self._bin("ADD", o)
+    def __radd__(self, o): return self._bin("ADD", o, rev=True)
+    def __sub__(self, o): return self._bin("SUB", o)
+    def __rsub__(self, o): return self._bin("SUB", o, rev=True)
+    def __mul__(self, o): return self._bin("MUL", o)
+    def __rmul__(self, o): return self._bin("MUL", o, rev=True)
+    def __truediv__(self, o): return self._bin("DIV", o)
+    def __rtruediv__(self, o): return self._bin("DIV", o, rev=True)
+    def __neg__(self): return Ex(_Node("NEG", (self.node,)), "f")
+    def __abs__(self): return self.abs()
+    def abs(self): return Ex(_Node("ABS", (self.node,)), "f")
+
+    # ---- comparisons (NaN compares false) ----
+    def __gt__(self, o): return self._bin("GT", o, "b")
+    def __ge__(self, o): return self._bin("GE", o, "b")
+    def __lt__(self, o): return self._bin("LT", o, "b")
+    def __le__(self, o): return self._bin("LE", o, "b")
+    def __eq__(self, o): return self._bin("EQ", o, "b")  # type: ignore[override]
+    def __ne__(self, o): return self._bin("NE", o, "b")  # type: ignore[override]
+
+    # ---- booleans ----
+    def __and__(self, o): return self._bin("AND", o, "b")
+    def __rand__(self, o): return self._bin("AND", o, "b", rev=True)
+    def __or__(self, o): return self._bin("OR", o, "b")
+    def __ror__(self, o): return self._bin("OR", o, "b", rev=True)
+    def __invert__(self): return Ex(_Node("NOT", (self.node,)), "b")
+
+    def float(self) -> "Ex":
+        """bool -> 0.0 / 1.0 (``.astype(float)`` / ``.to(torch.float64)``)."""
+        return Ex(self.node, "f")
+
+    def bool(self) -> "Ex":
+        return Ex(_Node("NE", (self.node, _const(0.0).node)), "b")
+
+    def __bool__(self):
+        raise TypeError("an Ex has no truth value (use & | ~ and where())")
+
+
+def _const(v) -> Ex:
+    return Ex(_Node("CONST", value=float(v)), "b" if isinstance(v, bool) else "f")
+
+
+def _as_ex(x) -> Ex:
+    if isinstance(x, Ex):
+        return x
+    if isinstance(x, torch.Tensor):
+        return inp(x)
+    if isinstance(x, (bool, int, float)):
+        return _const(x)
+    raise TypeError(f"cannot use {type(x).__name__} in a fused expression")
+
+
+def inp(t: torch.Tensor) -> Ex:
+    """A materialised operand: [S, T] (or [S, 1] per symbol, [T] / [1, T] one
+    series for every symbol), fp64 or bool, any strides."""
+    if t.dtype not in (torch.float64, torch.bool):
+        raise ValueError(f"fused operands are float64 or bool, got {t.dtype}")
+    kind = "b" if t.dtype == torch.bool else "f"
+    return Ex(_Node("LD", tensor=t, shift=0, value=0.0 if kind == "b" else NAN), kind)
+
+
+def const(v) -> Ex:
+    return _const(v)
+
+
+def where(cond, a, b) -> Ex:
+    c, x, y = _as_ex(cond), _as_ex(a), _as_ex(b)
+    kind = "b" if x.kind == "b" and y.kind == "b" else "f"
+    return Ex(_Node("WHERE", (c.node, x.node, y.node)), kind)
+
+
+def fmax(a, b) -> Ex:
+    """torch.fmax / DataFrame.max(axis=1): NaN is skipped."""
+    return _as_ex(a)._bin("FMAX", b)
+
+
+def fmin(a, b) -> Ex:
+    return _as_ex(a)._bin("FMIN", b)
+
+
+def maximum(a, b) -> Ex:
+    """torch.maximum: NaN propagates."""
+    return _as_ex(a)._bin("MAXIMUM", b)
+
+
+def minimum(a, b) -> Ex:
+    return _as_ex(a)._bin("MINIMUM", b)
+
+
+def isnan(x) -> Ex:
+    return Ex(_Node("ISNAN", (_as_ex(x).node,)), "b")
+
+
+def sqrt(x) -> Ex:
+    return Ex(_Node("SQRT", (_as_ex(x).node,)), "f")
+
+
+def log(x) -> Ex:
+    return Ex(_Node("LOG", (_as_ex(x).node,)), "f")
+
+
+def _at(n: _Node, k: int, memo: dict) -> _Node:
+    """n evaluated at t - k (every operation is element-wise)."""
+    key = (id(n), k)
+    hit = memo.get(key)
+    if hit is not None:
+        return hit
+    if n.op == "LD":
+        r = _Node("LD", tensor=n.tensor, shift=n.shift + k, value=n.value)
+    elif n.op == "CONST":
+        r = n
+    elif n.op == "INRANGE":
+        r = _Node("INRANGE", shift=n.shift + k)
+    else:
+        r = _Node(n.op, tuple(_at(a, k, memo) for a in n.args))
+    memo[key] = r
+    return r
+
+
+def shift(x, n: int) -> Ex:
+    """pandas Series.shift(n) along T: NaN (False for booleans) where t - n is
+    outside the row."""
+    e = _as_ex(x)
+    if n == 0:
+        return e
+    fill = 0.0 if e.kind == "b" else NAN
+    if e.node.op == "LD":
+        return Ex(_Node("LD", tensor=e.node.tensor, shift=e.node.shift + n, value=fill), e.kind)
+    moved = _at(e.node, n, {})
+    return Ex(_Node("WHERE", (_Node("INRANGE", shift=n), moved, _const(fill).node)), e.kind)
+
+
+def diff(x, n: int = 1) -> Ex:
+    """Series.diff(n)."""
+    e = _as_ex(x)
+    return e - shift(e, n)
+
+
+def clip_lower(x, lo: float) -> Ex:
+    """Series.clip(lower=lo): NaN stays NaN."""
+    e = _as_ex(x)
+    return where(e < lo, lo, e)
+
+
+def replace0(x) -> Ex:
+    """Series.replace(0, nan)."""
+    e = _as_ex(x)
+    return where(e == 0, NAN, e)
+
+
+def fillna(x, v: float) -> Ex:
+    e = _as_ex(x)
+    return where(isnan(e), v, e)
+
+
+# ---- program building ------------------------------------------------------------------
+
+
+@dataclass
+class Program:
+    """One bq_fused_eval launch: instructions, constants, operands, outputs."""
+
+    ins: list[int] = field(default_factory=list)
+    n_loads: int = 0
+    n_regs: int = 0
+    consts: list[float] = field(default_factory=list)
+    inputs: list[torch.Tensor] = field(default_factory=list)
+    outputs: list[tuple[str, str]] = field(default_factory=list)   # (name, kind)
+
+
+class ProgramTooLarge(Exception):
+    pass
+
+
+def _enc(op: str, d=0, a=0, b=0, c=0, imm=0) -> int:
+    if not -(1 << 23) <= imm < (1 << 23):
+        raise ProgramTooLarge("immediate out of range")
+    return (_OPS[op] | d << 8 | a << 16 | b << 24 | c << 32 | (imm & 0xFFFFFF) << 40)
+
+
+def _canon(roots: list[_Node]) -> tuple[list[_Node], dict]:
+    """Structural CSE + topological order (post-order DFS in output order)."""
+    table: dict = {}
+    order: list[_Node] = []
+    canon: dict[int, _Node] = {}
+
+    def visit(n: _Node) -> _Node:
+        c = canon.get(id(n))
+        if c is not None:
+            return c
+        args = tuple(visit(a) for a in n.args)
+        key = n.key if not args else (n.op,) + tuple(id(a) for a in args)
+        hit = table.get(key)
+        if hit is None:
+            hit = n if not args else _Node(n.op, args)
+            if n.op in ("LD", "CONST", "INRANGE"):
+                hit.tensor, hit.shift, hit.value = n.tensor, n.shift, n.value
+            table[key] = hit
+            order.append(hit)
+        canon[id(n)] = hit
+        return hit
+
+    mapped = [visit(r) for r in roots]
+    return order, {id(r): m for r, m in zip(roots, mapped)}
+
+
+def build(outputs: list[tuple[str, Ex]], block_loads: int | None = None) -> Program:
+    """Compile named outputs into one Program (raises ProgramTooLarge)."""
+    roots = [e.node for _, e in outputs]
+    order, mapped = _canon(roots)
+    P = Program()
+    consts: dict = {}
+    inputs: dict = {}
+
+    def const_idx(v: float) -> int:
+        k = _bits(v)
+        if k not in consts:
+            if len(consts) == _lib.FUSED_MAX_CONST:
+                raise ProgramTooLarge("constants")
+            consts[k] = len(consts)
+            P.consts.append(float(v))
+        return consts[k]
+
+    def input_idx(t: torch.Tensor) -> int:
+        k = _operand_key(t)
+        if k not in inputs:
+            if len(inputs) == _lib.FUSED_MAX_IN:
+                raise ProgramTooLarge("operands")
+            inputs[k] = len(inputs)
+            P.inputs.append(t)
+        return inputs[k]
+
+    # instruction sequence: the load block, then the other nodes in order;
+    # each output is stored as soon as it is computed
+    out_at: dict[int, list[int]] = {}
+    for j, (name, e) in enumerate(outputs):
+        out_at.setdefault(id(mapped[id(e.node)]), []).append(j)
+    if len(outputs) > _lib.FUSED_MAX_OUT:
+        raise ProgramTooLarge("outputs")
+    loads = [n for n in order if n.op == "LD"]
+    nblock = min(len(loads), _lib.FUSED_MAX_LOADS if block_loads is None else block_loads)
+    in_block = {id(n) for n in loads[:nblock]}
+    # constants are operands of the instructions that use them (no register),
+    # unless a constant is itself an output
+    seq = loads[:nblock] + [n for n in order if id(n) not in in_block and (n.op != "CONST" or id(n) in out_at)]
+    last_use: dict[int, int] = {}
+    for i, n in enumerate(seq):
+        for a in n.args:
+            if a.op != "CONST":
+                last_use[id(a)] = i
+    # linear scan; an argument dying at an instruction lends its register to
+    # the result (the kernel reads the operands before it writes)
+    free = list(range(_lib.FUSED_MAX_REGS - 1, -1, -1))
+    reg: dict[int, int] = {}
+    used = 0
+    for i, n in enumerate(seq):
+        for a in {id(x) for x in n.args if x.op != "CONST"}:
+            if last_use[a] == i:
+                free.append(reg[a])
+        if not free:
+            raise ProgramTooLarge("registers")
+        r = free.pop()
+        reg[id(n)] = r
+        used = max(used, r + 1)
+        if n.op == "LD":
+            P.ins.append(_enc("LD", d=r, b=input_idx(n.tensor), c=const_idx(n.value), imm=n.shift))
+        elif n.op == "CONST":
+            P.ins.append(_enc("CONST", d=r, imm=const_idx(n.value)))
+        elif n.op == "INRANGE":
+            P.ins.append(_enc("INRANGE", d=r, imm=n.shift))
+        else:
+            ar, flags = [0, 0, 0], 0
+            for k, a in enumerate(n.args):
+                if a.op == "CONST":
+                    ar[k] = const_idx(a.value)
+                    flags |= 1 << k
+                else:
+                    ar[k] = reg[id(a)]
+            P.ins.append(_enc(n.op, d=r, a=ar[0], b=ar[1], c=ar[2], imm=flags))
+        for j in out_at.get(id(n), ()):
+            name, e = outputs[j]
+            P.ins.append(_enc("ST", a=r, imm=len(P.outputs)))
+            P.outputs.append((name, e.kind))
+        if id(n) not in last_use and i >= nblock:
+            free.append(r)   # stored (or unused): no later reader
+        if len(P.ins) > _lib.FUSED_MAX_INS:
+            raise ProgramTooLarge("instructions")
+    P.n_loads = nblock
+    P.n_regs = max(used, 1)
+    return P
+
+
+def _plan(outputs: list[tuple[str, Ex]]) -> list[Program]:
+    """Programs for the outputs: one if it fits, else fewer block loads, else
+    the outputs split in halves (shared subexpressions are recomputed)."""
+    for nb in (None, 8, 4, 0):
+        try:
+            return [build(outputs, nb)]
+        except ProgramTooLarge:
+            continue
+    if len(outputs) == 1:
+        raise ProgramTooLarge("one output does not fit a program")
+    h = len(outputs) // 2
+    return _plan(outputs[:h]) + _plan(outputs[h:])
+
+
+def _operand(t: torch.Tensor, S: int, T: int, out: bool = False) -> _lib.BqFusedOperand:
+    dt = _lib.FUSED_U8 if t.dtype == torch.bool else _lib.FUSED_F64
+    if t.dim() == 1:
+        if t.shape[0] != T:
+            raise ValueError(f"a 1-D fused operand must have T={T} values, got {t.shape[0]}")
+        ss, st = 0, t.stride(0)
+    elif t.dim() == 2:
+        if t.shape[0] not in (1, S) or t.shape[1] not in (1, T):
+            raise ValueError(f"fused operand {tuple(t.shape)} does not broadcast to [{S}, {T}]")
+        ss = t.stride(0) if t.shape[0] == S else 0
+        st = t.stride(1) if t.shape[1] == T else 0
+    else:
+        raise ValueError("fused operands are 1-D or 2-D")
+    return _lib.BqFusedOperand(ctypes.c_void_p(t.data_ptr()), ss, st, dt, 0)
+
+
+def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | None = None,
+        device=None, stream=None) -> dict[str, torch.Tensor]:
+    """Evaluate the named expressions over the [S, T] panel (S, T and the
+    device taken from the operands when omitted). Outputs that are a plain
+    [S, T] operand are returned as that tensor (no copy)."""
+    res: dict[str, torch.Tensor] = {}
+    todo: list[tuple[str, Ex]] = []
+    shapes = []
+    for name, e in outputs.items():
+        if isinstance(e, torch.Tensor):
+            res[name] = e
+            continue
+        if not isinstance(e, Ex):
+            e = _as_ex(e)
+        n = e.node
+        if n.op == "LD" and n.shift == 0 and n.tensor.dim() == 2 and (e.kind == "b") == (n.tensor.dtype == torch.bool):
+            res[name] = n.tensor   # identity (shape checked below with the others)
+        todo.append((name, e))
+        _collect_shapes(n, shapes, set())
+    if S is None or T is None:
+        full = [s for s in shapes if len(s) == 2 and s[0] > 1 and s[1] > 1]
+        if not full:
+            raise ValueError("cannot infer [S, T]: pass S and T")
+        S, T = full[0]
+    todo = [(k, e) for k, e in todo if not (k in res and tuple(res[k].shape) == (S, T))]
+    for k, _ in todo:
+        res.pop(k, None)
+    if not todo:
+        return res
+    dev = device
+    if dev is None:
+        for name, e in todo:
+            t = _first_tensor(e.node)
+            if t is not None:
+                dev = t.device
+                break
+    if dev is None:
+        dev = torch.device("cuda")
+    if torch.device(dev).type != "cuda":
+        raise RuntimeError("fused evaluation needs a HIP device (no CPU fallback)")
+    lib = _lib.load()
+    for P in _plan(todo):
+        outs = []
+        for name, kind in P.outputs:
+            t = torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64, device=dev)
+            res[name] = t
+            outs.append(t)
+        prog = _lib.BqFusedProgram()
+        prog.n_ins, prog.n_loads, prog.n_regs = len(P.ins), P.n_loads, P.n_regs
+        prog.n_in, prog.n_out, prog.n_const = len(P.inputs), len(outs), len(P.consts)
+        for i, w in enumerate(P.ins):
+            prog.ins[i] = w
+        for i, v in enumerate(P.consts):
+            prog.consts[i] = v
+        for i, t in enumerate(P.inputs):
+            if t.device != torch.device(dev) and not (t.is_cuda and torch.device(dev).type == "cuda"):
+                raise ValueError("fused operands must be on the evaluation device")
+            prog.inp[i] = _operand(t, S, T)
+        for i, t in enumerate(outs):
+            prog.out[i] = _operand(t, S, T, out=True)
+        _lib.check(lib.bq_fused_eval(ctypes.byref(prog), S, T, engine._stream_handle(stream)), "bq_fused_eval")
+        # keep the operands alive until the launch is ordered on the stream
+        del prog
+    return {k: res[k] for k in outputs}
+
+
+def _collect_shapes(n: _Node, acc: list, seen: set):
+    if id(n) in seen:
+        return
+    seen.add(id(n))
+    if n.op == "LD":
+        t = n.tensor
+        acc.append(tuple(t.shape) if t.dim() == 2 else (1, t.shape[0]))
+    for a in n.args:
+        _collect_shapes(a, acc, seen)
+
+
+def _first_tensor(n: _Node):
+    if n.op == "LD":
+        return n.tensor
+    for a in n.args:
+        t = _first_tensor(a)
+        if t is not None:
+            return t
+    return None
+

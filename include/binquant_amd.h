@@ -447,6 +447,71 @@ int bq_parse_kline_events(const char* buf, int64_t len, int64_t max_rows, char* 
                           int64_t* open_time, int64_t* close_time, double* const* ohlcv, uint8_t* closed,
                           int64_t* n_rows, int64_t* n_bad);
 
+/* ---- fused element-wise programs ---------------------------------------------- */
+/*
+ * The element-wise glue of the strategy pipelines (SURVEY §8a a17-a20:
+ * ratios, clips, flags, shifted differences, where-selections between the
+ * rolling series — e.g. activity_burst_pump.py:64-133, liquidation_sweep_pump.py:
+ * 218-269, failed_spike_fade.py:260-493) evaluated as ONE launch per stage: a
+ * straight-line program run per element (s, t) of an [S, T] panel, values in
+ * fp64 with IEEE operations in the order the program lists them (the
+ * reference's pandas operation order), so results equal the unfused
+ * arithmetic bit for bit. Intermediates live in LDS registers, never in HBM.
+ *
+ * Instruction (uint64): op | dst << 8 | a << 16 | b << 24 | c << 32 | imm << 40
+ * (imm: signed 24-bit). The first n_loads instructions are BQ_F_LD, issued
+ * together before the rest runs.
+ *   LD      dst <- in[b] at t - imm (consts[c] when t - imm is outside [0, T))
+ *   CONST   dst <- consts[imm];   INRANGE dst <- 0 <= t - imm < T
+ *   binary  dst <- a (op) b;      unary dst <- (op) a
+ *   WHERE   dst <- a != 0 ? b : c
+ *   (operand k of these ops is consts[k-th index] instead of a register
+ *   when bit k of imm is set)
+ *   ST      out[imm] <- a (BQ_F_U8 outputs store a != 0)
+ * Comparisons give 1.0 / 0.0 (NaN compares false); AND / OR / NOT treat
+ * non-zero as true; FMAX / FMIN skip NaN (torch.fmax), MAXIMUM / MINIMUM
+ * propagate it (torch.maximum).
+ * Operands: element (s, t) at ptr + s * stride_s + t * stride_t elements
+ * (stride_t 0: a per-symbol value; stride_s 0: one series for all symbols).
+ */
+#define BQ_FUSED_MAX_INS 192
+#define BQ_FUSED_MAX_CONST 32
+#define BQ_FUSED_MAX_IN 16
+#define BQ_FUSED_MAX_OUT 24
+#define BQ_FUSED_MAX_REGS 20
+#define BQ_FUSED_MAX_LOADS 16
+
+enum bq_fused_dtype { BQ_F_F64 = 0, BQ_F_U8 = 1 };
+
+enum bq_fused_op {
+  BQ_F_LD = 1, BQ_F_CONST = 2, BQ_F_INRANGE = 3,
+  BQ_F_ADD = 4, BQ_F_SUB = 5, BQ_F_MUL = 6, BQ_F_DIV = 7,
+  BQ_F_FMAX = 8, BQ_F_FMIN = 9, BQ_F_MAXIMUM = 10, BQ_F_MINIMUM = 11,
+  BQ_F_GT = 12, BQ_F_GE = 13, BQ_F_LT = 14, BQ_F_LE = 15, BQ_F_EQ = 16, BQ_F_NE = 17,
+  BQ_F_AND = 18, BQ_F_OR = 19, BQ_F_NOT = 20,
+  BQ_F_ABS = 21, BQ_F_NEG = 22, BQ_F_ISNAN = 23, BQ_F_SQRT = 24, BQ_F_LOG = 25,
+  BQ_F_WHERE = 26, BQ_F_ST = 27
+};
+
+typedef struct {
+  const void* ptr;
+  int64_t stride_s, stride_t;   /* in elements */
+  int32_t dtype;                /* bq_fused_dtype */
+  int32_t reserved;
+} bq_fused_operand;
+
+typedef struct {
+  int32_t n_ins, n_loads, n_regs, n_in, n_out, n_const;
+  uint64_t ins[BQ_FUSED_MAX_INS];
+  double consts[BQ_FUSED_MAX_CONST];
+  bq_fused_operand in[BQ_FUSED_MAX_IN];
+  bq_fused_operand out[BQ_FUSED_MAX_OUT];
+} bq_fused_program;
+
+/* Validates the program (opcodes, register / operand / constant indices,
+ * loads first) and runs it over the [S, T] panel. Device operand pointers. */
+int bq_fused_eval(const bq_fused_program* prog, int64_t S, int64_t T, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
