@@ -67,6 +67,7 @@ AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7}
 ROLL_EWM = 8
+ROLL_FFILL = 9
 MAX_ROLL_JOBS = 16
 
 

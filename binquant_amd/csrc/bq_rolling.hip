@@ -167,7 +167,7 @@ struct Moments {
 };
 
 __host__ __device__ __forceinline__ int replay_class(int mode) {
-  return mode == BQ_ROLL_EWM ? 0 : mode >= BQ_ROLL_VAR ? 2 : 1;
+  return mode == BQ_ROLL_FFILL ? 3 : mode == BQ_ROLL_EWM ? 0 : mode >= BQ_ROLL_VAR ? 2 : 1;
 }
 
 // one lane's replay state: pandas' window recurrences (Moments) or the ewm
@@ -183,7 +183,12 @@ struct ReplayLane {
     nobs = 0;
   }
   // v_in = x[t - shift] (NaN before the row), v_out = x[t - shift - w]
-  __device__ __forceinline__ double step(const RollJob& A, bool EWM, bool welford, int t, double v_in, double v_out) {
+  __device__ __forceinline__ double step(const RollJob& A, bool EWM, bool welford, int t, double v_in, double v_out,
+                                         bool FFILL = false) {
+    if (FFILL) {   // last observation carried forward (weighted holds it)
+      if (v_in == v_in) weighted = v_in;
+      return weighted;
+    }
     if (EWM) {
       const double alpha = A.alpha, om = 1.0 - alpha;
       if (t == 0) {
@@ -221,7 +226,8 @@ struct ReplayLane {
 // in L2 before it is written back).
 __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int ring) {
   const RollJob& A = B.j[blockIdx.y];   // wave-uniform: scalar kernarg loads
-  const bool EWM = A.mode == BQ_ROLL_EWM;
+  const bool FFILL = A.mode == BQ_ROLL_FFILL;
+  const bool EWM = A.mode == BQ_ROLL_EWM || FFILL;   // no leaving value
   extern __shared__ double smem[];
   constexpr int TILE = RP_CT * STG_PITCH;
   const int RL = ring * RP_CT;
@@ -251,7 +257,7 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
       const double v_out = EWM ? 0.0 : smem[pout * STG_PITCH + lane];
       pin = pin + 1 == RL ? 0 : pin + 1;
       pout = pout + 1 == RL ? 0 : pout + 1;
-      const double res = st.step(A, EWM, welford, t, v_in, v_out);
+      const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL);
       if (live) orow[t] = res;
     };
     if (t0 + RP_CT <= T) {
@@ -277,7 +283,8 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
 template <int CLS>
 __device__ __forceinline__ void replay_restage_body(const RollJob& A, const RollBatch& B, double* s_in,
                                                     double* s_out) {
-  constexpr bool EWM = CLS == 0;
+  constexpr bool FFILL = CLS == 3;
+  constexpr bool EWM = CLS == 0 || FFILL;   // no leaving value
   constexpr bool welford = CLS == 2;
   const int lane = threadIdx.x;
   const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
@@ -302,7 +309,7 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
       const int t = t0 + j;
       const double v_in = s_in[j * STG_PITCH + lane];
       const double v_out = EWM ? 0.0 : s_out[j * STG_PITCH + lane];
-      const double res = st.step(A, EWM, welford, t, v_in, v_out);
+      const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL);
       if (live) orow[t] = res;
     };
     if (t0 + RP_CT <= T) {
@@ -619,6 +626,7 @@ namespace {
 bool job_ok(const bq_roll_job& j, int64_t T) {
   if (!j.x || !j.out || j.ld_in < T || j.ld_out < T || j.min_periods < 0) return false;
   if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
+  if (j.mode == BQ_ROLL_FFILL) return j.shift == 0;
   return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
          j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0 && j.q >= 0.0 && j.q <= 1.0;
 }
@@ -712,12 +720,12 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     // run one after the other, each latency-bound, so the ring kernel takes
     // the whole batch in one launch; otherwise the class-specialised
     // re-staging kernels (measured: tools/replay_ab.py, identical outputs)
-    int ncls[3] = {0, 0, 0};
+    int ncls[4] = {0, 0, 0, 0};
     for (int i = 0; i < nrep; ++i) ++ncls[replay_class(rep.j[i].mode)];
-    const int nclasses = (ncls[0] > 0) + (ncls[1] > 0) + (ncls[2] > 0);
+    const int nclasses = (ncls[0] > 0) + (ncls[1] > 0) + (ncls[2] > 0) + (ncls[3] > 0);
     if (replay_impl(nclasses, (S + WAVE - 1) / WAVE)) {
-      RollBatch cls[3];
-      for (int c = 0; c < 3; ++c) {
+      RollBatch cls[4];
+      for (int c = 0; c < 4; ++c) {
         memset(&cls[c], 0, sizeof(RollBatch));
         cls[c].S = S;
         cls[c].T = (int)T;
@@ -731,6 +739,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       if (ncls[0]) hipLaunchKernelGGL(replay_restage_kernel<0>, dim3(gx, (unsigned)ncls[0]), dim3(WAVE), 0, st, cls[0]);
       if (ncls[1]) hipLaunchKernelGGL(replay_restage_kernel<1>, dim3(gx, (unsigned)ncls[1]), dim3(WAVE), 0, st, cls[1]);
       if (ncls[2]) hipLaunchKernelGGL(replay_restage_kernel<2>, dim3(gx, (unsigned)ncls[2]), dim3(WAVE), 0, st, cls[2]);
+      if (ncls[3]) hipLaunchKernelGGL(replay_restage_kernel<3>, dim3(gx, (unsigned)ncls[3]), dim3(WAVE), 0, st, cls[3]);
     } else {
       hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
                          rep, ring);
@@ -779,7 +788,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     J.q = in.q;
     J.alpha = in.alpha;
     if (in.mode >= BQ_ROLL_MEAN) {   // moments / ewm: exact replay
-      const int back = in.mode == BQ_ROLL_EWM ? 0 : in.window + in.shift;
+      const int back = (in.mode == BQ_ROLL_EWM || in.mode == BQ_ROLL_FFILL) ? 0 : in.window + in.shift;
       max_back = back > max_back ? back : max_back;
       rep.j[nrep++] = J;
       if (nrep == RW_MAXJOBS) flush_rep();

@@ -372,6 +372,13 @@ class Ewm:
     min_periods: int = 0
 
 
+@dataclass
+class Ffill:
+    """x.ffill() along T (leading NaNs stay) as one series of a batch."""
+
+    x: torch.Tensor
+
+
 def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
     """Independent Roll / Ewm series over one [S, T] shape in as few launches
     as the kernel families allow (bq_rolling_batch): the lane-per-symbol
@@ -388,7 +395,9 @@ def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.
         out = torch.empty((S, T), dtype=torch.float64, device=x.device)
         j = _lib.BqRollJob()
         j.x, j.out, j.ld_in, j.ld_out = x.data_ptr(), out.data_ptr(), _row_stride(x), T
-        if isinstance(sp, Ewm):
+        if isinstance(sp, Ffill):
+            j.mode = _lib.ROLL_FFILL
+        elif isinstance(sp, Ewm):
             if (sp.alpha is None) == (sp.span is None):
                 raise ValueError("give exactly one of alpha / span")
             com = (float(sp.span) - 1.0) / 2.0 if sp.span is not None else 1.0 / float(sp.alpha) - 1.0

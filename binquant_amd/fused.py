@@ -414,10 +414,10 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
         todo.append((name, e))
         _collect_shapes(n, shapes, set())
     if S is None or T is None:
-        full = [s for s in shapes if len(s) == 2 and s[0] > 1 and s[1] > 1]
-        if not full:
-            raise ValueError("cannot infer [S, T]: pass S and T")
-        S, T = full[0]
+        if not shapes:
+            raise ValueError("cannot infer [S, T] from constants: pass S and T")
+        S = max(sh[0] for sh in shapes) if S is None else S   # broadcast shape of the operands
+        T = max(sh[1] for sh in shapes) if T is None else T
     todo = [(k, e) for k, e in todo if not (k in res and tuple(res[k].shape) == (S, T))]
     for k, _ in todo:
         res.pop(k, None)

@@ -18,8 +18,9 @@ prefix frame df.iloc[:t + 1]:
                      (strategies/top_gainer_early_momentum.py:92-160)
 * mean_reversion_features  the entry inputs of MeanReversionFade (:240-255)
 
-Everything runs through the bq_rolling / bq_ewm kernels plus device tensor
-glue in the reference's operation order; there is no CPU path.
+Everything runs through the bq_rolling / bq_ewm kernels plus fused
+element-wise programs (binquant_amd.fused) in the reference's operation order;
+there is no CPU path.
 """
 
 from __future__ import annotations
@@ -27,7 +28,7 @@ from __future__ import annotations
 import torch
 
 from . import engine
-from .strategies import _clip_lower, _diff, _shift
+from . import fused as F
 
 NAN = float("nan")
 
@@ -45,51 +46,66 @@ def ema(close: torch.Tensor, span: int, min_periods: int = 0) -> torch.Tensor:
     return engine.ewm(close, span=span, min_periods=min_periods)
 
 
+def _rsi_ex(close: torch.Tensor, window: int) -> F.Ex:
+    C = F.inp(close)
+    delta = F.diff(C, 1)
+    g = F.run({"g": F.clip_lower(delta, 0.0), "l": -F.where(delta > 0, 0.0, delta)})   # -delta.clip(upper=0)
+    ag, al = engine.rolling_many(engine.Ewm(g["g"], alpha=1 / window, min_periods=window),
+                                 engine.Ewm(g["l"], alpha=1 / window, min_periods=window))
+    AG = F.inp(ag)
+    den = AG + al
+    return F.where(den != 0, 100 * AG / den, 50.0)
+
+
 def wilder_rsi(close: torch.Tensor, window: int = 14) -> torch.Tensor:
     """Wilder RSI: ewm(alpha=1/window, min_periods=window, adjust=False) of
     gains/losses, 100*g/(g+l), 50 where g+l == 0 (NaN warm-up kept)."""
-    delta = _diff(close, 1)
-    gain = _clip_lower(delta, 0.0)
-    loss = -torch.where(delta > 0, torch.zeros_like(delta), delta)   # -delta.clip(upper=0), NaN stays
-    ag, al = engine.rolling_many(engine.Ewm(gain, alpha=1 / window, min_periods=window),
-                                 engine.Ewm(loss, alpha=1 / window, min_periods=window))
-    den = ag + al
-    return torch.where(den != 0, 100 * ag / den, torch.full_like(den, 50.0))
+    return F.run({"rsi": _rsi_ex(close, window)})["rsi"]
+
+
+def _trend_ex(close: torch.Tensor, fast: int, slow: int) -> F.Ex:
+    f, s = engine.rolling_many(engine.Ewm(close, span=fast), engine.Ewm(close, span=slow))
+    Fx, Sx = F.inp(f), F.inp(s)
+    return F.where(Sx == 0, 0.0, (Fx - Sx) / Sx.abs())
 
 
 def trend_score(close: torch.Tensor, fast: int = 20, slow: int = 50) -> torch.Tensor:
     """(ema_fast - ema_slow) / |ema_slow|, 0 where ema_slow == 0."""
-    f, s = engine.rolling_many(engine.Ewm(close, span=fast), engine.Ewm(close, span=slow))
-    return torch.where(s == 0, torch.zeros_like(s), (f - s) / s.abs())
+    return F.run({"t": _trend_ex(close, fast, slow)})["t"]
 
 
 def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int = 14) -> torch.Tensor:
     """_compute_adx at every t: rolling-sum DI+/DI-, dx NaN -> 0, mean over
     `window`; NaN (short history) -> 100."""
-    hd = _diff(high, 1)
-    ld = -_diff(low, 1)
-    zero = torch.zeros_like(hd)
-    plus_dm = torch.where((hd > ld) & (hd > 0), hd, zero)
-    minus_dm = torch.where((ld > hd) & (ld > 0), ld, zero)
-    pc = _shift(close, 1)
-    tr = torch.fmax(torch.fmax(high - low, (high - pc).abs()), (low - pc).abs())   # max(axis=1) skips NaN
+    H, L, C = F.inp(high), F.inp(low), F.inp(close)
+    hd = F.diff(H, 1)
+    ld = -F.diff(L, 1)
+    pc = F.shift(C, 1)
+    dm = F.run({
+        "tr": F.fmax(F.fmax(H - L, (H - pc).abs()), (L - pc).abs()),   # max(axis=1) skips NaN
+        "plus": F.where((hd > ld) & (hd > 0), hd, 0.0),
+        "minus": F.where((ld > hd) & (ld > 0), ld, 0.0),
+    })
     atr_sum, plus_sum, minus_sum = engine.rolling_many(
-        engine.Roll(tr, window, "sum"), engine.Roll(plus_dm, window, "sum"), engine.Roll(minus_dm, window, "sum"))
-    plus_di = 100.0 * plus_sum / atr_sum
-    minus_di = 100.0 * minus_sum / atr_sum
+        engine.Roll(dm["tr"], window, "sum"), engine.Roll(dm["plus"], window, "sum"),
+        engine.Roll(dm["minus"], window, "sum"))
+    A = F.inp(atr_sum)
+    plus_di = 100.0 * F.inp(plus_sum) / A
+    minus_di = 100.0 * F.inp(minus_sum) / A
     total = plus_di + minus_di
-    dx = 100.0 * (plus_di - minus_di).abs() / torch.where(total != 0, total, torch.full_like(total, NAN))
-    dx = torch.nan_to_num(dx, nan=0.0, posinf=torch.inf, neginf=-torch.inf)   # fillna(0.0)
+    dx = 100.0 * (plus_di - minus_di).abs() / F.where(total != 0, total, NAN)
+    dx = F.run({"dx": F.fillna(dx, 0.0)})["dx"]
     a = engine.rolling(dx, window, "mean")
-    return torch.where(torch.isnan(a), torch.full_like(a, 100.0), a)
+    return F.run({"adx": F.fillna(a, 100.0)})["adx"]
 
 
 def zscore(close: torch.Tensor, window: int = 20) -> torch.Tensor:
     """_compute_zscore at every t: (c - mean) / std(ddof=0); 0 where std is 0
     or NaN."""
     mean, std = engine.rolling_many(engine.Roll(close, window, "mean"), engine.Roll(close, window, "std0"))
-    bad = (std == 0) | torch.isnan(std)
-    return torch.where(bad, torch.zeros_like(std), (close - mean) / std)
+    SD = F.inp(std)
+    bad = (SD == 0) | F.isnan(SD)
+    return F.run({"z": F.where(bad, 0.0, (F.inp(close) - mean) / SD)})["z"]
 
 
 def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56, lookback_high: int = 48,
@@ -101,8 +117,6 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     S, T = c.shape
     dev = c.device
     eps = 1e-6
-    vals: dict[str, torch.Tensor] = {}
-    vals["close"], vals["open"], vals["high"], vals["low"], vals["volume"] = c, o, h, l, v
     R, E = engine.Roll, engine.Ewm
     # df["high"].iloc[-49:-1].max(): the 48 highs before t (fewer when short; nan-skipping)
     specs = [R(v, volume_window, "mean"), R(h, lookback_high, "max", min_periods=1, shift=1), E(c, span=20),
@@ -110,50 +124,55 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     if qv is not None:
         specs.append(R(qv, volume_window, "mean"))
     res = engine.rolling_many(*specs)
-    vma, vals["previous_high"], e20, e50 = res[:4]
-    if qv is not None:
-        vals["quote_volume"] = qv
-        qvma = res[4]
-    else:
-        vals["quote_volume"] = v * c
-        qvma = vma * c
+    vma, prev_high, e20, e50 = res[:4]
+    qvma = res[4] if qv is not None else None
+    C, O, H, L, V = (F.inp(x) for x in (c, o, h, l, v))
+    QV = F.inp(qv) if qv is not None else V * C
+    QVMA = F.inp(qvma) if qv is not None else F.inp(vma) * C
+    # close.iloc[-k - 1] of the prefix frame (t + 1 rows) is close[t - k]; rows
+    # with t < k are history_too_short (min_history > 24), masked below
     t = torch.arange(T, device=dev, dtype=torch.int64)
-
-    def back(k):
-        # close.iloc[-k - 1] of the prefix frame (t + 1 rows): index t - k,
-        # wrapping like python when t < k (those rows are history_too_short)
-        return c[:, torch.remainder(t - k, t + 1)]
-
-    vals["return_1h"] = c / back(4) - 1
-    vals["return_2h"] = c / back(8) - 1
-    vals["return_6h"] = c / back(24) - 1
     anchor = torch.clamp(t - full_extension_bars, min=0)
     bars = (t - anchor).to(torch.float64)
-    vals["extension_return"] = c / c[:, anchor] - 1
-    vals["extension_window_bars"] = bars.expand(S, T)
     short_cap = torch.clamp(max_extension * (bars / full_extension_bars), min=min_short_extension_cap)
     cap = torch.where(bars < full_extension_bars, short_cap, torch.full_like(bars, max_extension))
-    vals["extension_cap"] = cap.expand(S, T)
-    vals["candle_return"] = c / o - 1
-    vals["volume_ratio"] = v / (vma + eps)
-    vals["quote_volume_ratio"] = vals["quote_volume"] / (qvma + eps)
-    rng = h - l
-    vals["range_position"] = (c - l) / (rng + eps)
-    vals["upper_wick_fraction"] = (h - torch.maximum(o, c)) / (rng + eps)
-    vals["ema20"] = e20
-    vals["ema50"] = e50
-    vals["atr"] = atr if atr is not None else torch.zeros_like(c)
-    status = torch.full((S, T), TG_READY, dtype=torch.int8, device=dev)
-    finite = torch.ones((S, T), dtype=torch.bool, device=dev)
+    BARS, CAP = F.inp(bars), F.inp(cap)
+    # close at the anchor: close[t - 96], or the first close while t < 96
+    c_anchor = F.where(BARS < full_extension_bars, F.inp(c[:, :1]), F.shift(C, full_extension_bars))
+    rng = H - L
+    ex = {
+        "close": C, "open": O, "high": H, "low": L, "volume": V, "quote_volume": QV,
+        "previous_high": F.inp(prev_high),
+        "return_1h": C / F.shift(C, 4) - 1,
+        "return_2h": C / F.shift(C, 8) - 1,
+        "return_6h": C / F.shift(C, 24) - 1,
+        "extension_return": C / c_anchor - 1,
+        "extension_window_bars": BARS,
+        "extension_cap": CAP,
+        "candle_return": C / O - 1,
+        "volume_ratio": V / (F.inp(vma) + eps),
+        "quote_volume_ratio": QV / (QVMA + eps),
+        "range_position": (C - L) / (rng + eps),
+        "upper_wick_fraction": (H - F.maximum(O, C)) / (rng + eps),
+        "ema20": F.inp(e20),
+        "ema50": F.inp(e50),
+        "atr": F.inp(atr) if atr is not None else F.const(0.0),
+    }
+    # status: not finite -> NOT_READY, then python min() <= 0 -> INVALID, then short history
+    finite = None
     for k in TG_KEYS:
-        finite &= torch.isfinite(vals[k])
-    status[~finite] = TG_NOT_READY
-    mn = torch.minimum(torch.minimum(torch.minimum(c, o), torch.minimum(h, l)), v)
-    status[~(mn > 0) & ~torch.isnan(mn)] = TG_INVALID_CANDLE   # python min() <= 0
-    status[:, : min_history - 1] = TG_SHORT_HISTORY
-    ready = status == TG_READY
-    out = {k: torch.where(ready, vals[k], torch.full_like(c, NAN)) for k in TG_KEYS}
-    return out, status
+        x = ex[k]
+        ok = ~F.isnan(x - x)          # x - x is NaN for NaN and +-inf
+        finite = ok if finite is None else finite & ok
+    mn = F.minimum(F.minimum(F.minimum(C, O), F.minimum(H, L)), V)
+    invalid = ~(mn > 0) & ~F.isnan(mn)
+    short = F.inp(t.to(torch.float64)) < float(min_history - 1)   # len(prefix) = t + 1 < min_history
+    code = F.where(short, float(TG_SHORT_HISTORY),
+                   F.where(invalid, float(TG_INVALID_CANDLE), F.where(finite, float(TG_READY), float(TG_NOT_READY))))
+    status_f = F.run({"status": code}, S, T)["status"]
+    ready = F.inp(status_f) == float(TG_READY)
+    out = F.run({k: F.where(ready, ex[k], NAN) for k in TG_KEYS}, S, T)
+    return out, status_f.to(torch.int8)
 
 
 def mean_reversion_features(o, h, l, c, v, atr, rsi_window: int = 14, volume_ma_window: int = 20,
@@ -161,14 +180,15 @@ def mean_reversion_features(o, h, l, c, v, atr, rsi_window: int = 14, volume_ma_
     """The per-candle inputs MeanReversionFade reads (strategies/mean_reversion_fade.py:240-255):
     rsi / previous_rsi, volume_ma, atr_ma, trend_score and the upper rejection
     ratio of _resolve_entry (:124-134)."""
-    rsi = wilder_rsi(c, rsi_window)
-    rng = h - l
+    rsi = _rsi_ex(c, rsi_window)
     vma, ama = engine.rolling_many(engine.Roll(v, volume_ma_window, "mean"), engine.Roll(atr, atr_ma_window, "mean"))
-    return {
+    H, L, O, C = F.inp(h), F.inp(l), F.inp(o), F.inp(c)
+    rng = H - L
+    res = F.run({
         "rsi": rsi,
-        "previous_rsi": _shift(rsi, 1),
-        "volume_ma": vma,
-        "atr_ma": ama,
-        "trend_score": trend_score(c, fast, slow),
-        "upper_rejection_ratio": torch.where(rng > 0, (h - torch.maximum(o, c)) / rng, torch.full_like(c, NAN)),
-    }
+        "previous_rsi": F.shift(rsi, 1),
+        "trend_score": _trend_ex(c, fast, slow),
+        "upper_rejection_ratio": F.where(rng > 0, (H - F.maximum(O, C)) / rng, NAN),
+    })
+    return {"rsi": res["rsi"], "previous_rsi": res["previous_rsi"], "volume_ma": vma, "atr_ma": ama,
+            "trend_score": res["trend_score"], "upper_rejection_ratio": res["upper_rejection_ratio"]}

@@ -8,13 +8,15 @@
   (strategies/failed_spike_fade.py:533-544): base / early features, the
   whole-series auto-calibration, labels, cooldown and streaks.
 
-The order statistics and recurrences run in the hand-written kernels of
-bq_rolling.hip (rolling median / quantile / mean / sum / var / std / max / min
-with pandas' NaN and min_periods rules; ewm with NaN-gap decay) and
-bq_select.hip (whole-series numpy quantile, sequential cooldown); the
-element-wise glue is
-device tensor arithmetic in the reference's operation order. Every column
-keeps the reference's name; booleans are returned as torch.bool.
+Each pipeline is a few stages: the order statistics, recurrences and
+forward fills run in the kernels of bq_rolling.hip (rolling median / quantile
+/ mean / sum / var / std / max / min with pandas' NaN and min_periods rules;
+ewm with NaN-gap decay; ffill), batched per stage; the element-wise glue
+between them is one fused program per stage (binquant_amd.fused,
+bq_fused_eval) written in the reference's operation order, so every column
+equals the unfused arithmetic bit for bit. bq_select.hip adds the
+whole-series numpy quantile and the sequential cooldown. Every column keeps
+the reference's name; booleans are returned as torch.bool.
 """
 
 from __future__ import annotations
@@ -24,60 +26,18 @@ from dataclasses import dataclass
 import torch
 
 from . import engine
+from . import fused as F
 
 NAN = float("nan")
+R, E, FF = engine.Roll, engine.Ewm, engine.Ffill
 
 
-def _shift(x: torch.Tensor, n: int) -> torch.Tensor:
-    """pandas Series.shift(n) along T (negative n shifts backwards)."""
-    out = torch.full_like(x, NAN)
-    T = x.shape[-1]
-    if 0 <= n < T:
-        out[..., n:] = x[..., : T - n]
-    elif -T < n < 0:
-        out[..., : T + n] = x[..., -n:]
-    return out
-
-
-def _diff(x: torch.Tensor, n: int = 1) -> torch.Tensor:
-    """Series.diff(n)."""
-    return x - _shift(x, n)
-
-
-def _clip_lower(x: torch.Tensor, lo: float) -> torch.Tensor:
-    """Series.clip(lower=lo): NaN stays NaN."""
-    return torch.where(x < lo, torch.full_like(x, lo), x)
-
-
-def _gt(a, b):
-    """Elementwise a > b with NaN -> False (pandas comparison semantics)."""
-    return a > b
-
-
-def _replace0(x: torch.Tensor) -> torch.Tensor:
-    """Series.replace(0, nan)."""
-    return torch.where(x == 0, torch.full_like(x, NAN), x)
-
-
-def _pct_change(x: torch.Tensor, periods: int) -> torch.Tensor:
-    """Series.pct_change(periods) with pandas 2.3.3's default fill_method='pad':
-    forward-fill NaNs first ([1,2,nan,4,5] -> [nan,1,0,1,0.25])."""
-    f = _ffill(x)
-    return f / _shift(f, periods) - 1
-
-
-def _ffill(x: torch.Tensor) -> torch.Tensor:
-    """Forward fill along T, sync-free (no data-dependent host branch, so a
-    pipeline using it can be captured in a hipGraph)."""
-    T = x.shape[-1]
-    idx = torch.arange(T, device=x.device).expand_as(x)
-    valid = ~torch.isnan(x)
-    last = torch.where(valid, idx, torch.zeros_like(idx))
-    last = torch.cummax(last, dim=-1).values
-    out = torch.gather(x, -1, last)
-    # positions before the first observation stay NaN
-    seen = torch.cummax(valid.to(torch.int8), dim=-1).values.bool()
-    return torch.where(seen, out, torch.full_like(x, NAN))
+def pct_change_filled(filled: torch.Tensor | F.Ex, periods: int) -> F.Ex:
+    """Series.pct_change(periods) with pandas 2.3.3's default fill_method='pad',
+    given the forward-filled series (engine.Ffill): ffill(x) / ffill(x).shift(p) - 1
+    ([1,2,nan,4,5] -> [nan,1,0,1,0.25])."""
+    f = F._as_ex(filled)
+    return f / F.shift(f, periods) - 1
 
 
 @dataclass
@@ -102,66 +62,76 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     p = p or BurstParams()
     has_q = qv is not None
     bw = max(p.lookback_window, 2)
-    out: dict[str, torch.Tensor] = {}
+    O, H, L, C, V = (F.inp(t) for t in (o, h, l, c, v))
+    Q = F.inp(qv) if has_q else None
+    mb = p.min_baseline_volume
     # volume.shift(2).rolling(bw - 1, min_periods=bw - 1).median()   (:58-63)
-    R = engine.Roll
-    up = (c > _shift(c, 1)).to(torch.float64)
+    up = F.run({"up": (C > F.shift(C, 1)).float()})["up"]
     specs = [R(v, bw - 1, "median", min_periods=bw - 1, shift=2), R(up, 3, "sum", min_periods=3)]
     if has_q:
         specs.append(R(qv, bw - 1, "median", min_periods=bw - 1, shift=2))
     res = engine.rolling_many(*specs)
-    out["baseline_volume"] = res[0]
-    out["baseline_volume_safe"] = _clip_lower(out["baseline_volume"], p.min_baseline_volume)
-    out["volume_ratio"] = v / out["baseline_volume_safe"]
+    e: dict[str, object] = {}
+    e["baseline_volume"] = res[0]
+    bvs = F.clip_lower(res[0], mb)
+    e["baseline_volume_safe"] = bvs
+    vr = V / bvs
+    e["volume_ratio"] = vr
     if has_q:
-        out["baseline_quote_volume"] = res[2]
-        out["baseline_quote_volume_safe"] = _clip_lower(out["baseline_quote_volume"], p.min_baseline_volume)
-        out["quote_volume_ratio"] = qv / out["baseline_quote_volume_safe"]
+        e["baseline_quote_volume"] = res[2]
+        bqs = F.clip_lower(res[2], mb)
+        e["baseline_quote_volume_safe"] = bqs
+        qvr = Q / bqs
+        e["quote_volume_ratio"] = qvr
     else:
+        qvr = F.const(1.0)
+        e["quote_volume_ratio"] = qvr
+    prev_close = F.clip_lower(F.shift(C, 1), mb)
+    candle_range = F.clip_lower(H - L, mb)
+    candle_body = (C - O).abs()
+    pj = (C - F.shift(C, 1)) / prev_close
+    e["price_jump"] = pj
+    rf = candle_range / F.clip_lower(C, mb)
+    e["range_frac"] = rf
+    bf = candle_body / candle_range
+    e["body_frac"] = bf
+    cth = (H - C) / candle_range
+    e["close_to_high"] = cth
+    bull = C > O
+    e["is_bullish"] = bull
+    e["recent_up_closes"] = res[1]
+    e["vol_spike"] = V > (p.volume_multiplier * bvs)
+    e["quote_vol_spike"] = Q > (p.quote_volume_multiplier * bqs) if has_q else F.const(True)
+    e["price_jump_flag"] = pj > p.price_threshold
+    e["range_expansion_flag"] = rf > p.min_range_frac
+    e["body_quality_flag"] = bull & (bf > p.min_body_frac) & (cth < p.max_close_to_high)
+    min_up = p.min_recent_up_closes if has_q else 1
+    e["trend_quality_flag"] = F.inp(res[1]) >= min_up
+    pjc = F.clip_lower(pj, 0.0)
+    e["activity_burst_score"] = vr * qvr * pjc * (1 + bf) if has_q else vr * pjc
+    out = F.run(e)
+    if not has_q:
         out["baseline_quote_volume"] = out["baseline_volume"]
         out["baseline_quote_volume_safe"] = out["baseline_volume_safe"]
-        out["quote_volume_ratio"] = torch.ones_like(c)
-    prev_close = _clip_lower(_shift(c, 1), p.min_baseline_volume)
-    candle_range = _clip_lower(h - l, p.min_baseline_volume)
-    candle_body = (c - o).abs()
-    out["price_jump"] = (c - _shift(c, 1)) / prev_close
-    out["range_frac"] = candle_range / _clip_lower(c, p.min_baseline_volume)
-    out["body_frac"] = candle_body / candle_range
-    out["close_to_high"] = (h - c) / candle_range
-    out["is_bullish"] = c > o
-    out["recent_up_closes"] = res[1]
-    out["vol_spike"] = v > (p.volume_multiplier * out["baseline_volume_safe"])
-    if has_q:
-        out["quote_vol_spike"] = qv > (p.quote_volume_multiplier * out["baseline_quote_volume_safe"])
-    else:
-        out["quote_vol_spike"] = torch.ones_like(c, dtype=torch.bool)
-    out["price_jump_flag"] = out["price_jump"] > p.price_threshold
-    out["range_expansion_flag"] = out["range_frac"] > p.min_range_frac
-    out["body_quality_flag"] = (
-        out["is_bullish"] & (out["body_frac"] > p.min_body_frac) & (out["close_to_high"] < p.max_close_to_high)
-    )
-    min_up = p.min_recent_up_closes if has_q else 1
-    out["trend_quality_flag"] = out["recent_up_closes"] >= min_up
-    pj = _clip_lower(out["price_jump"], 0.0)
-    if has_q:
-        out["activity_burst_score"] = out["volume_ratio"] * out["quote_volume_ratio"] * pj * (1 + out["body_frac"])
-    else:
-        out["activity_burst_score"] = out["volume_ratio"] * pj
     # score.shift(1).rolling(80, min_periods=20).quantile(0.92)   (:134-139)
     out["score_threshold"] = engine.rolling(
         out["activity_burst_score"], p.score_lookback, "quantile", q=p.score_quantile,
         min_periods=p.lookback_window, shift=1,
     )
-    thr = torch.nan_to_num(out["score_threshold"], nan=0.0)
-    raw = (
-        out["vol_spike"] & out["quote_vol_spike"] & out["price_jump_flag"] & out["range_expansion_flag"]
-        & out["body_quality_flag"] & out["trend_quality_flag"] & (out["activity_burst_score"] >= thr)
-    )
+    thr = F.fillna(out["score_threshold"], 0.0)
+    flags = [F.inp(out[k]) for k in ("vol_spike", "quote_vol_spike", "price_jump_flag", "range_expansion_flag",
+                                     "body_quality_flag", "trend_quality_flag")]
+    raw = flags[0] & flags[1] & flags[2] & flags[3] & flags[4] & flags[5] & (F.inp(out["activity_burst_score"]) >= thr)
+    rawf = F.run({"raw": raw.float()})["raw"]
     # raw.shift(1).rolling(cooldown, min_periods=1).max().fillna(False)   (:147-152)
-    recent = engine.rolling(raw.to(torch.float64), p.cooldown_bars, "max", min_periods=1, shift=1)
-    recent = torch.nan_to_num(recent, nan=0.0) > 0
-    out["qualified_signal"] = raw & ~recent
-    return out
+    recent = engine.rolling(rawf, p.cooldown_bars, "max", min_periods=1, shift=1)
+    out["qualified_signal"] = F.run({"q": F.inp(rawf).bool() & ~(F.fillna(recent, 0.0) > 0)})["q"]
+    order = ["baseline_volume", "baseline_volume_safe", "volume_ratio", "baseline_quote_volume",
+             "baseline_quote_volume_safe", "quote_volume_ratio", "price_jump", "range_frac", "body_frac",
+             "close_to_high", "is_bullish", "recent_up_closes", "vol_spike", "quote_vol_spike", "price_jump_flag",
+             "range_expansion_flag", "body_quality_flag", "trend_quality_flag", "activity_burst_score",
+             "score_threshold", "qualified_signal"]
+    return {k: out[k] for k in order}
 
 
 @dataclass
@@ -181,40 +151,52 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -
     open_time grid (NaN where the benchmark has no candle), as
     `result[["open_time"]].merge(btc_by_open_time, how="left")` yields."""
     p = p or PumpParams()
-    out: dict[str, torch.Tensor] = {}
-    prev = _shift(c, 1)
-    tr = torch.fmax(torch.fmax(h - l, (h - prev).abs()), (l - prev).abs())   # concat(...).max(axis=1) skips NaN
-    R, E = engine.Roll, engine.Ewm
-    atr, vmean, hmax, lmin, e20, e50 = engine.rolling_many(
+    H, L, C, V = (F.inp(t) for t in (h, l, c, v))
+    prev = F.shift(C, 1)
+    tr = F.run({"tr": F.fmax(F.fmax(H - L, (H - prev).abs()), (L - prev).abs())})["tr"]   # max(axis=1) skips NaN
+    bench = btc_close.reshape(1, -1).contiguous()
+    atr, vmean, hmax, lmin, e20, e50, cf = engine.rolling_many(
         E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
         R(h, p.compression_bars, "max", shift=1), R(l, p.compression_bars, "min", shift=1),
-        E(c, span=20), E(c, span=50),
+        E(c, span=20), E(c, span=50), FF(c),
     )
-    out["candidate_atr"] = atr
-    out["momentum_3"] = _pct_change(c, p.momentum_bars)
-    out["relative_volume"] = v / vmean
-    out["pre_breakout_compression"] = (hmax - lmin) / prev
-    out["pump_score"] = (
-        out["relative_volume"] * _clip_lower(out["momentum_3"], 0.0) / _replace0(out["pre_breakout_compression"])
+    bf, be20, be50 = engine.rolling_many(FF(bench), E(bench, span=20), E(bench, span=50))
+    e: dict[str, object] = {}
+    e["candidate_atr"] = atr
+    m3 = pct_change_filled(cf, p.momentum_bars)
+    e["momentum_3"] = m3
+    rv = V / vmean
+    e["relative_volume"] = rv
+    comp = (F.inp(hmax) - lmin) / prev
+    e["pre_breakout_compression"] = comp
+    e["pump_score"] = rv * F.clip_lower(m3, 0.0) / F.replace0(comp)
+    st = F.run(e)
+    thr_s, thr_v = engine.rolling_many(
+        R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
     )
-    out["score_threshold"], out["volume_threshold"] = engine.rolling_many(
-        R(out["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
-        R(out["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
-    )
-    out["score_cross"] = (out["pump_score"] >= out["score_threshold"]) & (
-        _shift(out["pump_score"], 1) < _shift(out["score_threshold"], 1)
-    )
-    out["prior_high"] = hmax
-    out["close_location"] = (c - l) / _replace0(h - l)
-    out["ema20"] = e20
-    out["ema50"] = e50
-    out["trend_score"] = (out["ema20"] - out["ema50"]) / out["ema50"]
-    out["momentum_atr"] = out["momentum_3"] / (out["candidate_atr"] / c)
-    bench = btc_close.reshape(1, -1)
-    out["btc_momentum_3"] = _pct_change(bench, p.momentum_bars).expand_as(c)
-    be20, be50 = engine.rolling_many(E(bench.contiguous(), span=20), E(bench.contiguous(), span=50))
-    out["btc_trend_score"] = ((be20 - be50) / be50).expand_as(c)
-    out["relative_strength"] = out["momentum_3"] - out["btc_momentum_3"]
+    PS, TS = F.inp(st["pump_score"]), F.inp(thr_s)
+    E20, E50 = F.inp(e20), F.inp(e50)
+    bm3 = pct_change_filled(F.inp(bf[0]), p.momentum_bars)   # one series for every symbol
+    be50x = F.inp(be50[0])
+    e2: dict[str, object] = {
+        "score_cross": (PS >= TS) & (F.shift(PS, 1) < F.shift(TS, 1)),
+        "close_location": (C - L) / F.replace0(H - L),
+        "trend_score": (E20 - E50) / E50,
+        "momentum_atr": F.inp(st["momentum_3"]) / (F.inp(atr) / C),
+        "btc_momentum_3": bm3,
+        "btc_trend_score": (F.inp(be20[0]) - be50x) / be50x,
+        "relative_strength": F.inp(st["momentum_3"]) - bm3,
+    }
+    st2 = F.run(e2, *c.shape)
+    out = {
+        "candidate_atr": atr, "momentum_3": st["momentum_3"], "relative_volume": st["relative_volume"],
+        "pre_breakout_compression": st["pre_breakout_compression"], "pump_score": st["pump_score"],
+        "score_threshold": thr_s, "volume_threshold": thr_v, "score_cross": st2["score_cross"], "prior_high": hmax,
+        "close_location": st2["close_location"], "ema20": e20, "ema50": e50, "trend_score": st2["trend_score"],
+        "momentum_atr": st2["momentum_atr"], "btc_momentum_3": st2["btc_momentum_3"],
+        "btc_trend_score": st2["btc_trend_score"], "relative_strength": st2["relative_strength"],
+    }
     return out
 
 
@@ -255,151 +237,184 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
     'price_break_base_threshold' hold the per-symbol auto-calibrated values."""
     p = p or SpikeParams()
     eps = 1e-6
-    out: dict[str, torch.Tensor] = {}
+    S, T = c.shape
     w = p.base_window
+    O, H, L, C, V, Q = (F.inp(t) for t in (o, h, l, c, v, qv))
     # ---- compute_base_features (:260-322) ----
-    pc = _pct_change(c, 1)
+    (cf,) = engine.rolling_many(FF(c))
+    pc = pct_change_filled(cf, 1)
     pca = pc.abs()
-    out["price_change"] = pc
-    out["price_change_abs"] = pca
-    body = (c - o).abs()
-    out["body_size"] = body
-    out["body_size_pct"] = body / (o + eps)
-    out["upper_wick"] = h - torch.fmax(c, o)          # DataFrame.max(axis=1) skips NaN
-    out["lower_wick"] = torch.fmin(c, o) - l
-    out["upper_wick_ratio"] = out["upper_wick"] / (body + eps)
-    out["lower_wick_ratio"] = out["lower_wick"] / (body + eps)
-    out["total_range"] = h - l
-    out["range_pct"] = out["total_range"] / (o + eps)
-    out["is_bullish"] = c > o
-    out["close_open_ratio"] = (c - o) / (o + eps)
-    # every rolling series that depends only on the inputs: ONE batched call
-    R, E = engine.Roll, engine.Ewm  # noqa: F841
-    bsp = out["body_size_pct"]
+    body = (C - O).abs()
+    bsp = body / (O + eps)
+    e: dict[str, object] = {
+        "price_change": pc, "price_change_abs": pca, "body_size": body, "body_size_pct": bsp,
+        "upper_wick": H - F.fmax(C, O),          # DataFrame.max(axis=1) skips NaN
+        "lower_wick": F.fmin(C, O) - L,
+    }
+    e["upper_wick_ratio"] = e["upper_wick"] / (body + eps)
+    e["lower_wick_ratio"] = e["lower_wick"] / (body + eps)
+    e["total_range"] = H - L
+    e["range_pct"] = e["total_range"] / (O + eps)
+    e["is_bullish"] = C > O
+    e["close_open_ratio"] = (C - O) / (O + eps)
     cw, n = p.cumulative_price_window, p.streak_length
-    neg_pc = torch.where(pc > 0, torch.zeros_like(pc), pc).abs()   # clip(upper=0).abs(), NaN stays
-    specs = [R(c, w, "mean"), R(c, w, "std"), R(v, w, "mean"), R(v, w, "std"), R(qv, w, "mean"),
-             R(c, 8, "std"), R(c, 20, "std"), R(pc, 2, "sum"), R(pc, 3, "sum"),
-             R((pc > 0).to(torch.float64), 5, "sum"), R(pca, 5, "sum"), R(bsp, 10, "mean"), R(bsp, 10, "std"),
-             R((c > o).to(torch.float64), n, "sum"), R((c < o).to(torch.float64), n, "sum")]
+    # the rolling operands that are element-wise expressions
+    e["_pos"] = (pc > 0).float()
+    e["_green"] = (C > O).float()
+    e["_red"] = (C < O).float()
     if cw > 1:
-        specs += [R(_clip_lower(pc, 0.0), cw, "sum"), R(neg_pc, cw, "sum")]
+        e["_clip_pos"] = F.clip_lower(pc, 0.0)
+        e["_neg"] = F.where(pc > 0, 0.0, pc).abs()   # clip(upper=0).abs(), NaN stays
+    b = F.run(e)
+    # every rolling series that depends only on the inputs: ONE batched call
+    specs = [R(c, w, "mean"), R(c, w, "std"), R(v, w, "mean"), R(v, w, "std"), R(qv, w, "mean"),
+             R(c, 8, "std"), R(c, 20, "std"), R(b["price_change"], 2, "sum"), R(b["price_change"], 3, "sum"),
+             R(b["_pos"], 5, "sum"), R(b["price_change_abs"], 5, "sum"), R(b["body_size_pct"], 10, "mean"),
+             R(b["body_size_pct"], 10, "std"), R(b["_green"], n, "sum"), R(b["_red"], n, "sum")]
+    if cw > 1:
+        specs += [R(b["_clip_pos"], cw, "sum"), R(b["_neg"], cw, "sum")]
     if p.price_break_use_dynamic:
-        specs.append(R(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20))
+        specs.append(R(b["price_change_abs"], 60, "quantile", q=p.price_break_dynamic_q, min_periods=20))
     res = engine.rolling_many(*specs)
     (price_ma, price_std, volume_ma, volume_std, qv_ma, s8, s20, pc2, pc3, pos5, abs5, bsp_ma, bsp_sd, green,
      red) = res[:15]
     cum_pos, cum_neg = (res[15], res[16]) if cw > 1 else (None, None)
     dyn = res[-1] if p.price_break_use_dynamic else None
-    out["price_ma"] = price_ma
-    out["price_std"] = price_std
-    out["price_zscore"] = (c - out["price_ma"]) / (out["price_std"] + eps)
-    out["volume_ma"] = volume_ma
-    vr = v / (out["volume_ma"] + eps)
-    out["volume_ratio"] = vr
-    out["volume_zscore"] = (v - out["volume_ma"]) / (volume_std + eps)
-    out["quote_volume_ma"] = qv_ma
-    out["quote_volume_ratio"] = qv / (out["quote_volume_ma"] + eps)
-    out["momentum_3"] = _pct_change(c, 3)
-    out["momentum_5"] = _pct_change(c, 5)
-    out["close_to_high"] = (h - c) / (h + eps)
-    out["close_to_low"] = (c - l + eps) / (c + eps)
+    VR = V / (F.inp(volume_ma) + eps)
+    S8, S20 = F.inp(s8), F.inp(s20)
+    BSP = F.inp(b["body_size_pct"])
+    e2: dict[str, object] = {
+        "price_zscore": (C - price_ma) / (F.inp(price_std) + eps),
+        "volume_ratio": VR,
+        "volume_zscore": (V - volume_ma) / (F.inp(volume_std) + eps),
+        "quote_volume_ratio": Q / (F.inp(qv_ma) + eps),
+        "momentum_3": pct_change_filled(cf, 3),
+        "momentum_5": pct_change_filled(cf, 5),
+        "close_to_high": (H - C) / (H + eps),
+        "close_to_low": (C - L + eps) / (C + eps),
+        "std_ratio_8_20": S8 / (S20 + eps),
+        "body_size_pct_z": (BSP - bsp_ma) / (F.inp(bsp_sd) + eps),
+        "vol_compression_flag": S8 < S20 * 0.6,
+    }
+    m = F.run(e2)
     # ---- auto_calibrate (:229-257): whole-series np.quantile of the dropna'd columns ----
+    vr = m["volume_ratio"]
     qv_thr = engine.row_quantile(vr, p.volume_quantile).unsqueeze(1)
-    qp_thr = engine.row_quantile(pca, p.price_base_floor_quantile).unsqueeze(1)
+    qp_thr = engine.row_quantile(b["price_change_abs"], p.price_base_floor_quantile).unsqueeze(1)
     skip = torch.isnan(qv_thr) | torch.isnan(qp_thr)      # vols.empty or pcs.empty
     new_vol = torch.where(qv_thr > p.min_volume_ratio, qv_thr, torch.full_like(qv_thr, p.min_volume_ratio))
     new_floor = torch.where(qp_thr > p.min_price_abs_floor, qp_thr, torch.full_like(qp_thr, p.min_price_abs_floor))
     base0 = p.price_break_base_threshold
     new_base = torch.where(new_floor > base0, new_floor, torch.full_like(new_floor, base0))
-    vcmr = torch.where(skip, torch.full_like(new_vol, p.volume_cluster_min_ratio), new_vol)
-    pbbt = torch.where(skip, torch.full_like(new_base, base0), new_base)
+    vcmr = torch.where(skip, torch.full_like(new_vol, p.volume_cluster_min_ratio), new_vol).contiguous()
+    pbbt = torch.where(skip, torch.full_like(new_base, base0), new_base).contiguous()
+    # ---- compute_early_features (:324-357) and the flag operands ----
+    VRm, VC, PB = F.inp(vr), F.inp(vcmr), F.inp(pbbt)
+    cond = VRm >= VC
+    e3: dict[str, object] = {
+        "vol_ratio_slope_3": F.diff(VRm, 3),
+        "vol_ratio_accel": F.diff(F.diff(VRm, 3), 1),
+        "_cond": cond.float(),
+        "_cond8": (VRm >= VC * 0.8).float(),
+    }
+    if p.price_break_use_dynamic:
+        D = F.inp(dyn)
+        e3["_thr_pre"] = F.where(F.isnan(D), D, F.maximum(PB, D))
+    k = F.run(e3, S, T)
+    # ---- volume_cluster_flag (:360-370), the dynamic threshold's ffill (:372-400) ----
+    specs2 = [R(k["_cond"], p.volume_cluster_window, "sum", min_periods=1),
+              R(k["_cond8"], max(cw, 1), "max")]
+    if p.price_break_use_dynamic:
+        specs2.append(FF(k["_thr_pre"]))
+    res2 = engine.rolling_many(*specs2)
+    cnt, vmax = res2[0], res2[1]
+    THR = F.inp(res2[2]) if p.price_break_use_dynamic else PB
+    base = (F.inp(cnt) >= p.volume_cluster_min_count) & cond
+    if p.volume_cluster_label_mode == "last":
+        vcf = base & ~F.shift(base, -1)
+    elif p.volume_cluster_label_mode == "first":
+        vcf = base & ~F.shift(base, 1)
+    else:
+        vcf = base
+    PCA, PC = F.inp(b["price_change_abs"]), F.inp(b["price_change"])
+    pbf = PCA >= THR
+    # ---- cumulative_price_break_flag (:402-421) ----
+    if cw <= 1:
+        cum_f = cum_s = F.const(False)
+    else:
+        VM = F.inp(vmax)
+        vol_cond = F.isnan(VM) | (VM != 0)          # .astype(bool): NaN -> True
+        cum_f = (F.inp(cum_pos) >= p.cumulative_price_threshold) & vol_cond
+        cum_s = (F.inp(cum_neg) >= p.cumulative_price_threshold) & vol_cond
+    # ---- acceleration_flag (:423-444) ----
+    vd = VRm - F.shift(VRm, p.accel_volume_deriv_window)
+    acc = (vd >= p.accel_volume_deriv_min) & (PCA >= p.accel_price_change_min)
+    acc_l = acc & (PC > 0)
+    acc_s = acc & (PC < 0)
+    # ---- apply_preliminary_label (:446-488) ----
+    combo = (vcf & pbf) if p.require_both_patterns else (vcf | pbf)
+    label_pre = combo | cum_f | acc_l
+    if p.require_bullish_spike:
+        label_pre = label_pre & F.inp(b["is_bullish"])
+    if p.body_size_pct_min > 0:
+        label_pre = label_pre & (BSP >= p.body_size_pct_min)
+    label_short_pre = (combo | cum_s | acc_s) & (C < O)
+    if p.body_size_pct_min > 0:
+        label_short_pre = label_short_pre & (BSP >= p.body_size_pct_min)
+    e4: dict[str, object] = {
+        "volume_cluster_flag": vcf, "price_break_flag": pbf,
+        "price_break_threshold_series": THR,
+        "cumulative_price_break_flag": cum_f, "cumulative_price_break_short_flag": cum_s,
+        "accel_spike_flag": acc_l, "accel_spike_short_flag": acc_s,
+        "label_pre": label_pre, "label_short_pre": label_short_pre,
+        "upward": F.inp(green) >= n, "downward": F.inp(red) >= n,
+        "early_spike_proba": F.const(NAN), "early_proba_aug_flag": F.const(False),
+    }
+    f = F.run(e4, S, T)
+    out: dict[str, torch.Tensor] = {}
+    for key in ("price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
+                "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "is_bullish", "close_open_ratio"):
+        out[key] = b[key]
+    out["price_ma"] = price_ma
+    out["price_std"] = price_std
+    out["price_zscore"] = m["price_zscore"]
+    out["volume_ma"] = volume_ma
+    out["volume_ratio"] = m["volume_ratio"]
+    out["volume_zscore"] = m["volume_zscore"]
+    out["quote_volume_ma"] = qv_ma
+    for key in ("quote_volume_ratio", "momentum_3", "momentum_5", "close_to_high", "close_to_low"):
+        out[key] = m[key]
     out["volume_cluster_min_ratio"] = vcmr.squeeze(1)
     out["price_break_base_threshold"] = pbbt.squeeze(1)
-    # ---- compute_early_features (:324-357) ----
     out["rolling_price_std_8"] = s8
     out["rolling_price_std_20"] = s20
-    out["std_ratio_8_20"] = s8 / (s20 + eps)
-    out["vol_ratio_slope_3"] = _diff(vr, 3)
-    out["vol_ratio_accel"] = _diff(out["vol_ratio_slope_3"], 1)
-    out["pc_1"] = pc
+    out["std_ratio_8_20"] = m["std_ratio_8_20"]
+    out["vol_ratio_slope_3"] = k["vol_ratio_slope_3"]
+    out["vol_ratio_accel"] = k["vol_ratio_accel"]
+    out["pc_1"] = b["price_change"]
     out["pc_2c"] = pc2
     out["pc_3c"] = pc3
     out["pc_pos_count_5"] = pos5
     out["pc_abs_sum_5"] = abs5
     out["body_size_pct_ma_10"] = bsp_ma
     out["body_size_pct_std_10"] = bsp_sd
-    out["body_size_pct_z"] = (bsp - out["body_size_pct_ma_10"]) / (out["body_size_pct_std_10"] + eps)
-    out["vol_compression_flag"] = s8 < s20 * 0.6
-    # ---- volume_cluster_flag (:360-370) ----
-    cond = vr >= vcmr
-    # the two series that need the calibrated ratio: one more batched call
-    cnt, vmax = engine.rolling_many(
-        R(cond.to(torch.float64), p.volume_cluster_window, "sum", min_periods=1),
-        R((vr >= vcmr * 0.8).to(torch.float64), max(cw, 1), "max"),
-    )
-    base = (cnt >= p.volume_cluster_min_count) & cond
-    if p.volume_cluster_label_mode == "last":
-        nxt = torch.zeros_like(base)
-        nxt[:, :-1] = base[:, 1:]
-        vcf = base & ~nxt
-    elif p.volume_cluster_label_mode == "first":
-        prv = torch.zeros_like(base)
-        prv[:, 1:] = base[:, :-1]
-        vcf = base & ~prv
-    else:
-        vcf = base
-    out["volume_cluster_flag"] = vcf
-    # ---- price_break_flag (:372-400), auto_tune off ----
-    if p.price_break_use_dynamic:
-        thr = _ffill(torch.where(torch.isnan(dyn), dyn, torch.maximum(pbbt.expand_as(dyn), dyn)))
-    else:
-        thr = pbbt.expand_as(pca).clone()
-    out["price_break_flag"] = pca >= thr
-    out["price_break_threshold_series"] = thr
-    # ---- cumulative_price_break_flag (:402-421) ----
-    cw = p.cumulative_price_window
-    if cw <= 1:
-        cum_f = torch.zeros_like(cond)
-        cum_s = torch.zeros_like(cond)
-    else:
-        vol_cond = torch.isnan(vmax) | (vmax != 0)          # .astype(bool): NaN -> True
-        cum_f = (cum_pos >= p.cumulative_price_threshold) & vol_cond
-        cum_s = (cum_neg >= p.cumulative_price_threshold) & vol_cond
-    out["cumulative_price_break_flag"] = cum_f
-    out["cumulative_price_break_short_flag"] = cum_s
-    # ---- acceleration_flag (:423-444) ----
-    vd = vr - _shift(vr, p.accel_volume_deriv_window)
-    acc = (vd >= p.accel_volume_deriv_min) & (pca >= p.accel_price_change_min)
-    out["accel_spike_flag"] = acc & (pc > 0)
-    out["accel_spike_short_flag"] = acc & (pc < 0)
-    # ---- apply_preliminary_label (:446-488) ----
-    if p.require_both_patterns:
-        combo = vcf & out["price_break_flag"]
-    else:
-        combo = vcf | out["price_break_flag"]
-    label_pre = combo | cum_f | out["accel_spike_flag"]
-    if p.require_bullish_spike:
-        label_pre = label_pre & out["is_bullish"]
-    if p.body_size_pct_min > 0:
-        label_pre = label_pre & (bsp >= p.body_size_pct_min)
-    label_short_pre = (combo | cum_s | out["accel_spike_short_flag"]) & (c < o)
-    if p.body_size_pct_min > 0:
-        label_short_pre = label_short_pre & (bsp >= p.body_size_pct_min)
-    out["label_pre"] = label_pre
-    out["label_short_pre"] = label_short_pre
-    # ---- compute_early_proba (:490-493): disabled in the reference ----
-    out["early_spike_proba"] = torch.full_like(c, NAN)
-    out["early_proba_aug_flag"] = torch.zeros_like(label_pre)
+    out["body_size_pct_z"] = m["body_size_pct_z"]
+    out["vol_compression_flag"] = m["vol_compression_flag"]
+    for key in ("volume_cluster_flag", "price_break_flag", "price_break_threshold_series",
+                "cumulative_price_break_flag", "cumulative_price_break_short_flag", "accel_spike_flag",
+                "accel_spike_short_flag", "label_pre", "label_short_pre", "early_spike_proba",
+                "early_proba_aug_flag"):
+        out[key] = f[key]
     # ---- apply_cooldown (:495-520) ----
+    label_pre_t, label_short_t = f["label_pre"], f["label_short_pre"]
     if p.post_spike_cooldown_bars <= 0:
-        out["label"], out["suppressed_label"] = label_pre.clone(), torch.zeros_like(label_pre)
-        out["label_short"], out["suppressed_label_short"] = label_short_pre.clone(), torch.zeros_like(label_pre)
+        out["label"], out["suppressed_label"] = label_pre_t.clone(), torch.zeros_like(label_pre_t)
+        out["label_short"], out["suppressed_label_short"] = label_short_t.clone(), torch.zeros_like(label_pre_t)
     else:
-        out["label"], out["suppressed_label"] = engine.cooldown(label_pre, p.post_spike_cooldown_bars)
-        out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_pre,
+        out["label"], out["suppressed_label"] = engine.cooldown(label_pre_t, p.post_spike_cooldown_bars)
+        out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_t,
                                                                             p.post_spike_cooldown_bars)
     # ---- detect_streaks (:522-531) ----
-    out["upward"] = green >= n
-    out["downward"] = red >= n
+    out["upward"] = f["upward"]
+    out["downward"] = f["downward"]
     return out

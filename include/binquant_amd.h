@@ -213,7 +213,9 @@ enum bq_roll_mode {
   BQ_ROLL_STD = 5,   /* ddof 1 */
   BQ_ROLL_VAR0 = 6,  /* ddof 0 */
   BQ_ROLL_STD0 = 7,  /* ddof 0 */
-  BQ_ROLL_EWM = 8    /* bq_rolling_batch only: ewm(alpha, adjust=False, min_periods) */
+  BQ_ROLL_EWM = 8,   /* bq_rolling_batch only: ewm(alpha, adjust=False, min_periods) */
+  BQ_ROLL_FFILL = 9  /* bq_rolling_batch only: ffill() (leading NaNs stay), shift 0;
+                        Series.pct_change's default fill_method='pad' */
 };
 /*
  * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,
