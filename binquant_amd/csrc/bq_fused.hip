@@ -3,11 +3,13 @@
 //  as one launch per stage instead of one torch kernel
 // per operator, each of which reads and writes a whole [S, T] fp64 panel.
 //
-// Mapping: 256 threads = 256 consecutive candles of one symbol (coalesced
-// loads / stores, shifted loads are offset rows of the same lines). The
+// Mapping: a block = 256 consecutive candles of one symbol (coalesced loads /
+// stores, shifted loads are offset rows of the same lines), one or two per
+// thread. The
 // program is wave-uniform: instructions and operand descriptors are read
 // from the kernarg segment with scalar loads and dispatched by a scalar
-// branch. Program registers live in LDS ([reg][thread], conflict-free);
+// branch. Program registers live in LDS ([reg][thread], conflict-free,
+// sized to the program's register count);
 // the loads are issued together first (up to 16 in flight per thread) so a
 // thread waits for HBM once, not once per operand. Arithmetic is plain IEEE
 // fp64 (-ffp-contract=off: no FMA contraction), in the program's order.
@@ -15,9 +17,31 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <string.h>
+
 namespace bq {
 
-constexpr int FU_NT = 256;
+constexpr int FU_SPAN = 256;   // candles per block
+
+// The launch form of a program (translated from bq_fused_program on the
+// host, once per call): every operand of every instruction is pre-resolved
+// to an LDS slot — registers at r * NT + thread, constants (copied into LDS
+// once per block) at a slot every lane reads — so an instruction reads its
+// three operands with three independent LDS loads and one wait, no branches
+// and no scalar address arithmetic.
+//   code: op (6 bits) | dst slot (13) | A | B | C, operand = slot << 1 | per-lane (14 bits each)
+//   aux:  LD: shift (16, signed) | operand index << 16 | fill constant << 24;
+//         INRANGE: shift; ST: output index
+enum : int { FK_MOV = 63 };
+struct FusedLaunch {
+  int32_t n_ins, n_loads, n_const, cbase;
+  uint64_t code[BQ_FUSED_MAX_INS];
+  int32_t aux[BQ_FUSED_MAX_INS];
+  double consts[BQ_FUSED_MAX_CONST];
+  bq_fused_operand in[BQ_FUSED_MAX_IN];
+  bq_fused_operand out[BQ_FUSED_MAX_OUT];
+};
+static_assert(sizeof(FusedLaunch) <= 4000, "the program travels as a kernel argument (4 KiB)");
 
 __device__ __forceinline__ double fused_load(const bq_fused_operand& X, int64_t sym, int ts) {
   const int64_t off = sym * X.stride_s + (int64_t)ts * X.stride_t;
@@ -25,99 +49,163 @@ __device__ __forceinline__ double fused_load(const bq_fused_operand& X, int64_t 
                             : static_cast<const double*>(X.ptr)[off];
 }
 
-__global__ __launch_bounds__(FU_NT) void fused_kernel(const bq_fused_program P, int T, int nbt) {
-  __shared__ double R[BQ_FUSED_MAX_REGS * FU_NT];
+// one decoded instruction over the K candles of a thread: the dispatch is
+// once per instruction, the arithmetic an element-wise vector expression
+template <int K>
+__device__ __forceinline__ auto vec_op(int op, double __attribute__((ext_vector_type(K))) x,
+                                       double __attribute__((ext_vector_type(K))) y,
+                                       double __attribute__((ext_vector_type(K))) z) {
+  typedef double vk __attribute__((ext_vector_type(K)));
+  vk r;
+  auto b = [](bool c) { return c ? 1.0 : 0.0; };
+  switch (op) {
+    case BQ_F_ADD: return x + y;
+    case BQ_F_SUB: return x - y;
+    case BQ_F_MUL: return x * y;
+    case BQ_F_DIV: return x / y;
+    case BQ_F_NEG: return -x;
+#define BQ_EACH(expr)                          \
+  _Pragma("unroll") for (int k = 0; k < K; ++k) { \
+    const double u = x[k], v = y[k], w = z[k];  \
+    (void)v;                                    \
+    (void)w;                                    \
+    r[k] = (expr);                              \
+  }                                             \
+  return r;
+    case BQ_F_FMAX: BQ_EACH(fmax(u, v))
+    case BQ_F_FMIN: BQ_EACH(fmin(u, v))
+    case BQ_F_MAXIMUM: BQ_EACH((u != u || v != v) ? qnan() : (u > v ? u : v))
+    case BQ_F_MINIMUM: BQ_EACH((u != u || v != v) ? qnan() : (u < v ? u : v))
+    case BQ_F_GT: BQ_EACH(b(u > v))
+    case BQ_F_GE: BQ_EACH(b(u >= v))
+    case BQ_F_LT: BQ_EACH(b(u < v))
+    case BQ_F_LE: BQ_EACH(b(u <= v))
+    case BQ_F_EQ: BQ_EACH(b(u == v))
+    case BQ_F_NE: BQ_EACH(b(u != v))
+    case BQ_F_AND: BQ_EACH(b(u != 0.0 && v != 0.0))
+    case BQ_F_OR: BQ_EACH(b(u != 0.0 || v != 0.0))
+    case BQ_F_NOT: BQ_EACH(b(u == 0.0))
+    case BQ_F_ABS: BQ_EACH(fabs(u))
+    case BQ_F_ISNAN: BQ_EACH(b(u != u))
+    case BQ_F_SQRT: BQ_EACH(sqrt(u))
+    case BQ_F_LOG: BQ_EACH(log(u))
+    case BQ_F_WHERE: BQ_EACH(u != 0.0 ? v : w)
+#undef BQ_EACH
+    default: return x;   // FK_MOV (a constant into a register)
+  }
+}
+
+// K candles per thread (t = block start + k * NT + thread): one decoded
+// instruction is applied to K elements, and a slot is K consecutive doubles
+// in LDS (ds_read_b128 pairs).
+template <int K>
+__global__ __launch_bounds__(FU_SPAN / K) void fused_kernel(const FusedLaunch P, int T, int nbt) {
+  constexpr int NT = FU_SPAN / K;
+  constexpr int LB = K >= 4 ? 8 : 16;   // loads in flight per batch (VGPR budget)
+  typedef double vk __attribute__((ext_vector_type(K)));
+  extern __shared__ double fused_lds[];
+  vk* R = reinterpret_cast<vk*>(fused_lds);   // [n_regs][NT] slots, then the constants
   const int tid = threadIdx.x;
   const int64_t sym = blockIdx.x / nbt;
-  const int t = (int)(blockIdx.x % nbt) * FU_NT + tid;
-  const bool live = t < T;
-  auto reg = [&](uint64_t r) -> double& { return R[(int)r * FU_NT + tid]; };
-
-  // loads first, all in flight together
-  double lv[BQ_FUSED_MAX_LOADS];
+  const int t0 = (int)(blockIdx.x % nbt) * FU_SPAN + tid;
+  for (int j = tid; j < P.n_const; j += NT) R[P.cbase + j] = vk(P.consts[j]);
+  auto load = [&](int ax) -> vk {
+    const int sh = (int)(int16_t)(ax & 0xffff), b = (ax >> 16) & 0xff, c = (ax >> 24) & 0xff;
+    vk v;
 #pragma unroll
-  for (int i = 0; i < BQ_FUSED_MAX_LOADS; ++i) {
-    if (i < P.n_loads) {
-      const uint64_t in = P.ins[i];
-      const int b = (int)((in >> 24) & 0xff), c = (int)((in >> 32) & 0xff);
-      const int ts = t - (int)((int64_t)in >> 40);
-      lv[i] = (live && ts >= 0 && ts < T) ? fused_load(P.in[b], sym, ts) : P.consts[c];
+    for (int k = 0; k < K; ++k) {
+      const int ts = t0 + k * NT - sh;
+      v[k] = (t0 + k * NT < T && ts >= 0 && ts < T) ? fused_load(P.in[b], sym, ts) : P.consts[c];
     }
-  }
+    return v;
+  };
+  auto slot = [&](uint64_t o) -> int { return (int)(o >> 1) + ((o & 1) ? tid : 0); };
+
+  // the load block, LB loads in flight at a time
+  for (int i0 = 0; i0 < P.n_loads; i0 += LB) {
+    vk lv[LB];
 #pragma unroll
-  for (int i = 0; i < BQ_FUSED_MAX_LOADS; ++i)
-    if (i < P.n_loads) reg((P.ins[i] >> 8) & 0xff) = lv[i];
+    for (int i = 0; i < LB; ++i)
+      if (i0 + i < P.n_loads) lv[i] = load(P.aux[i0 + i]);
+#pragma unroll
+    for (int i = 0; i < LB; ++i)
+      if (i0 + i < P.n_loads) R[(int)((P.code[i0 + i] >> 6) & 0x1fff) + tid] = lv[i];
+  }
+  __syncthreads();   // the constants
 
   for (int pc = P.n_loads; pc < P.n_ins; ++pc) {
-    const uint64_t in = P.ins[pc];
-    const int op = (int)(in & 0xff);
-    const uint64_t d = (in >> 8) & 0xff, a = (in >> 16) & 0xff, b = (in >> 24) & 0xff, c = (in >> 32) & 0xff;
-    const int imm = (int)((int64_t)in >> 40);
-    // operands of the arithmetic ops: a register, or a constant (flag bits 40-42)
-    auto opd = [&](uint64_t r, int k) -> double { return ((in >> (40 + k)) & 1) ? P.consts[r] : reg(r); };
-    double r = 0.0;
-    switch (op) {
-      case BQ_F_LD: {   // a load after the first block (programs with > 16 loads)
-        const int ts = t - imm;
-        r = (live && ts >= 0 && ts < T) ? fused_load(P.in[b], sym, ts) : P.consts[c];
-        break;
-      }
-      case BQ_F_CONST: r = P.consts[imm]; break;
-      case BQ_F_INRANGE: r = (t - imm >= 0 && t - imm < T) ? 1.0 : 0.0; break;
-      case BQ_F_ADD: r = opd(a, 0) + opd(b, 1); break;
-      case BQ_F_SUB: r = opd(a, 0) - opd(b, 1); break;
-      case BQ_F_MUL: r = opd(a, 0) * opd(b, 1); break;
-      case BQ_F_DIV: r = opd(a, 0) / opd(b, 1); break;
-      case BQ_F_FMAX: r = fmax(opd(a, 0), opd(b, 1)); break;
-      case BQ_F_FMIN: r = fmin(opd(a, 0), opd(b, 1)); break;
-      case BQ_F_MAXIMUM: {
-        const double x = opd(a, 0), y = opd(b, 1);
-        r = (x != x || y != y) ? qnan() : (x > y ? x : y);
-        break;
-      }
-      case BQ_F_MINIMUM: {
-        const double x = opd(a, 0), y = opd(b, 1);
-        r = (x != x || y != y) ? qnan() : (x < y ? x : y);
-        break;
-      }
-      case BQ_F_GT: r = opd(a, 0) > opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_GE: r = opd(a, 0) >= opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_LT: r = opd(a, 0) < opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_LE: r = opd(a, 0) <= opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_EQ: r = opd(a, 0) == opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_NE: r = opd(a, 0) != opd(b, 1) ? 1.0 : 0.0; break;
-      case BQ_F_AND: r = (opd(a, 0) != 0.0 && opd(b, 1) != 0.0) ? 1.0 : 0.0; break;
-      case BQ_F_OR: r = (opd(a, 0) != 0.0 || opd(b, 1) != 0.0) ? 1.0 : 0.0; break;
-      case BQ_F_NOT: r = opd(a, 0) != 0.0 ? 0.0 : 1.0; break;
-      case BQ_F_ABS: r = fabs(opd(a, 0)); break;
-      case BQ_F_NEG: r = -opd(a, 0); break;
-      case BQ_F_ISNAN: {
-        const double x = opd(a, 0);
-        r = x != x ? 1.0 : 0.0;
-        break;
-      }
-      case BQ_F_SQRT: r = sqrt(opd(a, 0)); break;
-      case BQ_F_LOG: r = log(opd(a, 0)); break;
-      case BQ_F_WHERE: r = opd(a, 0) != 0.0 ? opd(b, 1) : opd(c, 2); break;
-      case BQ_F_ST: {
-        if (live) {
-          const bq_fused_operand& Y = P.out[imm];
+    const uint64_t cw = P.code[pc];
+    const int op = (int)(cw & 63);
+    const int d = (int)((cw >> 6) & 0x1fff) + tid;
+    const vk x = R[slot((cw >> 19) & 0x3fff)];
+    const vk y = R[slot((cw >> 33) & 0x3fff)];
+    const vk z = R[slot((cw >> 47) & 0x3fff)];
+    vk r;
+    if (op == BQ_F_ST) {
+      const bq_fused_operand& Y = P.out[P.aux[pc]];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int t = t0 + k * NT;
+        if (t < T) {
           const int64_t off = sym * Y.stride_s + (int64_t)t * Y.stride_t;
-          const double x = reg(a);
-          if (Y.dtype == BQ_F_U8) static_cast<uint8_t*>(const_cast<void*>(Y.ptr))[off] = x != 0.0;
-          else static_cast<double*>(const_cast<void*>(Y.ptr))[off] = x;
+          if (Y.dtype == BQ_F_U8) static_cast<uint8_t*>(const_cast<void*>(Y.ptr))[off] = x[k] != 0.0;
+          else static_cast<double*>(const_cast<void*>(Y.ptr))[off] = x[k];
         }
-        continue;
       }
-      default: break;
+      continue;
+    } else if (op == BQ_F_LD) {   // a load after the block (programs with > 16 loads)
+      r = load(P.aux[pc]);
+    } else if (op == BQ_F_INRANGE) {
+      const int sh = P.aux[pc];
+#pragma unroll
+      for (int k = 0; k < K; ++k) r[k] = (t0 + k * NT - sh >= 0 && t0 + k * NT - sh < T) ? 1.0 : 0.0;
+    } else {
+      r = vec_op<K>(op, x, y, z);
     }
-    reg(d) = r;
+    R[d] = r;
   }
 }
 
 }  // namespace bq
 
 namespace {
+
+// bq_fused_program (ABI form, validated) -> the launch form for NT threads
+void translate(const bq_fused_program& P, int NT, bq::FusedLaunch& L) {
+  memset(&L, 0, sizeof(L));
+  L.n_ins = P.n_ins;
+  L.n_loads = P.n_loads;
+  L.n_const = P.n_const;
+  L.cbase = P.n_regs * NT;
+  memcpy(L.consts, P.consts, sizeof(L.consts));
+  memcpy(L.in, P.in, sizeof(L.in));
+  memcpy(L.out, P.out, sizeof(L.out));
+  auto reg_opd = [&](uint64_t r) -> uint64_t { return ((uint64_t)(r * NT) << 1) | 1ull; };
+  auto const_opd = [&](uint64_t j) -> uint64_t { return (uint64_t)(L.cbase + j) << 1; };
+  const uint64_t none = const_opd(0);   // harmless slot for unused operands
+  for (int pc = 0; pc < P.n_ins; ++pc) {
+    const uint64_t in = P.ins[pc];
+    int op = (int)(in & 0xff);
+    const uint64_t d = (in >> 8) & 0xff, a = (in >> 16) & 0xff, b = (in >> 24) & 0xff, c = (in >> 32) & 0xff;
+    const int64_t imm = (int64_t)in >> 40;
+    uint64_t A = none, B = none, C = none;
+    int32_t aux = 0;
+    switch (op) {
+      case BQ_F_LD: aux = (int32_t)((imm & 0xffff) | (int64_t)(b << 16) | (int64_t)(c << 24)); break;
+      case BQ_F_CONST: op = bq::FK_MOV; A = const_opd((uint64_t)imm); break;
+      case BQ_F_INRANGE: aux = (int32_t)imm; break;
+      case BQ_F_ST: A = reg_opd(a); aux = (int32_t)imm; break;
+      default: {
+        const uint64_t ops[3] = {a, b, c};
+        uint64_t* dst[3] = {&A, &B, &C};
+        const int n = op == BQ_F_WHERE ? 3 : (op == BQ_F_NOT || (op >= BQ_F_ABS && op <= BQ_F_LOG)) ? 1 : 2;
+        for (int k = 0; k < n; ++k) *dst[k] = ((imm >> k) & 1) ? const_opd(ops[k]) : reg_opd(ops[k]);
+      }
+    }
+    L.code[pc] = (uint64_t)op | ((uint64_t)(d * NT) << 6) | (A << 19) | (B << 33) | (C << 47);
+    L.aux[pc] = aux;
+  }
+}
 
 int arity(int op) {
   switch (op) {
@@ -170,12 +258,26 @@ int bq_fused_eval(const bq_fused_program* P, int64_t S, int64_t T, void* stream)
     if (op == BQ_F_CONST && (imm < 0 || imm >= P->n_const)) return BQ_EINVAL;
     if (op == BQ_F_ST && (imm < 0 || imm >= P->n_out)) return BQ_EINVAL;
   }
-  static_assert(sizeof(bq_fused_program) <= 4000, "the program travels as a kernel argument (4 KiB)");
   if (S == 0 || T == 0 || P->n_ins == 0) return BQ_OK;
-  const int nbt = (int)((T + FU_NT - 1) / FU_NT);
+  const int nbt = (int)((T + FU_SPAN - 1) / FU_SPAN);
   const int64_t blocks = S * nbt;
   if (blocks > 0x7fffffff) return BQ_EINVAL;
-  hipLaunchKernelGGL(fused_kernel, dim3((unsigned)blocks), dim3(FU_NT), 0, (hipStream_t)stream, *P, (int)T, nbt);
+  const size_t lds = ((size_t)P->n_regs * FU_SPAN + (size_t)(P->n_const + 1) * 2) * sizeof(double);
+  if (P->n_regs * FU_SPAN + P->n_const + 1 >= (1 << 13)) return BQ_EINVAL;   // slot field width
+  FusedLaunch L;
+  // candles per thread: more amortise the decode over more elements, but a
+  // program register costs K * 512 bytes of LDS per wave; keep >= 8 waves per
+  // CU (160 KiB), and one candle per thread on short rows (live frames of a
+  // few hundred bars) so no thread idles on the tail
+  const int K = T < 4 * FU_SPAN ? 1 : P->n_regs <= 10 ? 4 : P->n_regs <= 20 ? 2 : 1;
+  translate(*P, FU_SPAN / K, L);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 4)
+    hipLaunchKernelGGL(fused_kernel<4>, dim3((unsigned)blocks), dim3(FU_SPAN / 4), lds, st, L, (int)T, nbt);
+  else if (K == 2)
+    hipLaunchKernelGGL(fused_kernel<2>, dim3((unsigned)blocks), dim3(FU_SPAN / 2), lds, st, L, (int)T, nbt);
+  else
+    hipLaunchKernelGGL(fused_kernel<1>, dim3((unsigned)blocks), dim3(FU_SPAN), lds, st, L, (int)T, nbt);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

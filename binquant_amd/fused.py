@@ -31,6 +31,7 @@ import torch
 from . import _lib, engine
 
 _OPS = _lib.FUSED_OPS
+_TRACE = bool(__import__("os").environ.get("BQ_FUSED_TRACE"))
 NAN = float("nan")
 
 
@@ -435,7 +436,13 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
     if torch.device(dev).type != "cuda":
         raise RuntimeError("fused evaluation needs a HIP device (no CPU fallback)")
     lib = _lib.load()
-    for P in _plan(todo):
+    plans = _plan(todo)
+    if _TRACE:
+        import sys
+        for P in plans:
+            print(f"[fused] ins={len(P.ins)} loads={P.n_loads} regs={P.n_regs} in={len(P.inputs)} "
+                  f"out={len(P.outputs)} consts={len(P.consts)} S={S} T={T}", file=sys.stderr)
+    for P in plans:
         outs = []
         for name, kind in P.outputs:
             t = torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64, device=dev)
