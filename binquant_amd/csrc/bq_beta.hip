@@ -12,7 +12,7 @@
 //   corr = cov / (var_x * var_y) ** 0.5                 (roll_var, ddof 1)
 // NaN where the window is incomplete (t < window).
 //
-// One 256-thread workgroup per symbol, tiles of 1024 candles (4 per lane),
+// One 256-thread workgroup per symbol, tiles of 2048 candles (8 per lane),
 // returns staged in an LDS ring with a 128-candle halo; each lane walks its
 // window once and slides it over its 4 candles.
 #include "bq_device.h"
@@ -23,10 +23,14 @@
 namespace bq {
 
 constexpr int BC_NT = 256;
-constexpr int BC_K = 4;
+constexpr int BC_K = 8;
 constexpr int BC_TT = BC_NT * BC_K;
 constexpr int BC_H = 128;
 constexpr int BC_R = BC_H + BC_TT;
+// LDS index skew: one pad double every 32, so the lanes' stride-4 window
+// walks (lane i at 4i + j) spread over all bank pairs instead of 8
+__device__ __forceinline__ int bsk(int p) { return p + (p >> 5); }
+constexpr int BC_RS = BC_R + (BC_R >> 5) + 1;
 
 struct BetaArgs {
   const double* close;   // PAIRS: symbol returns
@@ -46,15 +50,15 @@ __device__ __forceinline__ double log_return(double c, double p) { return log(c 
 // (bq_join_returns), first full window at t = w - 1.
 template <bool PAIRS>
 __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
-  __shared__ double sX[BC_R], sY[BC_R];
+  __shared__ double sX[BC_RS], sY[BC_RS];
   const int tid = threadIdx.x;
   const int64_t sym = blockIdx.x;
   const double* __restrict__ rc = A.close + sym * A.ld_in;
   const double* __restrict__ rb = PAIRS ? A.btc + sym * A.ld_in : A.btc;
   const int T = A.T, w = A.win;
   if (tid < BC_H) {
-    sX[tid] = qnan();
-    sY[tid] = qnan();
+    sX[bsk(tid)] = qnan();
+    sY[bsk(tid)] = qnan();
   }
   __syncthreads();
   for (int t0 = 0; t0 < T; t0 += BC_TT) {
@@ -74,8 +78,8 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
           x[k] = log_return(c, pc);   // NaN at candle 0 (dropna)
           y[k] = log_return(b, pbt);
         }
-        sX[pb + k] = x[k];
-        sY[pb + k] = y[k];
+        sX[bsk(pb + k)] = x[k];
+        sY[bsk(pb + k)] = y[k];
         pc = c;
         pbt = b;
       }
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
         pxy = xy;
       };
       for (int i = pb - w + 1; i <= pb; ++i) {
-        const double xi = sX[i], yi = sY[i];
+        const double xi = sX[bsk(i)], yi = sY[bsk(i)];
         if (xi == xi && yi == yi) add(xi, yi, 1.0);
         track(xi, yi);
       }
@@ -117,7 +121,7 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
       for (int k = 0; k < BC_K; ++k) {
         const int t = tb + k, p = pb + k;
         if (k > 0) {
-          const double xo = sX[p - w], yo = sY[p - w];
+          const double xo = sX[bsk(p - w)], yo = sY[bsk(p - w)];
           if (xo == xo && yo == yo) add(xo, yo, -1.0);
           add(x[k], y[k], 1.0);
           track(x[k], y[k]);
@@ -152,8 +156,8 @@ __global__ __launch_bounds__(BC_NT) void beta_corr_kernel(const BetaArgs A) {
     if (pb >= BC_TT) {   // owners of [TT, R) become the next tile's halo
 #pragma unroll
       for (int k = 0; k < BC_K; ++k) {
-        sX[pb + k - BC_TT] = x[k];
-        sY[pb + k - BC_TT] = y[k];
+        sX[bsk(pb + k - BC_TT)] = x[k];
+        sY[bsk(pb + k - BC_TT)] = y[k];
       }
     }
   }
