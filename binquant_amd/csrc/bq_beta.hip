@@ -14,7 +14,7 @@
 //
 // One 256-thread workgroup per symbol, tiles of 2048 candles (8 per lane),
 // returns staged in an LDS ring with a 128-candle halo; each lane walks its
-// window once and slides it over its 4 candles.
+// window once and slides it over its 8 candles.
 #include "bq_device.h"
 #include "binquant_amd.h"
 
