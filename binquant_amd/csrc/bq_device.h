@@ -220,15 +220,24 @@ __device__ __forceinline__ double sqrt_nr(double v) {
 // writes and the per-lane reads free of bank conflicts for 8-byte elements.
 constexpr int STG_PITCH = WAVE + 2;
 
+// 64-bit payload type of __builtin_amdgcn_raw_buffer_store_b64
+typedef unsigned int bq_u32x2 __attribute__((__vector_size__(8)));
+
 template <int CT>
 __device__ __forceinline__ void stage_load(const double* __restrict__ base, int64_t ld, int64_t sym0, int64_t S,
                                            int t0, int T, int lane, double (&r)[CT]) {
+  // every lane loads a clamped, valid address (S, T >= 1) and selects NaN
+  // outside the panel: no branch around a load, so the waits for a
+  // prefetched chunk stay counted (vmcnt(N)) instead of draining the stores
 #pragma unroll
   for (int k = 0; k < CT; ++k) {
     const int e = lane + WAVE * k;
     const int64_t s = sym0 + e / CT;
     const int t = t0 + e % CT;
-    r[k] = (s < S && t >= 0 && t < T) ? base[s * ld + t] : qnan();
+    const int64_t sc = s < S ? s : S - 1;
+    const int tc = t < 0 ? 0 : t < T ? t : T - 1;
+    const double v = base[sc * ld + tc];
+    r[k] = (s < S && t >= 0 && t < T) ? v : qnan();
   }
 }
 
@@ -242,15 +251,29 @@ __device__ __forceinline__ void stage_put(double* lds, int lane, const double (&
 }
 
 // LDS [CT][PITCH] (written by lane = symbol) -> [S][ld] rows, coalesced.
+// Buffer stores issued by every lane through a per-wave descriptor over the
+// wave's rows: elements outside the panel (and every element when base is
+// null) get an offset past the range, which the hardware drops — no branch
+// around a store, so later waits stay counted. Host: 64 * ld * 8 < 2^31.
 template <int CT, typename OutT>
 __device__ __forceinline__ void stage_store(const double* lds, OutT* __restrict__ base, int64_t ld, int64_t sym0,
                                             int64_t S, int t0, int T, int lane) {
+  const int64_t rows = S - sym0 < WAVE ? S - sym0 : WAVE;
+  const int nbytes = base ? (int)(rows * ld * (int64_t)sizeof(OutT)) : 0;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base ? base + sym0 * ld : nullptr, 0, nbytes, 0x00020000);
 #pragma unroll
   for (int k = 0; k < CT; ++k) {
     const int e = lane + WAVE * k;
-    const int64_t s = sym0 + e / CT;
+    const int r = e / CT;
     const int t = t0 + e % CT;
-    if (s < S && t < T) base[s * ld + t] = (OutT)lds[(e % CT) * STG_PITCH + e / CT];
+    const bool ok = r < rows && t < T;
+    const unsigned off = ok ? (unsigned)(((int64_t)r * ld + t) * (int64_t)sizeof(OutT)) : (unsigned)nbytes;
+    const double v = lds[(e % CT) * STG_PITCH + r];
+    if constexpr (sizeof(OutT) == 1)
+      __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(OutT)v, rs, off, 0, 0);
+    else
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bq_u32x2, (double)(OutT)v), rs, off, 0, 0);
   }
 }
 

@@ -137,9 +137,14 @@ __global__ __launch_bounds__(FU_SPAN / K) void fused_kernel(const FusedLaunch P,
     const uint64_t cw = P.code[pc];
     const int op = (int)(cw & 63);
     const int d = (int)((cw >> 6) & 0x1fff) + tid;
+    // only the operands the op reads (arity in bits 61-62; wave-uniform
+    // branch): the interpreter is LDS-bandwidth bound, and a unary or binary
+    // op no longer pays for three operand reads
+    const int na = (int)(cw >> 61) & 3;
     const vk x = R[slot((cw >> 19) & 0x3fff)];
-    const vk y = R[slot((cw >> 33) & 0x3fff)];
-    const vk z = R[slot((cw >> 47) & 0x3fff)];
+    vk y = x, z = x;
+    if (na >= 2) y = R[slot((cw >> 33) & 0x3fff)];
+    if (na >= 3) z = R[slot((cw >> 47) & 0x3fff)];
     vk r;
     if (op == BQ_F_ST) {
       const bq_fused_operand& Y = P.out[P.aux[pc]];
@@ -169,6 +174,8 @@ __global__ __launch_bounds__(FU_SPAN / K) void fused_kernel(const FusedLaunch P,
 }  // namespace bq
 
 namespace {
+
+int arity(int op);
 
 // bq_fused_program (ABI form, validated) -> the launch form for NT threads
 void translate(const bq_fused_program& P, int NT, bq::FusedLaunch& L) {
@@ -202,7 +209,8 @@ void translate(const bq_fused_program& P, int NT, bq::FusedLaunch& L) {
         for (int k = 0; k < n; ++k) *dst[k] = ((imm >> k) & 1) ? const_opd(ops[k]) : reg_opd(ops[k]);
       }
     }
-    L.code[pc] = (uint64_t)op | ((uint64_t)(d * NT) << 6) | (A << 19) | (B << 33) | (C << 47);
+    const uint64_t na = op == bq::FK_MOV ? 1 : (uint64_t)arity(op);
+    L.code[pc] = (uint64_t)op | ((uint64_t)(d * NT) << 6) | (A << 19) | (B << 33) | (C << 47) | (na << 61);
     L.aux[pc] = aux;
   }
 }

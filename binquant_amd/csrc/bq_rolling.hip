@@ -272,63 +272,148 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
   }
 }
 
-// Same replay with a fixed 2-tile LDS footprint (16.9 KB per wave instead of
+// Same replay with a fixed 2-tile LDS footprint (≈17 KB per wave instead of
 // the ring's ceil((w + shift) / 16) + 1 tiles, up to 59 KB at w = 80): the
 // leaving values are staged from the input again (chunk t0 - shift - w, an
 // L2 / MALL hit: it was read w candles earlier), so up to 9 waves per CU fit
 // instead of 2-6. Costs one more read of the input (from cache).
-// CLS: 0 = ewm, 1 = Kahan sum / mean, 2 = Welford var / std — the body is
-// specialised per class (shorter dependent chain per step, and a per-class
-// launch keeps the registers to that class's state: 107 / 166 / 186 VGPRs).
-template <int CLS>
+// CLS: 0 = ewm, 1 = Kahan sum / mean, 2 = Welford var / std, 3 = ffill — the
+// body is specialised per class (shorter dependent chain per step, and a
+// per-class launch keeps the registers to that class's state).
+// SPW: symbols per wave (64; 32, 16, 8 for measurement). With SPW < 64 the
+// same rows spread over 64/SPW times as many waves (lanes >= SPW only help
+// stage; each chunk is RP_ELEMS / SPW candles long). Measured: no faster —
+// a 12.5k-symbol replay (196 waves) costs ~600 cycles per step in the wave's
+// own ~100-instruction stream (NaN guards, the same-value rule, the IEEE
+// divide of the mean), not in a shortage of waves.
+constexpr int RP_ELEMS = RP_CT * WAVE;   // staged values per wave and chunk
+
+template <int SPW>
+struct ReplayTile {
+  static constexpr int CT = RP_ELEMS / SPW;   // candles per chunk
+  static constexpr int P = SPW + 2;           // LDS pitch (doubles) of one candle's row
+  static constexpr int N = CT * P;
+  // [SPW symbols][CT candles] of rows sym0.. from column t0, read so that
+  // consecutive lanes read consecutive candles of one row
+  __device__ __forceinline__ static void load(const double* __restrict__ base, int64_t ld, int64_t sym0, int64_t S,
+                                              int t0, int T, int lane, double (&r)[RP_CT]) {
+// Every lane loads (a clamped, valid address) and selects NaN outside the
+  // panel: no branch around a load, so no load forces a full vmcnt drain.
+#pragma unroll
+    for (int k = 0; k < RP_CT; ++k) {
+      const int e = lane + WAVE * k;
+      const int64_t s = sym0 + e / CT;
+      const int t = t0 + e % CT;
+      const int64_t sc = s < S ? s : S - 1;
+      const int tc = t < 0 ? 0 : t < T ? t : T - 1;
+      const double v = base[sc * ld + tc];
+      r[k] = (s < S && t >= 0 && t < T) ? v : qnan();
+    }
+  }
+  // transposed into LDS: lds[candle * P + symbol]
+  __device__ __forceinline__ static void put(double* lds, int lane, const double (&r)[RP_CT]) {
+#pragma unroll
+    for (int k = 0; k < RP_CT; ++k) {
+      const int e = lane + WAVE * k;
+      lds[(e % CT) * P + e / CT] = r[k];
+    }
+  }
+};
+
+// Results leave through one buffer store per step, issued by every lane:
+// rows past S and lanes >= SPW get an offset past the descriptor's range,
+// which the hardware drops. Unconditional stores keep the loop's waits
+// counted (vmcnt(N) for the prefetched chunk) instead of draining every
+// outstanding result store at each chunk boundary (gfx950's vmcnt counts
+// loads and stores alike). Host guarantees 64 * ld_out * 8 < 2^31 (job_ok).
+template <int CLS, int SPW>
 __device__ __forceinline__ void replay_restage_body(const RollJob& A, const RollBatch& B, double* s_in,
                                                     double* s_out) {
+  using Tl = ReplayTile<SPW>;
+  constexpr int CT = Tl::CT;
   constexpr bool FFILL = CLS == 3;
   constexpr bool EWM = CLS == 0 || FFILL;   // no leaving value
   constexpr bool welford = CLS == 2;
   const int lane = threadIdx.x;
-  const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
+  const int64_t sym0 = (int64_t)blockIdx.x * SPW;
   const int64_t S = B.S;
   const int T = B.T, w = A.win, sh = A.shift;
-  const bool live = sym0 + lane < S;
-  double* __restrict__ orow = A.out + (live ? sym0 + lane : 0) * A.ld_out;
+  const int64_t rows = S - sym0 < SPW ? S - sym0 : SPW;
+  const int nbytes = (int)(rows * A.ld_out * (int64_t)sizeof(double));
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(A.out + sym0 * A.ld_out, 0, nbytes, 0x00020000);
+  const bool live = lane < rows;
+  const unsigned obase = live ? (unsigned)(lane * A.ld_out * (int64_t)sizeof(double)) : (unsigned)nbytes;
+  const int rl = lane < SPW ? lane : SPW - 1;   // lanes >= SPW replay a copy (stores dropped)
   double ri[RP_CT], ro[RP_CT];
-  stage_load<RP_CT>(A.x, A.ld_in, sym0, S, -sh, T, lane, ri);
-  if (!EWM) stage_load<RP_CT>(A.x, A.ld_in, sym0, S, -sh - w, T, lane, ro);
+  Tl::load(A.x, A.ld_in, sym0, S, -sh, T, lane, ri);
+  if (!EWM) Tl::load(A.x, A.ld_in, sym0, S, -sh - w, T, lane, ro);
   ReplayLane st;
   st.init();
-  for (int t0 = 0; t0 < T; t0 += RP_CT) {
-    stage_put<RP_CT>(s_in, lane, ri);
-    if (!EWM) stage_put<RP_CT>(s_out, lane, ro);
-    __syncthreads();
-    if (t0 + RP_CT < T) {   // next chunks in flight during this one's replay
-      stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT - sh, T, lane, ri);
-      if (!EWM) stage_load<RP_CT>(A.x, A.ld_in, sym0, S, t0 + RP_CT - sh - w, T, lane, ro);
-    }
-    auto step = [&](int j) {
-      const int t = t0 + j;
-      const double v_in = s_in[j * STG_PITCH + lane];
-      const double v_out = EWM ? 0.0 : s_out[j * STG_PITCH + lane];
-      const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL);
-      if (live) orow[t] = res;
-    };
-    if (t0 + RP_CT <= T) {
+  auto step = [&](int t, double v_in, double v_out) {
+    const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bq_u32x2, res), orsrc,
+                                          obase + (unsigned)t * (unsigned)sizeof(double), 0, 0);
+  };
+  // 16 steps at a time: their LDS operands are read into registers first, so
+  // no LDS latency sits between two dependent state updates
+  constexpr int G = 16;
+  auto steps16 = [&](int t0, int g) {
+    double vi[G], vo[G];
 #pragma unroll
-      for (int j = 0; j < RP_CT; ++j) step(j);
-    } else {
-      for (int j = 0; j < T - t0; ++j) step(j);
+    for (int k = 0; k < G; ++k) {
+      vi[k] = s_in[(g + k) * Tl::P + rl];
+      vo[k] = EWM ? 0.0 : s_out[(g + k) * Tl::P + rl];
     }
+#pragma unroll
+    for (int k = 0; k < G; ++k) step(t0 + g + k, vi[k], vo[k]);
+  };
+  const int tfull = T - T % CT;
+  int t0 = 0;
+  for (; t0 < tfull; t0 += CT) {
+    Tl::put(s_in, lane, ri);
+    if (!EWM) Tl::put(s_out, lane, ro);
+    __syncthreads();
+    // next chunks in flight during this one's replay (past T: NaN, unused)
+    Tl::load(A.x, A.ld_in, sym0, S, t0 + CT - sh, T, lane, ri);
+    if (!EWM) Tl::load(A.x, A.ld_in, sym0, S, t0 + CT - sh - w, T, lane, ro);
+#pragma unroll 1
+    for (int g = 0; g < CT; g += G) steps16(t0, g);
     __syncthreads();   // both tiles are rewritten by the next chunk
+  }
+  if (t0 < T) {   // tail chunk
+    Tl::put(s_in, lane, ri);
+    if (!EWM) Tl::put(s_out, lane, ro);
+    __syncthreads();
+    for (int j = 0; j < T - t0; ++j) step(t0 + j, s_in[j * Tl::P + rl], EWM ? 0.0 : s_out[j * Tl::P + rl]);
   }
 }
 
-
 // every job of the batch is of class CLS
-template <int CLS>
+// (the job is copied out of the kernel arguments once: read through a
+// reference, its fields are re-loaded from memory at every step)
+template <int CLS, int SPW>
 __global__ __launch_bounds__(WAVE) void replay_restage_kernel(const RollBatch B) {
-  __shared__ double s_in[RP_CT * STG_PITCH];
-  __shared__ double s_out[RP_CT * STG_PITCH];
-  replay_restage_body<CLS>(B.j[blockIdx.y], B, s_in, s_out);
+  __shared__ double s_in[ReplayTile<SPW>::N];
+  __shared__ double s_out[ReplayTile<SPW>::N];
+  const RollJob A = B.j[blockIdx.y];
+  replay_restage_body<CLS, SPW>(A, B, s_in, s_out);
+}
+
+// jobs of any class in one launch (wave-uniform switch on the job's class):
+// for batches that do not fill the chip, where per-class launches would run
+// one latency-bound replay after the other
+template <int SPW>
+__global__ __launch_bounds__(WAVE) void replay_mixed_kernel(const RollBatch B) {
+  __shared__ double s_in[ReplayTile<SPW>::N];
+  __shared__ double s_out[ReplayTile<SPW>::N];
+  const RollJob A = B.j[blockIdx.y];
+  switch (replay_class(A.mode)) {
+    case 0: replay_restage_body<0, SPW>(A, B, s_in, s_out); break;
+    case 1: replay_restage_body<1, SPW>(A, B, s_in, s_out); break;
+    case 2: replay_restage_body<2, SPW>(A, B, s_in, s_out); break;
+    default: replay_restage_body<3, SPW>(A, B, s_in, s_out);
+  }
 }
 
 // ---- rank kernels (lane = symbol x segment, sorted window in registers) -----------
@@ -625,6 +710,8 @@ namespace {
 
 bool job_ok(const bq_roll_job& j, int64_t T) {
   if (!j.x || !j.out || j.ld_in < T || j.ld_out < T || j.min_periods < 0) return false;
+  // replay results leave through 32-bit buffer offsets over 64 rows
+  if (j.ld_out > BQ_MAX_ROLL_LD) return false;
   if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
   if (j.mode == BQ_ROLL_FFILL) return j.shift == 0;
   return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
@@ -648,18 +735,61 @@ void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
-// which replay kernel: 0 = LDS ring over the window, 1 = re-staged leaving
-// values (fixed LDS). BQ_REPLAY_IMPL=ring|restage forces one (measurement).
-int replay_impl(int nclasses, int64_t waves_per_job) {
+// which replay kernel: 0 = LDS ring over the window (one launch, 64 symbols
+// per wave), 1 = re-staged leaving values, one launch per class, 2 = re-staged,
+// all classes in one launch. BQ_REPLAY_IMPL=ring|restage|mixed forces one
+// (measurement; all give identical outputs).
+int replay_impl(int nclasses, int64_t waves64) {
   static const int forced = [] {
     const char* e = getenv("BQ_REPLAY_IMPL");
-    return !e ? -1 : (strcmp(e, "ring") == 0 ? 0 : strcmp(e, "restage") == 0 ? 1 : -1);
+    return !e ? -1
+              : (strcmp(e, "ring") == 0      ? 0
+                 : strcmp(e, "restage") == 0 ? 1
+                 : strcmp(e, "mixed") == 0   ? 2
+                                             : -1);
   }();
   if (forced >= 0) return forced;
-  // mixed classes on <= 4096 symbols: the one-launch ring kernel (1000 x 400:
-  // 8 jobs 0.26 vs 0.34 ms); on 12.5k symbols the per-class launches win
-  // (16 jobs 4.5 vs 3.1 ms)
-  return nclasses > 1 && waves_per_job <= 64 ? 0 : 1;
+  // mixed classes: one launch (measured, tools/replay_ab.sh, identical
+  // digests: 1000 x 400 batch16 0.18 vs 0.33 ms per class; 12.5k x 2k
+  // batch16 2.69 vs 2.87 ms — the classes' replays overlap instead of
+  // running one after the other)
+  (void)waves64;
+  return nclasses > 1 ? 2 : 1;
+}
+
+// symbols per wave of the re-staged replays: 64. BQ_REPLAY_SPW=32|16|8
+// forces fewer (measurement: spreading 12.5k symbols over 2-8x as many
+// waves did not shorten the replay — the step cost is the wave's own
+// instruction stream, not a shortage of waves — tools/replay_ab.sh).
+int replay_spw() {
+  static const int forced = [] {
+    const char* e = getenv("BQ_REPLAY_SPW");
+    const int v = e ? atoi(e) : 0;
+    return (v == 32 || v == 16 || v == 8) ? v : 64;
+  }();
+  return forced;
+}
+
+template <int SPW>
+void launch_restage(int cls, const bq::RollBatch& B, int n, hipStream_t st) {
+  const dim3 grid((unsigned)((B.S + SPW - 1) / SPW), (unsigned)n);
+  switch (cls) {
+    case 0: hipLaunchKernelGGL((bq::replay_restage_kernel<0, SPW>), grid, dim3(bq::WAVE), 0, st, B); break;
+    case 1: hipLaunchKernelGGL((bq::replay_restage_kernel<1, SPW>), grid, dim3(bq::WAVE), 0, st, B); break;
+    case 2: hipLaunchKernelGGL((bq::replay_restage_kernel<2, SPW>), grid, dim3(bq::WAVE), 0, st, B); break;
+    case 3: hipLaunchKernelGGL((bq::replay_restage_kernel<3, SPW>), grid, dim3(bq::WAVE), 0, st, B); break;
+    default: hipLaunchKernelGGL((bq::replay_mixed_kernel<SPW>), grid, dim3(bq::WAVE), 0, st, B);
+  }
+}
+
+// cls 0-3: one class; 4: mixed
+void launch_restage_any(int cls, const bq::RollBatch& B, int n, hipStream_t st) {
+  switch (replay_spw()) {
+    case 64: launch_restage<64>(cls, B, n, st); break;
+    case 32: launch_restage<32>(cls, B, n, st); break;
+    case 16: launch_restage<16>(cls, B, n, st); break;
+    default: launch_restage<8>(cls, B, n, st);
+  }
 }
 
 // which order-statistic kernel: 0 = lane (sorted window per lane), 1 = tile
@@ -716,14 +846,14 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
         hipFuncSetAttribute((const void*)replay_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==
         hipSuccess;
     (void)lds_opt_in;
-    // few waves (live shapes) with mixed classes: per-class launches would
-    // run one after the other, each latency-bound, so the ring kernel takes
-    // the whole batch in one launch; otherwise the class-specialised
-    // re-staging kernels (measured: tools/replay_ab.py, identical outputs)
+    // re-staging kernels: class-specialised when the batch has one class,
+    // the mixed kernel otherwise (the LDS ring kernel only when forced;
+    // measured: tools/replay_ab.sh, identical outputs)
     int ncls[4] = {0, 0, 0, 0};
     for (int i = 0; i < nrep; ++i) ++ncls[replay_class(rep.j[i].mode)];
     const int nclasses = (ncls[0] > 0) + (ncls[1] > 0) + (ncls[2] > 0) + (ncls[3] > 0);
-    if (replay_impl(nclasses, (S + WAVE - 1) / WAVE)) {
+    const int impl = replay_impl(nclasses, ((S + WAVE - 1) / WAVE) * nrep);
+    if (impl == 1) {
       RollBatch cls[4];
       for (int c = 0; c < 4; ++c) {
         memset(&cls[c], 0, sizeof(RollBatch));
@@ -735,11 +865,10 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
         const int c = replay_class(rep.j[i].mode);
         cls[c].j[ncls[c]++] = rep.j[i];
       }
-      const unsigned gx = (unsigned)((S + WAVE - 1) / WAVE);
-      if (ncls[0]) hipLaunchKernelGGL(replay_restage_kernel<0>, dim3(gx, (unsigned)ncls[0]), dim3(WAVE), 0, st, cls[0]);
-      if (ncls[1]) hipLaunchKernelGGL(replay_restage_kernel<1>, dim3(gx, (unsigned)ncls[1]), dim3(WAVE), 0, st, cls[1]);
-      if (ncls[2]) hipLaunchKernelGGL(replay_restage_kernel<2>, dim3(gx, (unsigned)ncls[2]), dim3(WAVE), 0, st, cls[2]);
-      if (ncls[3]) hipLaunchKernelGGL(replay_restage_kernel<3>, dim3(gx, (unsigned)ncls[3]), dim3(WAVE), 0, st, cls[3]);
+      for (int c = 0; c < 4; ++c)
+        if (ncls[c]) launch_restage_any(c, cls[c], ncls[c], st);
+    } else if (impl == 2) {
+      launch_restage_any(4, rep, nrep, st);
     } else {
       hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
                          rep, ring);

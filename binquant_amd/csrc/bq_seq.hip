@@ -52,12 +52,12 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
     stage_put<ST_CT>(sX[2], lane, rc);
     stage_put<ST_CT>(sX[3], lane, ra);
     __syncthreads();
-    if (t0 + ST_CT < T) {   // prefetch the next chunk
-      stage_load<ST_CT>(A.h, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rh);
-      stage_load<ST_CT>(A.l, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rl);
-      stage_load<ST_CT>(A.c, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rc);
-      stage_load<ST_CT>(A.atr, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, ra);
-    }
+    // prefetch the next chunk (unconditional: past T the clamped loads give
+    // NaN that is never used; no branch keeps the loop's waits counted)
+    stage_load<ST_CT>(A.h, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rh);
+    stage_load<ST_CT>(A.l, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rl);
+    stage_load<ST_CT>(A.c, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rc);
+    stage_load<ST_CT>(A.atr, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, ra);
     const int n = min(ST_CT, T - t0);
     for (int j = 0; j < n; ++j) {
       const int i = j * STG_PITCH + lane;
@@ -79,8 +79,8 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
       sX[2][i] = up ? 1.0 : 0.0;
     }
     __syncthreads();
-    if (A.upper) stage_store<ST_CT>(sX[0], A.upper, A.ld_out, sym0, A.S, t0, T, lane);
-    if (A.lower) stage_store<ST_CT>(sX[1], A.lower, A.ld_out, sym0, A.S, t0, T, lane);
+    stage_store<ST_CT>(sX[0], A.upper, A.ld_out, sym0, A.S, t0, T, lane);   // null: dropped
+    stage_store<ST_CT>(sX[1], A.lower, A.ld_out, sym0, A.S, t0, T, lane);
     stage_store<ST_CT>(sX[2], A.up, A.ld_out, sym0, A.S, t0, T, lane);
     __syncthreads();
   }
@@ -93,6 +93,7 @@ extern "C" int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, in
   using namespace bq;
   if (!hlca || !up || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff || !(multiplier == multiplier))
     return BQ_EINVAL;
+  if (ld_out > BQ_MAX_ROLL_LD) return BQ_EINVAL;   // 32-bit buffer offsets over a wave's 64 rows
   for (int i = 0; i < 4; ++i)
     if (!hlca[i]) return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;

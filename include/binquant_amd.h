@@ -225,8 +225,10 @@ enum bq_roll_mode {
  * window sums to 0 when min_periods is 0). Replaces the
  * pandas rolling calls of strategies/activity_burst_pump.py:58-63,134-152,
  * strategies/liquidation_sweep_pump.py:218-245, strategies/failed_spike_fade.py:376-378.
- * x, out [S][ld] fp64 device pointers; window <= BQ_MAX_ROLLING_WINDOW.
+ * x, out [S][ld] fp64 device pointers; window <= BQ_MAX_ROLLING_WINDOW;
+ * ld_out <= BQ_MAX_ROLL_LD (else BQ_EINVAL).
  */
+#define BQ_MAX_ROLL_LD 4194303   /* 64 rows x ld_out x 8 B < 2^31 (32-bit buffer offsets) */
 int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream);
 

@@ -1,5 +1,5 @@
 """Run one strategy pipeline a few times (for rocprofv3 kernel breakdowns).
-Usage: python tools/pipeline_run.py <activity_burst|pump_score|failed_spike|top_gainer|adx> [S] [T]"""
+Usage: python tools/pipeline_run.py <activity_burst|pump_score|failed_spike|top_gainer|adx|zscore|wilder_rsi> [S] [T]"""
 import os
 import sys
 
@@ -21,6 +21,8 @@ fn = {
     "failed_spike": lambda: strategies.failed_spike_features(o, h, l, c, v, qv),
     "top_gainer": lambda: signals.top_gainer_features(o, h, l, c, v, qv),
     "adx": lambda: signals.adx(h, l, c),
+    "zscore": lambda: signals.zscore(c),
+    "wilder_rsi": lambda: signals.wilder_rsi(c),
 }[name]
 for _ in range(3):
     fn()

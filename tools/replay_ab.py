@@ -14,7 +14,7 @@ from binquant_amd import engine
 from binquant_amd.engine import Ewm, Roll
 from binquant_amd.synth import device_panel
 
-impl = os.environ.get("BQ_REPLAY_IMPL", "auto")
+impl = os.environ.get("BQ_REPLAY_IMPL", "auto") + os.environ.get("BQ_REPLAY_SPW", "")
 for S, T, reps in ((1000, 400, 50), (12_500, 2_000, 10)):
     p = device_panel(S, T, seed=5)
     x = p["volume"].clone()
