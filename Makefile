@@ -14,7 +14,7 @@ LIB       := binquant_amd/lib/libbinquant_amd.so
 
 all: $(LIB)
 
-build/%.o: binquant_amd/csrc/%.hip binquant_amd/csrc/bq_device.h include/binquant_amd.h
+build/%.o: binquant_amd/csrc/%.hip binquant_amd/csrc/bq_device.h binquant_amd/csrc/bq_fused_jit.h include/binquant_amd.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -25,7 +25,7 @@ build/%.o: binquant_amd/csrc/%.cpp include/binquant_amd.h
 
 $(LIB): $(OBJS)
 	@mkdir -p binquant_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lhiprtc
 
 resource-usage: $(SRCS)
 	@for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "remark" ; done

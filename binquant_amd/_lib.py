@@ -207,6 +207,11 @@ SIGNATURES: dict[str, tuple] = {
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
     "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
     "bq_fused_eval": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), _I64, _I64, _P]),
+    "bq_fused_set_native": (ctypes.c_int, [_I32]),
+    "bq_fused_set_cache_dir": (ctypes.c_int, [ctypes.c_char_p]),
+    "bq_fused_source": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), ctypes.c_char_p, _I64, ctypes.POINTER(_I64)]),
+    "bq_fused_compile": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram)]),
+    "bq_fused_stats": (ctypes.c_int, [ctypes.POINTER(_I64)] * 3),
     "bq_micro_regime": (ctypes.c_int, [_I64] + [_P] * 13 + [_P]),
     "bq_context_score": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.POINTER(BqContextScalars),
                                         ctypes.POINTER(BqScorerWeights), _P, _I64, _P]),
@@ -238,6 +243,14 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # compiled fused programs persist next to the library (bq_fused_jit.hip)
+    cache = os.environ.get("BQ_FUSED_CACHE", str(p.parent / "fused_cache"))
+    if cache:
+        try:
+            os.makedirs(cache, exist_ok=True)
+            lib.bq_fused_set_cache_dir(cache.encode())
+        except OSError:
+            pass   # read-only tree: the per-process cache still applies
     if path is None:
         _lib = lib
     return lib

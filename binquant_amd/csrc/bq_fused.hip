@@ -16,6 +16,7 @@
 // Constant operands are read from the kernarg table directly (no register).
 #include "bq_device.h"
 #include "binquant_amd.h"
+#include "bq_fused_jit.h"
 
 #include <string.h>
 
@@ -231,42 +232,52 @@ bool operand_ok(const bq_fused_operand& X) {
 
 }  // namespace
 
-extern "C" {
+namespace bq {
 
-int bq_fused_eval(const bq_fused_program* P, int64_t S, int64_t T, void* stream) {
-  using namespace bq;
-  if (!P || S < 0 || T < 0 || T > 0x7fffffff) return BQ_EINVAL;
-  if (P->n_ins < 0 || P->n_ins > BQ_FUSED_MAX_INS || P->n_loads < 0 || P->n_loads > BQ_FUSED_MAX_LOADS ||
-      P->n_loads > P->n_ins || P->n_regs < 0 || P->n_regs > BQ_FUSED_MAX_REGS || P->n_in < 0 ||
-      P->n_in > BQ_FUSED_MAX_IN || P->n_out < 0 || P->n_out > BQ_FUSED_MAX_OUT || P->n_const < 0 ||
-      P->n_const > BQ_FUSED_MAX_CONST)
+int fused_validate(const bq_fused_program& P) {
+  if (P.n_ins < 0 || P.n_ins > BQ_FUSED_MAX_INS || P.n_loads < 0 || P.n_loads > BQ_FUSED_MAX_LOADS ||
+      P.n_loads > P.n_ins || P.n_regs < 0 || P.n_regs > BQ_FUSED_MAX_REGS || P.n_in < 0 ||
+      P.n_in > BQ_FUSED_MAX_IN || P.n_out < 0 || P.n_out > BQ_FUSED_MAX_OUT || P.n_const < 0 ||
+      P.n_const > BQ_FUSED_MAX_CONST)
     return BQ_EINVAL;
-  for (int i = 0; i < P->n_in; ++i)
-    if (!operand_ok(P->in[i])) return BQ_EINVAL;
-  for (int i = 0; i < P->n_out; ++i)
-    if (!operand_ok(P->out[i])) return BQ_EINVAL;
-  for (int pc = 0; pc < P->n_ins; ++pc) {
-    const uint64_t in = P->ins[pc];
+  for (int i = 0; i < P.n_in; ++i)
+    if (!operand_ok(P.in[i])) return BQ_EINVAL;
+  for (int i = 0; i < P.n_out; ++i)
+    if (!operand_ok(P.out[i])) return BQ_EINVAL;
+  for (int pc = 0; pc < P.n_ins; ++pc) {
+    const uint64_t in = P.ins[pc];
     const int op = (int)(in & 0xff);
     const int d = (int)((in >> 8) & 0xff), a = (int)((in >> 16) & 0xff), b = (int)((in >> 24) & 0xff),
               c = (int)((in >> 32) & 0xff);
     const int64_t imm = (int64_t)in >> 40;
     if (op < BQ_F_LD || op > BQ_F_ST) return BQ_EINVAL;
-    if (pc < P->n_loads && op != BQ_F_LD) return BQ_EINVAL;   // the load block comes first
-    if (op != BQ_F_ST && d >= P->n_regs) return BQ_EINVAL;
+    if (pc < P.n_loads && op != BQ_F_LD) return BQ_EINVAL;   // the load block comes first
+    if (op != BQ_F_ST && d >= P.n_regs) return BQ_EINVAL;
     const int n = arity(op);
     const bool imm_op = op == BQ_F_LD || op == BQ_F_CONST || op == BQ_F_INRANGE || op == BQ_F_ST;
     const int idx[3] = {a, b, c};
     for (int k = 0; k < n; ++k) {
       const bool is_const = !imm_op && ((imm >> k) & 1);
-      if (idx[k] >= (is_const ? P->n_const : P->n_regs)) return BQ_EINVAL;
+      if (idx[k] >= (is_const ? P.n_const : P.n_regs)) return BQ_EINVAL;
     }
     if (!imm_op && (imm >> n) != 0) return BQ_EINVAL;   // flags only for the operands used
-    if (op == BQ_F_LD && (b >= P->n_in || c >= P->n_const)) return BQ_EINVAL;
-    if (op == BQ_F_CONST && (imm < 0 || imm >= P->n_const)) return BQ_EINVAL;
-    if (op == BQ_F_ST && (imm < 0 || imm >= P->n_out)) return BQ_EINVAL;
+    if (op == BQ_F_LD && (b >= P.n_in || c >= P.n_const)) return BQ_EINVAL;
+    if (op == BQ_F_CONST && (imm < 0 || imm >= P.n_const)) return BQ_EINVAL;
+    if (op == BQ_F_ST && (imm < 0 || imm >= P.n_out)) return BQ_EINVAL;
   }
+  return BQ_OK;
+}
+
+}  // namespace bq
+
+extern "C" {
+
+int bq_fused_eval(const bq_fused_program* P, int64_t S, int64_t T, void* stream) {
+  using namespace bq;
+  if (!P || S < 0 || T < 0 || T > 0x7fffffff) return BQ_EINVAL;
+  if (fused_validate(*P) != BQ_OK) return BQ_EINVAL;
   if (S == 0 || T == 0 || P->n_ins == 0) return BQ_OK;
+  if (fused_native_enabled()) return fused_native_eval(*P, S, T, (hipStream_t)stream);
   const int nbt = (int)((T + FU_SPAN - 1) / FU_SPAN);
   const int64_t blocks = S * nbt;
   if (blocks > 0x7fffffff) return BQ_EINVAL;

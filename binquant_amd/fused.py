@@ -395,6 +395,63 @@ def _operand(t: torch.Tensor, S: int, T: int, out: bool = False) -> _lib.BqFused
     return _lib.BqFusedOperand(ctypes.c_void_p(t.data_ptr()), ss, st, dt, 0)
 
 
+def _abi(P: Program, outs: list[torch.Tensor], S: int, T: int) -> _lib.BqFusedProgram:
+    """The ABI struct of a Program whose outputs are the tensors ``outs``."""
+    prog = _lib.BqFusedProgram()
+    prog.n_ins, prog.n_loads, prog.n_regs = len(P.ins), P.n_loads, P.n_regs
+    prog.n_in, prog.n_out, prog.n_const = len(P.inputs), len(outs), len(P.consts)
+    for i, w in enumerate(P.ins):
+        prog.ins[i] = w
+    for i, v in enumerate(P.consts):
+        prog.consts[i] = v
+    for i, t in enumerate(P.inputs):
+        prog.inp[i] = _operand(t, S, T)
+    for i, t in enumerate(outs):
+        prog.out[i] = _operand(t, S, T, out=True)
+    return prog
+
+
+def native_source(outputs: dict[str, Ex], S: int, T: int) -> list[str]:
+    """The HIP source bq_fused_eval generates for these outputs (one string per
+    program of the plan). Operands may live on any device: nothing runs."""
+    lib = _lib.load()
+    srcs = []
+    for P in _plan([(k, e if isinstance(e, Ex) else _as_ex(e)) for k, e in outputs.items()]):
+        outs = [torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64) for _, kind in P.outputs]
+        prog = _abi(P, outs, S, T)
+        n = ctypes.c_int64()
+        _lib.check(lib.bq_fused_source(ctypes.byref(prog), None, 0, ctypes.byref(n)), "bq_fused_source")
+        buf = ctypes.create_string_buffer(n.value + 1)
+        _lib.check(lib.bq_fused_source(ctypes.byref(prog), buf, n.value + 1, ctypes.byref(n)), "bq_fused_source")
+        srcs.append(buf.value.decode())
+    return srcs
+
+
+def native_compile(outputs: dict[str, Ex], S: int, T: int) -> int:
+    """Compile (hiprtc, gfx950) the programs for these outputs into the
+    caches without launching them; returns the number of programs. No device
+    is needed, so the code objects can be built ahead of a GPU run."""
+    lib = _lib.load()
+    plans = _plan([(k, e if isinstance(e, Ex) else _as_ex(e)) for k, e in outputs.items()])
+    for P in plans:
+        outs = [torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64) for _, kind in P.outputs]
+        _lib.check(lib.bq_fused_compile(ctypes.byref(_abi(P, outs, S, T))), "bq_fused_compile")
+    return len(plans)
+
+
+def native_stats() -> dict[str, int]:
+    lib = _lib.load()
+    v = [ctypes.c_int64() for _ in range(3)]
+    _lib.check(lib.bq_fused_stats(*[ctypes.byref(x) for x in v]), "bq_fused_stats")
+    return {"compiles": v[0].value, "disk_hits": v[1].value, "cached": v[2].value}
+
+
+def set_native(on: bool | None) -> int:
+    """Select the compiled (True) or interpreted (False) evaluation; None
+    restores the BQ_FUSED_NATIVE default. Returns the previous setting."""
+    return int(_lib.load().bq_fused_set_native(-1 if on is None else int(bool(on))))
+
+
 def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | None = None,
         device=None, stream=None) -> dict[str, torch.Tensor]:
     """Evaluate the named expressions over the [S, T] panel (S, T and the
@@ -448,19 +505,10 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
             t = torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64, device=dev)
             res[name] = t
             outs.append(t)
-        prog = _lib.BqFusedProgram()
-        prog.n_ins, prog.n_loads, prog.n_regs = len(P.ins), P.n_loads, P.n_regs
-        prog.n_in, prog.n_out, prog.n_const = len(P.inputs), len(outs), len(P.consts)
-        for i, w in enumerate(P.ins):
-            prog.ins[i] = w
-        for i, v in enumerate(P.consts):
-            prog.consts[i] = v
-        for i, t in enumerate(P.inputs):
+        for t in P.inputs:
             if t.device != torch.device(dev) and not (t.is_cuda and torch.device(dev).type == "cuda"):
                 raise ValueError("fused operands must be on the evaluation device")
-            prog.inp[i] = _operand(t, S, T)
-        for i, t in enumerate(outs):
-            prog.out[i] = _operand(t, S, T, out=True)
+        prog = _abi(P, outs, S, T)
         _lib.check(lib.bq_fused_eval(ctypes.byref(prog), S, T, engine._stream_handle(stream)), "bq_fused_eval")
         # keep the operands alive until the launch is ordered on the stream
         del prog

@@ -516,6 +516,24 @@ typedef struct {
  * loads first) and runs it over the [S, T] panel. Device operand pointers. */
 int bq_fused_eval(const bq_fused_program* prog, int64_t S, int64_t T, void* stream);
 
+/* Native form of the same programs: bq_fused_eval translates the program into
+ * straight-line HIP source (operand layouts specialised, constants as exact
+ * bit patterns), compiles it for gfx950 with hiprtc on first use and launches
+ * the compiled kernel — bit-identical to the interpreter (the default; the
+ * environment variable BQ_FUSED_NATIVE=0 or bq_fused_set_native(0) selects
+ * the interpreter, -1 restores the environment's choice; returns the previous
+ * setting, -1 if unset). Compiled code objects are cached per process and,
+ * if a directory is set, on disk (<dir>/<hash>.gfx950.co + its source). */
+int bq_fused_set_native(int on);
+int bq_fused_set_cache_dir(const char* dir);
+/* generated source of a (validated) program: *len = its length; up to cap-1
+ * bytes + NUL copied into buf when buf is non-null. No device needed. */
+int bq_fused_source(const bq_fused_program* prog, char* buf, int64_t cap, int64_t* len);
+/* compile (or find in the caches) without launching. No device needed. */
+int bq_fused_compile(const bq_fused_program* prog);
+/* counters: hiprtc compiles, disk-cache hits, programs in the process cache */
+int bq_fused_stats(int64_t* compiles, int64_t* disk_hits, int64_t* cached);
+
 #ifdef __cplusplus
 }
 #endif

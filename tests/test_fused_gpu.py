@@ -15,6 +15,15 @@ from fused_util import assert_same, expressions, random_panel, torch_eval
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["native", "interp"])
+def mode(request):
+    """Both evaluations of a program: the hiprtc-compiled kernel and the
+    LDS-register interpreter."""
+    prev = F.set_native(request.param == "native")
+    yield request.param
+    F.set_native(None if prev < 0 else bool(prev))
+
+
 def _operands(S, T, dev):
     x, y, z = (random_panel(S, T, seed=k).to(dev) for k in range(3))
     b = (torch.rand(S, T, generator=torch.Generator().manual_seed(9)) < 0.5).to(dev)
@@ -24,7 +33,7 @@ def _operands(S, T, dev):
 
 
 @pytest.mark.parametrize("S,T", [(5, 37), (70, 600)])
-def test_each_expression_matches_torch(cuda, S, T):
+def test_each_expression_matches_torch(cuda, mode, S, T):
     ex = expressions(*_operands(S, T, "cuda"))
     for name, e in ex.items():
         got = F.run({name: e}, S, T)[name]
@@ -33,7 +42,7 @@ def test_each_expression_matches_torch(cuda, S, T):
         assert_same(name, got.cpu().numpy(), want.cpu().numpy())
 
 
-def test_all_outputs_in_one_call(cuda):
+def test_all_outputs_in_one_call(cuda, mode):
     S, T = 33, 300
     ex = expressions(*_operands(S, T, "cuda"))
     got = F.run(ex, S, T)
@@ -79,3 +88,31 @@ def test_invalid_programs_are_rejected(cuda):
     assert launch(lambda p: p.ins.__setitem__(0, 99)) != 0                   # unknown opcode
     assert launch(lambda p: setattr(p, "n_loads", 2)) != 0                   # a non-load in the load block
     assert launch(lambda p: setattr(p, "n_const", 0)) != 0                   # constant index out of range
+
+
+@pytest.mark.parametrize("S,T", [(3, 5), (40, 1100), (24, 4099)])
+def test_native_equals_interpreter_bits(cuda, S, T):
+    """Long rows take the 2- and 4-candles-per-thread forms of both
+    evaluations; the compiled kernel reproduces the interpreter's bits
+    (signed zeros included) for every output."""
+    ex = expressions(*_operands(S, T, "cuda"))
+    prev = F.set_native(False)
+    try:
+        ref = F.run(ex, S, T)
+        F.set_native(True)
+        before = F.native_stats()
+        got = F.run(ex, S, T)
+        st = F.native_stats()
+        assert st["cached"] >= 1 and st["compiles"] + st["disk_hits"] >= before["compiles"] + before["disk_hits"]
+    finally:
+        F.set_native(None if prev < 0 else bool(prev))
+    for name in ex:
+        a, b = got[name], ref[name]
+        if a.dtype == torch.float64:
+            # a NaN's sign bit is not a value (the compiler may fold a
+            # negation into a constant): NaN where the interpreter has NaN,
+            # identical bits everywhere else
+            nan = torch.isnan(b)
+            assert torch.equal(torch.isnan(a), nan), name
+            a, b = a[~nan].view(torch.int64), b[~nan].view(torch.int64)
+        assert torch.equal(a, b), name

@@ -70,3 +70,37 @@ def test_register_budget_and_errors():
         bool(X > 0)
     with pytest.raises(RuntimeError):
         F.run({"y": X + 1})   # CPU tensors: no CPU fallback
+
+
+def test_native_source_compiles_for_gfx950(tmp_path, monkeypatch):
+    """The native form of every battery expression (and of the whole battery
+    as one plan) is generated and compiled by hiprtc for gfx950 on the host;
+    constants travel as exact bit patterns; the disk cache is reused."""
+    from binquant_amd import _lib as L
+    lib = L.load()
+    lib.bq_fused_set_cache_dir(str(tmp_path).encode())
+    try:
+        ex = expressions(*_operands())
+        srcs = F.native_source(ex, S, T)
+        assert srcs and all("extern \"C\" __global__" in s and "bq_fk4" in s for s in srcs)
+        # 1e-6 and NaN fills as bit patterns, never decimal literals
+        joined = "\n".join(srcs)
+        assert "0x3eb0c6f7a0b5ed8dull" in joined and "0x7ff8000000000000ull" in joined
+        before = F.native_stats()
+        n = F.native_compile(ex, S, T)
+        after = F.native_stats()
+        assert after["compiles"] + after["disk_hits"] - before["compiles"] - before["disk_hits"] <= n
+        assert len(list(tmp_path.glob("*.gfx950.co"))) >= 1
+        assert F.native_compile(ex, S, T) == n   # process cache: no new compile
+        assert F.native_stats()["compiles"] == after["compiles"]
+    finally:
+        lib.bq_fused_set_cache_dir(str(L.LIB_PATH.parent / "fused_cache").encode())
+
+
+def test_native_source_rejects_invalid_program():
+    prog = _lib.BqFusedProgram()
+    prog.n_ins = 1
+    prog.ins[0] = 999   # bad opcode
+    n = __import__("ctypes").c_int64()
+    assert _lib.load().bq_fused_source(prog, None, 0, n) == _lib.BQ_EINVAL
+    assert _lib.load().bq_fused_compile(prog) == _lib.BQ_EINVAL
