@@ -704,6 +704,97 @@ __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
   }
 }
 
+// ---- stencil rank kernel (lane = one output, window from an LDS row span) ------------
+// For short windows (w <= 32): a block takes 256 consecutive outputs of one
+// symbol and stages their values plus the w - 1 before them in LDS with one
+// coalesced pass; each lane copies its own window into registers (NaN ->
+// +inf, counted out) and sorts it with Batcher's odd-even merge network on N
+// slots (N the window bucket; slots >= w hold +inf, comparators beyond N are
+// pruned — a +inf partner never moves), then picks its ranks. No state along
+// the row (no warm-up, no lane walking its own row through the caches),
+// ~1.1 reads and one coalesced write per output; the network is
+// O(N log^2 N) min/max pairs per output.
+template <int N>
+__device__ __forceinline__ void sort_network(double (&v)[N]) {
+  constexpr int NP = N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16 : 32;
+#pragma unroll
+  for (int p = 1; p < NP; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < NP; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k; ++i) {
+          const int a = i + j, b = i + j + k;
+          if (b < N && a / (2 * p) == b / (2 * p)) {
+            const double x = v[a], y = v[b];
+            v[a] = fmin(x, y);
+            v[b] = fmax(x, y);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ double pick(const double (&v)[N], int k) {   // v[k], k run-time
+  unsigned long long r = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r |= (0ull - (unsigned long long)(i == k)) & (unsigned long long)__double_as_longlong(v[i]);
+  return __longlong_as_double((long long)r);
+}
+
+constexpr int SR_NT = 256;
+
+template <int N>
+__global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) {
+  __shared__ double s[SR_NT + N - 1];
+  const RollJob& A = B.j[blockIdx.y];
+  const int T = B.T, w = A.win;
+  const int nbt = (T + SR_NT - 1) / SR_NT;
+  const int64_t sym = blockIdx.x / nbt;
+  const int t0 = (int)(blockIdx.x % nbt) * SR_NT;
+  const double* __restrict__ x = A.x + sym * A.ld_in;
+  // s[i] = the series value of candle t0 - (w - 1) + i, i.e. x[that - shift]
+  const int base = t0 - (w - 1) - A.shift;
+  for (int i = threadIdx.x; i < SR_NT + w - 1; i += SR_NT) {
+    const int xi = base + i;
+    s[i] = (xi >= 0 && xi < T) ? x[xi] : qnan();
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T) return;
+  double v[N];
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double a = s[threadIdx.x + j];   // in bounds for every j < N; slots >= w are pads
+    const bool num = j < w && a == a;
+    n += num ? 1 : 0;
+    v[j] = num ? a : __builtin_inf();
+  }
+  sort_network<N>(v);
+  double r = qnan();
+  if (n >= A.minp && n > 0) {
+    if (A.mode == BQ_ROLL_MEDIAN) {
+      const int h = n >> 1;
+      r = (n & 1) ? pick(v, h) : (pick(v, h - 1) + pick(v, h)) / 2.0;
+    } else if (n == 1) {
+      r = v[0];
+    } else {   // roll_quantile, linear interpolation (max / min: q = 1 / 0)
+      const double idxf = A.q * (double)(n - 1);
+      const int idx = (int)idxf;
+      if ((double)idx == idxf) r = pick(v, idx);
+      else {
+        const double lo = pick(v, idx), hi = pick(v, idx + 1);
+        r = lo + (hi - lo) * (idxf - (double)idx);
+      }
+    }
+  }
+  A.out[sym * A.ld_out + t] = r;
+}
+
 }  // namespace bq
 
 namespace {
@@ -733,6 +824,20 @@ void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   const int64_t nt = (B.T + bq::WAVE * OPL - 1) / (bq::WAVE * OPL);
   const unsigned blocks = (unsigned)((B.S * nt + 3) / 4);
   hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+}
+
+int stencil_bucket(int w) { return w <= 4 ? 0 : w <= 8 ? 1 : w <= 16 ? 2 : w <= 24 ? 3 : 4; }
+
+void launch_stencil(int b, const bq::RollBatch& B, int n, hipStream_t st) {
+  const int64_t nbt = (B.T + bq::SR_NT - 1) / bq::SR_NT;
+  const dim3 grid((unsigned)(B.S * nbt), (unsigned)n);
+  switch (b) {
+    case 0: hipLaunchKernelGGL(bq::stencil_rank_kernel<4>, grid, dim3(bq::SR_NT), 0, st, B); break;
+    case 1: hipLaunchKernelGGL(bq::stencil_rank_kernel<8>, grid, dim3(bq::SR_NT), 0, st, B); break;
+    case 2: hipLaunchKernelGGL(bq::stencil_rank_kernel<16>, grid, dim3(bq::SR_NT), 0, st, B); break;
+    case 3: hipLaunchKernelGGL(bq::stencil_rank_kernel<24>, grid, dim3(bq::SR_NT), 0, st, B); break;
+    default: hipLaunchKernelGGL(bq::stencil_rank_kernel<32>, grid, dim3(bq::SR_NT), 0, st, B);
+  }
 }
 
 // which replay kernel: 0 = LDS ring over the window (one launch, 64 symbols
@@ -793,21 +898,25 @@ void launch_restage_any(int cls, const bq::RollBatch& B, int n, hipStream_t st) 
 }
 
 // which order-statistic kernel: 0 = lane (sorted window per lane), 1 = tile
-// (sorted union per wave). BQ_RANK_IMPL=lane|tile forces one (measurement).
+// (sorted union per wave), 2 = stencil (sorting network per output, w <= 32).
+// BQ_RANK_IMPL=lane|tile|stencil forces one (measurement; stencil falls back
+// to tile above w = 32).
 int rank_impl(int w, int64_t S, int64_t T) {
   static const int forced = [] {
     const char* e = getenv("BQ_RANK_IMPL");
-    return !e ? -1 : (strcmp(e, "lane") == 0 ? 0 : strcmp(e, "tile") == 0 ? 1 : -1);
+    return !e ? -1
+              : (strcmp(e, "lane") == 0      ? 0
+                 : strcmp(e, "tile") == 0    ? 1
+                 : strcmp(e, "stencil") == 0 ? 2
+                                             : -1);
   }();
-  if (forced >= 0) return forced;
-  // measured (tools/rank_ab.py, bit-identical outputs): the tile kernel wins
-  // for every window at live shapes (1000 x 400: w 80 0.68 -> 0.027 ms) and
-  // for w >= 24 at 12.5k x 2k (w 80 1.59 -> 0.73 ms); the lane kernel keeps
-  // short windows on large panels (w 3: 0.53 vs 0.92 ms), where its warm-up
-  // is short and the per-step pass over w slots is cheap
-  if (w <= 8) return 0;
-  if (w <= 20 && S * T >= 4000000) return 0;
-  return 1;
+  (void)S;
+  (void)T;
+  if (forced >= 0) return forced == 2 && w > 32 ? 1 : forced;
+  // short windows: the stencil kernel (coalesced, no warm-up, no per-lane row
+  // walk); longer ones: the tile kernel, whose sort is shared by 64 / 128
+  // outputs (the lane kernel stays selectable for measurement)
+  return w <= 32 ? 2 : 1;
 }
 
 }  // namespace
@@ -902,6 +1011,18 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     else launch_tile_rank<4, 2>(tile[g], ntile[g], st);
     ntile[g] = 0;
   };
+  RollBatch sten[5];
+  int nsten[5] = {0, 0, 0, 0, 0};
+  for (int b = 0; b < 5; ++b) {
+    memset(&sten[b], 0, sizeof(RollBatch));
+    sten[b].S = S;
+    sten[b].T = (int)T;
+  }
+  auto flush_sten = [&](int b) {
+    if (!nsten[b]) return;
+    launch_stencil(b, sten[b], nsten[b], st);
+    nsten[b] = 0;
+  };
   for (int i = 0; i < n_jobs; ++i) {
     const bq_roll_job& in = jobs[i];
     RollJob J;
@@ -921,7 +1042,11 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       max_back = back > max_back ? back : max_back;
       rep.j[nrep++] = J;
       if (nrep == RW_MAXJOBS) flush_rep();
-    } else if (rank_impl(in.window, S, T)) {
+    } else if (rank_impl(in.window, S, T) == 2 && S * ((T + SR_NT - 1) / SR_NT) <= 0x7fffffff) {
+      const int b = stencil_bucket(in.window);
+      sten[b].j[nsten[b]++] = J;
+      if (nsten[b] == RW_MAXJOBS) flush_sten(b);
+    } else if (rank_impl(in.window, S, T) >= 1) {
       const int g = in.window <= 65 ? 0 : 1;   // union of a 64- / 128-output tile fits 128 / 256 slots
       tile[g].j[ntile[g]++] = J;
       if (ntile[g] == RW_MAXJOBS) flush_tile(g);
@@ -952,6 +1077,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   flush_rep();
   for (int b = 0; b < 6; ++b) flush_rank(b);
   for (int g = 0; g < 2; ++g) flush_tile(g);
+  for (int b = 0; b < 5; ++b) flush_sten(b);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

@@ -1,5 +1,6 @@
 """Both kernel families behind each rolling statistic give the same bits:
-the per-lane sorted window vs the per-wave sorted union (order statistics),
+the per-lane sorted window vs the per-wave sorted union vs the per-output
+sorting network (order statistics),
 the LDS-ring replay vs the class-specialised re-staging replay (moments, ewm,
 ffill). Each implementation is forced in its own child process
 (BQ_RANK_IMPL / BQ_REPLAY_IMPL) over the same battery — NaN gaps, constant
@@ -30,6 +31,7 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
     runs = {
         "lane_ring": _run(tmp_path, "lane_ring", {"BQ_RANK_IMPL": "lane", "BQ_REPLAY_IMPL": "ring"}),
         "tile_restage": _run(tmp_path, "tile_restage", {"BQ_RANK_IMPL": "tile", "BQ_REPLAY_IMPL": "restage"}),
+        "stencil_mixed": _run(tmp_path, "stencil_mixed", {"BQ_RANK_IMPL": "stencil", "BQ_REPLAY_IMPL": "mixed"}),
         "auto": _run(tmp_path, "auto", {}),
     }
     ref = runs["auto"]
