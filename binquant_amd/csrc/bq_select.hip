@@ -13,9 +13,10 @@
 //
 //     Mapping: one 256-thread workgroup per row, radix select over the
 //     order-preserving 64-bit image of the doubles: 8 passes of an 8-bit digit
-//     histogram in LDS narrow the k-th key, one more pass finds its successor.
-//     Every pass streams the row (<= 80 KB at T = 10^4, L2-resident after the
-//     first pass); no sort, no scratch in HBM.
+//     histogram in LDS narrow the k-th key (the digit picked by a block scan
+//     of the bins), one more pass finds its successor. Rows up to 10,240
+//     values keep their keys in registers (one HBM read); longer rows stream
+//     each pass (L2-resident after the first); no sort, no scratch in HBM.
 //
 //   bq_cooldown: FailedSpikeFade.apply_cooldown
 //     (strategies/failed_spike_fade.py:495-520): walking forward, a label
@@ -72,18 +73,37 @@ __device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t* red) {
   return m;
 }
 
+// KR > 0: the row's keys stay in registers (KR per thread, T <= 256 * KR), so
+// the row is read from HBM once; KR == 0 streams the row on every pass. The
+// digit whose bin holds rank k is found by a block-wide scan of the 256 bins
+// (one bin per thread), not by a serial walk.
+template <int KR>
 __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __restrict__ x, int T, int64_t ld_in,
                                                              double q, double* __restrict__ out) {
   __shared__ unsigned hist[256];
   __shared__ int red_i[SQ_NT / 64];
   __shared__ uint64_t red_u[SQ_NT / 64];
+  __shared__ unsigned wsum[SQ_NT / 64];
   __shared__ uint64_t s_prefix;
   __shared__ int s_k;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* __restrict__ r = x + (int64_t)blockIdx.x * ld_in;
 
+  // key 0 never encodes a number (order_key sets bit 63 for positives and
+  // only an all-ones NaN would map a negative to 0): it marks NaN / padding
+  uint64_t kr[KR > 0 ? KR : 1];
   int cnt = 0;
-  for (int t = tid; t < T; t += SQ_NT) cnt += r[t] == r[t];
+  if (KR > 0) {
+#pragma unroll
+    for (int i = 0; i < (KR > 0 ? KR : 1); ++i) {
+      const int t = tid + i * SQ_NT;
+      const double v = t < T ? r[t] : qnan();
+      kr[i] = v == v ? order_key(v) : 0ull;
+      cnt += v == v;
+    }
+  } else {
+    for (int t = tid; t < T; t += SQ_NT) cnt += r[t] == r[t];
+  }
   const int n = block_sum(cnt, red_i);
   if (n == 0) {
     if (tid == 0) out[blockIdx.x] = qnan();
@@ -101,23 +121,38 @@ __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __res
   for (int sh = 56; sh >= 0; sh -= 8) {
     hist[tid] = 0;   // SQ_NT == 256 bins
     __syncthreads();
-    for (int t = tid; t < T; t += SQ_NT) {
-      const double v = r[t];
-      if (v == v) {
-        const uint64_t key = order_key(v);
-        if ((key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+    if (KR > 0) {
+#pragma unroll
+      for (int i = 0; i < (KR > 0 ? KR : 1); ++i) {
+        const uint64_t key = kr[i];
+        if (key && (key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+      }
+    } else {
+      for (int t = tid; t < T; t += SQ_NT) {
+        const double v = r[t];
+        if (v == v) {
+          const uint64_t key = order_key(v);
+          if ((key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+        }
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      int cum = 0, b = 0;
-      for (; b < 255; ++b) {
-        const int h = (int)hist[b];
-        if (cum + h > k) break;
-        cum += h;
-      }
-      s_prefix = prefix | ((uint64_t)b << sh);
-      s_k = k - cum;
+    // exclusive prefix of the bins; the bin with excl <= k < excl + h holds rank k
+    const unsigned h = hist[tid];
+    unsigned incl = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    unsigned excl = incl - h;
+#pragma unroll
+    for (int w = 0; w < SQ_NT / 64; ++w) excl += w < wave ? wsum[w] : 0u;
+    if (h > 0 && (int)excl <= k && k < (int)(excl + h)) {
+      s_prefix = prefix | ((uint64_t)tid << sh);
+      s_k = k - (int)excl;
     }
     __syncthreads();
     prefix = s_prefix;
@@ -129,12 +164,23 @@ __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __res
   if (next != prev) {
     int le = 0;
     uint64_t above = ~0ull;
-    for (int t = tid; t < T; t += SQ_NT) {
-      const double v = r[t];
-      if (v == v) {
-        const uint64_t key = order_key(v);
-        le += key <= prefix;
-        if (key > prefix && key < above) above = key;
+    if (KR > 0) {
+#pragma unroll
+      for (int i = 0; i < (KR > 0 ? KR : 1); ++i) {
+        const uint64_t key = kr[i];
+        if (key) {
+          le += key <= prefix;
+          if (key > prefix && key < above) above = key;
+        }
+      }
+    } else {
+      for (int t = tid; t < T; t += SQ_NT) {
+        const double v = r[t];
+        if (v == v) {
+          const uint64_t key = order_key(v);
+          le += key <= prefix;
+          if (key > prefix && key < above) above = key;
+        }
       }
     }
     const int nle = block_sum(le, red_i);
@@ -192,8 +238,12 @@ int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double
   if (!x || !out || S < 0 || T < 0 || ld_in < T || !(q >= 0.0 && q <= 1.0) || T > 0x7fffffff || S > 0x7fffffff)
     return BQ_EINVAL;
   if (S == 0) return BQ_OK;
-  hipLaunchKernelGGL(row_quantile_kernel, dim3((unsigned)S), dim3(SQ_NT), 0, (hipStream_t)stream, x, (int)T, ld_in,
-                     q, out);
+  const dim3 g((unsigned)S), blk(SQ_NT);
+  hipStream_t st = (hipStream_t)stream;
+  if (T <= 8 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<8>, g, blk, 0, st, x, (int)T, ld_in, q, out);
+  else if (T <= 16 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<16>, g, blk, 0, st, x, (int)T, ld_in, q, out);
+  else if (T <= 40 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<40>, g, blk, 0, st, x, (int)T, ld_in, q, out);
+  else hipLaunchKernelGGL(row_quantile_kernel<0>, g, blk, 0, st, x, (int)T, ld_in, q, out);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

@@ -114,11 +114,11 @@ def test_rolling_signed_series_vs_pandas(cuda, stat, window, minp):
         np.testing.assert_array_equal(got[s], want, err_msg=f"{stat} {s}")
 
 
-def test_row_quantile_is_numpy_bitwise(cuda):
+@pytest.mark.parametrize("T", [700, 3000, 9000])   # register-resident row forms (8 / 16 / 40 keys per thread)
+def test_row_quantile_is_numpy_bitwise(cuda, T):
     from binquant_amd import engine
 
     rng = np.random.default_rng(11)
-    T = 3000
     x = rng.lognormal(0, 1, (10, T))
     x[1] = rng.normal(0, 1, T)                    # negatives
     x[2] = np.round(rng.normal(0, 3, T))          # heavy ties
@@ -126,7 +126,7 @@ def test_row_quantile_is_numpy_bitwise(cuda):
     x[4, :] = np.nan
     x[4, 17] = 2.5                                # single observation
     x[5, :] = np.nan
-    x[5, [3, 900]] = [4.0, -1.0]                  # two observations
+    x[5, [3, T - 100]] = [4.0, -1.0]              # two observations
     x[6, ::3] = np.nan                            # ragged NaNs
     x[7, :] = 7.0                                 # constant
     x[8, :11] = np.nan                            # leading NaNs (rolling warm-up)
