@@ -765,6 +765,29 @@ __global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) 
   __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= T) return;
+  if (A.mode == BQ_ROLL_ISUM) {
+    // integers: every partial sum is exact, so any order gives pandas' Kahan
+    // value; pandas' same-value rule (the run of equal values covers the
+    // window: prev * nobs) only decides the sign of a zero sum
+    double sum = 0.0, last = qnan();
+    int n = 0;
+    bool same = true;
+    for (int j = w - 1; j >= 0; --j) {   // newest first: `last` is pandas' prev
+      const double a = s[threadIdx.x + j];
+      if (a == a) {
+        if (n == 0) last = a;
+        same = same && a == last;
+        sum += a;
+        ++n;
+      }
+    }
+    double r;
+    if (n == 0 && A.minp == 0) r = 0.0;
+    else if (n < A.minp || n == 0) r = qnan();
+    else r = same ? last * (double)n : sum;
+    A.out[sym * A.ld_out + t] = r;
+    return;
+  }
   double v[N];
   int n = 0;
 #pragma unroll
@@ -806,7 +829,8 @@ bool job_ok(const bq_roll_job& j, int64_t T) {
   if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
   if (j.mode == BQ_ROLL_FFILL) return j.shift == 0;
   return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
-         j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0 && j.q >= 0.0 && j.q <= 1.0;
+         ((j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0) || j.mode == BQ_ROLL_ISUM) && j.q >= 0.0 &&
+         j.q <= 1.0;
 }
 
 int rank_bucket(int w) {
@@ -1037,8 +1061,14 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     J.mode = in.mode;
     J.q = in.q;
     J.alpha = in.alpha;
-    if (in.mode >= BQ_ROLL_MEAN) {   // moments / ewm: exact replay
-      const int back = (in.mode == BQ_ROLL_EWM || in.mode == BQ_ROLL_FFILL) ? 0 : in.window + in.shift;
+    if (in.mode == BQ_ROLL_ISUM && (in.window > 32 || S * ((T + SR_NT - 1) / SR_NT) > 0x7fffffff))
+      J.mode = BQ_ROLL_SUM;   // long window: the replay (identical values for integer series)
+    if (J.mode == BQ_ROLL_ISUM) {   // integer-valued sum: a direct window sum, stencil launch
+      const int b = stencil_bucket(in.window);
+      sten[b].j[nsten[b]++] = J;
+      if (nsten[b] == RW_MAXJOBS) flush_sten(b);
+    } else if (J.mode >= BQ_ROLL_MEAN) {   // moments / ewm: exact replay
+      const int back = (J.mode == BQ_ROLL_EWM || J.mode == BQ_ROLL_FFILL) ? 0 : in.window + in.shift;
       max_back = back > max_back ? back : max_back;
       rep.j[nrep++] = J;
       if (nrep == RW_MAXJOBS) flush_rep();
@@ -1083,7 +1113,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
 
 int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream) {
-  if (mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0) return BQ_EINVAL;
+  if ((mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0) && mode != BQ_ROLL_ISUM) return BQ_EINVAL;
   bq_roll_job j;
   memset(&j, 0, sizeof(j));
   j.x = x;

@@ -302,7 +302,9 @@ def rolling(
 ) -> torch.Tensor:
     """x.shift(shift).rolling(window, min_periods).<stat>() along T of a [S, T]
     panel; stat in {"quantile", "median", "mean", "sum", "var", "std", "max",
-    "min"} (var / std: ddof 1)."""
+    "min", "isum"} (var / std: ddof 1; isum: the sum of an integer-valued
+    series such as a flag count — pandas' value, computed without the
+    sequential replay)."""
     x = _check_panel(x, "x")
     S, T = x.shape
     if stat == "max":

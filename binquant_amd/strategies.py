@@ -67,7 +67,7 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     mb = p.min_baseline_volume
     # volume.shift(2).rolling(bw - 1, min_periods=bw - 1).median()   (:58-63)
     up = F.run({"up": (C > F.shift(C, 1)).float()})["up"]
-    specs = [R(v, bw - 1, "median", min_periods=bw - 1, shift=2), R(up, 3, "sum", min_periods=3)]
+    specs = [R(v, bw - 1, "median", min_periods=bw - 1, shift=2), R(up, 3, "isum", min_periods=3)]
     if has_q:
         specs.append(R(qv, bw - 1, "median", min_periods=bw - 1, shift=2))
     res = engine.rolling_many(*specs)
@@ -269,8 +269,8 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
     # every rolling series that depends only on the inputs: ONE batched call
     specs = [R(c, w, "mean"), R(c, w, "std"), R(v, w, "mean"), R(v, w, "std"), R(qv, w, "mean"),
              R(c, 8, "std"), R(c, 20, "std"), R(b["price_change"], 2, "sum"), R(b["price_change"], 3, "sum"),
-             R(b["_pos"], 5, "sum"), R(b["price_change_abs"], 5, "sum"), R(b["body_size_pct"], 10, "mean"),
-             R(b["body_size_pct"], 10, "std"), R(b["_green"], n, "sum"), R(b["_red"], n, "sum")]
+             R(b["_pos"], 5, "isum"), R(b["price_change_abs"], 5, "sum"), R(b["body_size_pct"], 10, "mean"),
+             R(b["body_size_pct"], 10, "std"), R(b["_green"], n, "isum"), R(b["_red"], n, "isum")]
     if cw > 1:
         specs += [R(b["_clip_pos"], cw, "sum"), R(b["_neg"], cw, "sum")]
     if p.price_break_use_dynamic:
@@ -322,7 +322,7 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
         e3["_thr_pre"] = F.where(F.isnan(D), D, F.maximum(PB, D))
     k = F.run(e3, S, T)
     # ---- volume_cluster_flag (:360-370), the dynamic threshold's ffill (:372-400) ----
-    specs2 = [R(k["_cond"], p.volume_cluster_window, "sum", min_periods=1),
+    specs2 = [R(k["_cond"], p.volume_cluster_window, "isum", min_periods=1),
               R(k["_cond8"], max(cw, 1), "max")]
     if p.price_break_use_dynamic:
         specs2.append(FF(k["_thr_pre"]))
