@@ -118,6 +118,8 @@ int main(int argc, char** argv) {
       {"pf2_3wg", 0, 0, 0, 256, 2, 52000},  {"pf1_2wg", 0, 0, 0, 256, 1, 78000},
       {"pf1_3wg_b", 0, 0, 0, 256, 1, 52000}, {"pf2_2wg_b", 0, 0, 0, 256, 2, 78000},
       {"pf2_3wg_b", 0, 0, 0, 256, 2, 52000}, {"pf1_4wg", 0, 0, 0, 256, 1, 39000},
+      {"pf1_5wg", 0, 0, 0, 256, 1, 31000},  {"pf1_6wg", 0, 0, 0, 256, 1, 26000},
+      {"pf1_8wg", 0, 0, 0, 256, 1, 19000},  {"pf2_4wg", 0, 0, 0, 256, 2, 39000},
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
