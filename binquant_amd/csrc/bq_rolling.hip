@@ -51,6 +51,7 @@
 #include "binquant_amd.h"
 
 #include <stdlib.h>
+#include <type_traits>
 #include <string.h>
 
 namespace bq {
@@ -183,15 +184,17 @@ struct ReplayLane {
     nobs = 0;
   }
   // v_in = x[t - shift] (NaN before the row), v_out = x[t - shift - w]
+  // steady: t >= window + shift + 1 (no first candle, the leaving value is
+  // always inside the row) — lets a caller drop the per-step checks
   __device__ __forceinline__ double step(const RollJob& A, bool EWM, bool welford, int t, double v_in, double v_out,
-                                         bool FFILL = false) {
+                                         bool FFILL = false, bool steady = false) {
     if (FFILL) {   // last observation carried forward (weighted holds it)
       if (v_in == v_in) weighted = v_in;
       return weighted;
     }
     if (EWM) {
       const double alpha = A.alpha, om = 1.0 - alpha;
-      if (t == 0) {
+      if (!steady && t == 0) {
         weighted = v_in;
         nobs = v_in == v_in;
       } else {
@@ -212,8 +215,8 @@ struct ReplayLane {
       }
       return nobs >= A.minp ? weighted : qnan();
     }
-    if (t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
-    if (t >= A.win && t - A.shift - A.win >= 0) m.remove(v_out, welford);
+    if (!steady && t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
+    if (steady || (t >= A.win && t - A.shift - A.win >= 0)) m.remove(v_out, welford);
     m.add(v_in, welford);
     return m.result(A.mode, A.minp);
   }
@@ -282,25 +285,43 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
 // per-class launch keeps the registers to that class's state).
 // SPW: symbols per wave (64; 32, 16, 8 for measurement). With SPW < 64 the
 // same rows spread over 64/SPW times as many waves (lanes >= SPW only help
-// stage; each chunk is RP_ELEMS / SPW candles long). Measured: no faster —
+// stage; each chunk is RS_V * 64 / SPW candles long). Measured: no faster —
 // a 12.5k-symbol replay (196 waves) costs ~600 cycles per step in the wave's
 // own ~100-instruction stream (NaN guards, the same-value rule, the IEEE
 // divide of the mean), not in a shortage of waves.
-constexpr int RP_ELEMS = RP_CT * WAVE;   // staged values per wave and chunk
+// staged values per lane and chunk: 16 for the class kernels, 8 for the
+// all-classes kernel (its register footprint then allows 2 waves per SIMD
+// instead of 1; measured tools/pipe_ab.sh: failed-spike replay 3.6 -> 3.2 ms,
+// while the class kernels are faster with 16)
+#ifndef BQ_RS_V
+#define BQ_RS_V 16
+#endif
+#ifndef BQ_RS_V_MIXED
+#define BQ_RS_V_MIXED 8
+#endif
+#ifndef BQ_RS_STAGE_OUT
+#define BQ_RS_STAGE_OUT 1   // results leave through LDS as coalesced row segments
+#endif
+#ifndef BQ_RS_WPS
+#define BQ_RS_WPS 2   // min waves per SIMD (register cap) of the re-staging replays
+#endif
+#ifndef BQ_RS_WPS_MIXED
+#define BQ_RS_WPS_MIXED 2   // the all-classes kernel
+#endif
 
-template <int SPW>
+template <int SPW, int RS_V>
 struct ReplayTile {
-  static constexpr int CT = RP_ELEMS / SPW;   // candles per chunk
+  static constexpr int CT = RS_V * WAVE / SPW;   // candles per chunk
   static constexpr int P = SPW + 2;           // LDS pitch (doubles) of one candle's row
   static constexpr int N = CT * P;
   // [SPW symbols][CT candles] of rows sym0.. from column t0, read so that
   // consecutive lanes read consecutive candles of one row
   __device__ __forceinline__ static void load(const double* __restrict__ base, int64_t ld, int64_t sym0, int64_t S,
-                                              int t0, int T, int lane, double (&r)[RP_CT]) {
+                                              int t0, int T, int lane, double (&r)[RS_V]) {
 // Every lane loads (a clamped, valid address) and selects NaN outside the
   // panel: no branch around a load, so no load forces a full vmcnt drain.
 #pragma unroll
-    for (int k = 0; k < RP_CT; ++k) {
+    for (int k = 0; k < RS_V; ++k) {
       const int e = lane + WAVE * k;
       const int64_t s = sym0 + e / CT;
       const int t = t0 + e % CT;
@@ -310,10 +331,22 @@ struct ReplayTile {
       r[k] = (s < S && t >= 0 && t < T) ? v : qnan();
     }
   }
-  // transposed into LDS: lds[candle * P + symbol]
-  __device__ __forceinline__ static void put(double* lds, int lane, const double (&r)[RP_CT]) {
+  // interior chunk (rows sym0 .. sym0 + SPW - 1 all < S, candles t .. t + CT - 1
+  // all inside the row): buffer loads at a per-lane offset fixed for the whole
+  // walk plus a per-k scalar row step — no per-element address arithmetic or
+  // range selects (the general form above handles the edges)
+  static constexpr bool FAST = CT <= WAVE;
+  __device__ __forceinline__ static void load_fast(__amdgpu_buffer_rsrc_t rs, unsigned loff, unsigned rowstep,
+                                                   int t, double (&r)[RS_V]) {
+    const unsigned v = loff + (unsigned)t * (unsigned)sizeof(double);
 #pragma unroll
-    for (int k = 0; k < RP_CT; ++k) {
+    for (int k = 0; k < RS_V; ++k)
+      r[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, v, (unsigned)k * rowstep, 0));
+  }
+  // transposed into LDS: lds[candle * P + symbol]
+  __device__ __forceinline__ static void put(double* lds, int lane, const double (&r)[RS_V]) {
+#pragma unroll
+    for (int k = 0; k < RS_V; ++k) {
       const int e = lane + WAVE * k;
       lds[(e % CT) * P + e / CT] = r[k];
     }
@@ -326,10 +359,10 @@ struct ReplayTile {
 // counted (vmcnt(N) for the prefetched chunk) instead of draining every
 // outstanding result store at each chunk boundary (gfx950's vmcnt counts
 // loads and stores alike). Host guarantees 64 * ld_out * 8 < 2^31 (job_ok).
-template <int CLS, int SPW>
+template <int CLS, int SPW, int RS_V>
 __device__ __forceinline__ void replay_restage_body(const RollJob& A, const RollBatch& B, double* s_in,
                                                     double* s_out) {
-  using Tl = ReplayTile<SPW>;
+  using Tl = ReplayTile<SPW, RS_V>;
   constexpr int CT = Tl::CT;
   constexpr bool FFILL = CLS == 3;
   constexpr bool EWM = CLS == 0 || FFILL;   // no leaving value
@@ -345,20 +378,28 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
   const bool live = lane < rows;
   const unsigned obase = live ? (unsigned)(lane * A.ld_out * (int64_t)sizeof(double)) : (unsigned)nbytes;
   const int rl = lane < SPW ? lane : SPW - 1;   // lanes >= SPW replay a copy (stores dropped)
-  double ri[RP_CT], ro[RP_CT];
+  double ri[RS_V], ro[RS_V];
   Tl::load(A.x, A.ld_in, sym0, S, -sh, T, lane, ri);
   if (!EWM) Tl::load(A.x, A.ld_in, sym0, S, -sh - w, T, lane, ro);
   ReplayLane st;
   st.init();
-  auto step = [&](int t, double v_in, double v_out) {
-    const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL);
+  auto step = [&](int t, double v_in, double v_out, auto steady) {
+    const double res = st.step(A, EWM, welford, t, v_in, v_out, FFILL, decltype(steady)::value);
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bq_u32x2, res), orsrc,
                                           obase + (unsigned)t * (unsigned)sizeof(double), 0, 0);
   };
+  // full chunks (CT <= 64): a step's result goes into the LDS slot its input
+  // came from (already read by this lane), and the chunk leaves through
+  // coalesced row segments after its last step — one store instruction then
+  // covers 64 / CT rows x CT candles instead of 64 rows x 1 candle
+  constexpr bool OUT_LDS = Tl::FAST && BQ_RS_STAGE_OUT;
+  auto step_lds = [&](int t, int j, double v_in, double v_out, auto steady) {
+    s_in[j * Tl::P + rl] = st.step(A, EWM, welford, t, v_in, v_out, FFILL, decltype(steady)::value);
+  };
   // 16 steps at a time: their LDS operands are read into registers first, so
   // no LDS latency sits between two dependent state updates
-  constexpr int G = 16;
-  auto steps16 = [&](int t0, int g) {
+  constexpr int G = CT < 16 ? CT : 16;
+  auto steps16 = [&](int t0, int g, auto steady) {
     double vi[G], vo[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
@@ -366,7 +407,34 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
       vo[k] = EWM ? 0.0 : s_out[(g + k) * Tl::P + rl];
     }
 #pragma unroll
-    for (int k = 0; k < G; ++k) step(t0 + g + k, vi[k], vo[k]);
+    for (int k = 0; k < G; ++k) {
+      if (OUT_LDS) step_lds(t0 + g + k, g + k, vi[k], vo[k], steady);
+      else step(t0 + g + k, vi[k], vo[k], steady);
+    }
+  };
+  // the chunk's results, transposed back out of LDS: element e = lane + 64k is
+  // row e / CT, candle e % CT; rows past S fall outside the descriptor
+  const unsigned ooff = (unsigned)(((lane / CT) * A.ld_out + lane % CT) * (int64_t)sizeof(double));
+  const unsigned orowstep = (unsigned)((WAVE / CT) * A.ld_out * (int64_t)sizeof(double));
+  auto flush = [&](int t0) {
+    const unsigned v = ooff + (unsigned)t0 * (unsigned)sizeof(double);
+#pragma unroll
+    for (int k = 0; k < RS_V; ++k) {
+      const int e = lane + WAVE * k;
+      const double r = s_in[(e % CT) * Tl::P + e / CT];
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(bq_u32x2, r), orsrc, v, (unsigned)k * orowstep, 0);
+    }
+  };
+  // input rows as one buffer (interior chunks load through it)
+  const bool rows_full = rows == SPW && A.ld_in <= BQ_MAX_ROLL_LD;
+  const __amdgpu_buffer_rsrc_t irsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(A.x) + sym0 * A.ld_in, 0, rows_full ? (int)(SPW * A.ld_in * (int64_t)sizeof(double)) : 0,
+      0x00020000);
+  const unsigned loff = (unsigned)(((lane / CT) * A.ld_in + lane % CT) * (int64_t)sizeof(double));
+  const unsigned rowstep = (unsigned)((WAVE / CT) * A.ld_in * (int64_t)sizeof(double));
+  auto stage = [&](int t, double (&r)[RS_V]) {
+    if (Tl::FAST && rows_full && t >= 0 && t + CT <= T) Tl::load_fast(irsrc, loff, rowstep, t, r);
+    else Tl::load(A.x, A.ld_in, sym0, S, t, T, lane, r);
   };
   const int tfull = T - T % CT;
   int t0 = 0;
@@ -375,17 +443,27 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
     if (!EWM) Tl::put(s_out, lane, ro);
     __syncthreads();
     // next chunks in flight during this one's replay (past T: NaN, unused)
-    Tl::load(A.x, A.ld_in, sym0, S, t0 + CT - sh, T, lane, ri);
-    if (!EWM) Tl::load(A.x, A.ld_in, sym0, S, t0 + CT - sh - w, T, lane, ro);
+    stage(t0 + CT - sh, ri);
+    if (!EWM) stage(t0 + CT - sh - w, ro);
+    if (t0 >= w + sh + 1) {   // every step of the chunk is steady
 #pragma unroll 1
-    for (int g = 0; g < CT; g += G) steps16(t0, g);
+      for (int g = 0; g < CT; g += G) steps16(t0, g, std::true_type{});
+    } else {
+#pragma unroll 1
+      for (int g = 0; g < CT; g += G) steps16(t0, g, std::false_type{});
+    }
+    if (OUT_LDS) {
+      __syncthreads();   // the chunk's results are in s_in
+      flush(t0);
+    }
     __syncthreads();   // both tiles are rewritten by the next chunk
   }
   if (t0 < T) {   // tail chunk
     Tl::put(s_in, lane, ri);
     if (!EWM) Tl::put(s_out, lane, ro);
     __syncthreads();
-    for (int j = 0; j < T - t0; ++j) step(t0 + j, s_in[j * Tl::P + rl], EWM ? 0.0 : s_out[j * Tl::P + rl]);
+    for (int j = 0; j < T - t0; ++j)
+      step(t0 + j, s_in[j * Tl::P + rl], EWM ? 0.0 : s_out[j * Tl::P + rl], std::false_type{});
   }
 }
 
@@ -393,26 +471,27 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
 // (the job is copied out of the kernel arguments once: read through a
 // reference, its fields are re-loaded from memory at every step)
 template <int CLS, int SPW>
-__global__ __launch_bounds__(WAVE) void replay_restage_kernel(const RollBatch B) {
-  __shared__ double s_in[ReplayTile<SPW>::N];
-  __shared__ double s_out[ReplayTile<SPW>::N];
+__global__ __launch_bounds__(WAVE, BQ_RS_WPS) void replay_restage_kernel(const RollBatch B) {
+  __shared__ double s_in[ReplayTile<SPW, BQ_RS_V>::N];
+  __shared__ double s_out[ReplayTile<SPW, BQ_RS_V>::N];
   const RollJob A = B.j[blockIdx.y];
-  replay_restage_body<CLS, SPW>(A, B, s_in, s_out);
+  replay_restage_body<CLS, SPW, BQ_RS_V>(A, B, s_in, s_out);
 }
 
 // jobs of any class in one launch (wave-uniform switch on the job's class):
 // for batches that do not fill the chip, where per-class launches would run
 // one latency-bound replay after the other
 template <int SPW>
-__global__ __launch_bounds__(WAVE) void replay_mixed_kernel(const RollBatch B) {
-  __shared__ double s_in[ReplayTile<SPW>::N];
-  __shared__ double s_out[ReplayTile<SPW>::N];
+__global__ __launch_bounds__(WAVE, BQ_RS_WPS_MIXED) void replay_mixed_kernel(const RollBatch B) {
+  constexpr int V = SPW >= 16 ? BQ_RS_V_MIXED : BQ_RS_V;   // chunks of >= 8 candles for SPW < 16
+  __shared__ double s_in[ReplayTile<SPW, V>::N];
+  __shared__ double s_out[ReplayTile<SPW, V>::N];
   const RollJob A = B.j[blockIdx.y];
   switch (replay_class(A.mode)) {
-    case 0: replay_restage_body<0, SPW>(A, B, s_in, s_out); break;
-    case 1: replay_restage_body<1, SPW>(A, B, s_in, s_out); break;
-    case 2: replay_restage_body<2, SPW>(A, B, s_in, s_out); break;
-    default: replay_restage_body<3, SPW>(A, B, s_in, s_out);
+    case 0: replay_restage_body<0, SPW, V>(A, B, s_in, s_out); break;
+    case 1: replay_restage_body<1, SPW, V>(A, B, s_in, s_out); break;
+    case 2: replay_restage_body<2, SPW, V>(A, B, s_in, s_out); break;
+    default: replay_restage_body<3, SPW, V>(A, B, s_in, s_out);
   }
 }
 
