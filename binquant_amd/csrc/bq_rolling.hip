@@ -966,15 +966,18 @@ int replay_impl(int nclasses, int64_t waves64) {
 }
 
 // symbols per wave of the re-staged replays: 64. BQ_REPLAY_SPW=32|16|8
-// forces fewer (measurement: spreading 12.5k symbols over 2-8x as many
-// waves did not shorten the replay — the step cost is the wave's own
-// instruction stream, not a shortage of waves — tools/replay_ab.sh).
-int replay_spw() {
+// forces fewer (measurement: spreading the rows over 2-4x as many waves did
+// not shorten the replay even for small batches — ADX's 3 series over 12.5k
+// symbols (588 waves of 64) took 1.12 ms at 64 and 1.49 ms at 16 symbols per
+// wave: the step cost is the wave's own instruction stream, not a shortage of
+// waves — tools/spw_ab.sh, tools/replay_ab.sh).
+int replay_spw(int64_t waves64) {
   static const int forced = [] {
     const char* e = getenv("BQ_REPLAY_SPW");
     const int v = e ? atoi(e) : 0;
     return (v == 32 || v == 16 || v == 8) ? v : 64;
   }();
+  (void)waves64;
   return forced;
 }
 
@@ -992,7 +995,7 @@ void launch_restage(int cls, const bq::RollBatch& B, int n, hipStream_t st) {
 
 // cls 0-3: one class; 4: mixed
 void launch_restage_any(int cls, const bq::RollBatch& B, int n, hipStream_t st) {
-  switch (replay_spw()) {
+  switch (replay_spw((B.S + bq::WAVE - 1) / bq::WAVE * n)) {
     case 64: launch_restage<64>(cls, B, n, st); break;
     case 32: launch_restage<32>(cls, B, n, st); break;
     case 16: launch_restage<16>(cls, B, n, st); break;

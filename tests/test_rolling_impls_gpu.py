@@ -32,6 +32,8 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
         "lane_ring": _run(tmp_path, "lane_ring", {"BQ_RANK_IMPL": "lane", "BQ_REPLAY_IMPL": "ring"}),
         "tile_restage": _run(tmp_path, "tile_restage", {"BQ_RANK_IMPL": "tile", "BQ_REPLAY_IMPL": "restage"}),
         "stencil_mixed": _run(tmp_path, "stencil_mixed", {"BQ_RANK_IMPL": "stencil", "BQ_REPLAY_IMPL": "mixed"}),
+        "restage64": _run(tmp_path, "restage64", {"BQ_REPLAY_IMPL": "restage", "BQ_REPLAY_SPW": "64"}),
+        "mixed32": _run(tmp_path, "mixed32", {"BQ_REPLAY_IMPL": "mixed", "BQ_REPLAY_SPW": "32"}),
         "auto": _run(tmp_path, "auto", {}),
     }
     ref = runs["auto"]
