@@ -1,8 +1,9 @@
 // Native fused element-wise programs: each validated bq_fused_program is
 // translated into straight-line HIP source (one SSA value per instruction,
-// constants as exact bit patterns, operand layouts specialised), compiled for
-// gfx950 with hiprtc once per program structure, and launched as an ordinary
-// kernel. The interpreter in bq_fused.hip decodes every instruction per
+// operand layouts specialised), compiled for gfx950 with hiprtc once per
+// program STRUCTURE and launched as an ordinary kernel. Constants travel in
+// the kernel arguments (exact doubles), not in the source: a stage called
+// with new threshold values every message reuses its compiled kernel. The interpreter in bq_fused.hip decodes every instruction per
 // element group and keeps program registers in LDS; here the compiler
 // allocates VGPRs and schedules the loads, so a stage costs its HBM traffic
 // plus the arithmetic, not the decode.
@@ -40,6 +41,7 @@ struct JitArgs {
   long long ss_in[BQ_FUSED_MAX_IN], st_in[BQ_FUSED_MAX_IN];
   void* out[BQ_FUSED_MAX_OUT];
   long long ss_out[BQ_FUSED_MAX_OUT], st_out[BQ_FUSED_MAX_OUT];
+  double c[BQ_FUSED_MAX_CONST];
   int T, nbt;
 };
 
@@ -49,16 +51,9 @@ const char* kArgsDecl =
     "  long long ss_in[" BQ_STR(BQ_FUSED_MAX_IN) "], st_in[" BQ_STR(BQ_FUSED_MAX_IN) "];\n"
     "  void* out[" BQ_STR(BQ_FUSED_MAX_OUT) "];\n"
     "  long long ss_out[" BQ_STR(BQ_FUSED_MAX_OUT) "], st_out[" BQ_STR(BQ_FUSED_MAX_OUT) "];\n"
+    "  double c[" BQ_STR(BQ_FUSED_MAX_CONST) "];\n"
     "  int T, nbt;\n"
     "};\n";
-
-std::string dlit(double v) {
-  uint64_t u;
-  memcpy(&u, &v, 8);
-  char b[64];
-  snprintf(b, sizeof b, "__builtin_bit_cast(double, 0x%016llxull)", (unsigned long long)u);
-  return b;
-}
 
 // stride_t class of an operand: 1 (contiguous along t), 0 (one value per symbol), else general
 int tclass(int64_t st) { return st == 1 ? 1 : st == 0 ? 0 : 2; }
@@ -121,7 +116,7 @@ std::string generate(const bq_fused_program& P) {
   snprintf(b, sizeof b, "  const int t0 = (int)(blockIdx.x %% a.nbt) * (%d * K) + threadIdx.x;\n", JIT_NT);
   s += b;
   for (int j = 0; j < P.n_const; ++j) {
-    snprintf(b, sizeof b, "  const double C%d = %s;\n", j, dlit(P.consts[j]).c_str());
+    snprintf(b, sizeof b, "  const double C%d = a.c[%d];\n", j, j);
     s += b;
   }
   // loads (every LD instruction, wherever the program placed it)
@@ -380,6 +375,7 @@ int fused_native_eval(const bq_fused_program& P, int64_t S, int64_t T, hipStream
     A.ss_out[i] = P.out[i].stride_s;
     A.st_out[i] = P.out[i].stride_t;
   }
+  memcpy(A.c, P.consts, sizeof(A.c));
   A.T = (int)T;
   const int span = JIT_NT * K;
   A.nbt = (int)((T + span - 1) / span);

@@ -116,3 +116,23 @@ def test_native_equals_interpreter_bits(cuda, S, T):
             assert torch.equal(torch.isnan(a), nan), name
             a, b = a[~nan].view(torch.int64), b[~nan].view(torch.int64)
         assert torch.equal(a, b), name
+
+
+def test_native_constants_are_arguments(cuda):
+    """A stage re-run with new constant values (thresholds that change per
+    message) reuses its compiled kernel and uses the new values exactly."""
+    F.set_native(True)
+    try:
+        S, T = 16, 300
+        x = random_panel(S, T, seed=3).cuda()
+        X = F.inp(x)
+        F.run({"y": F.where(X > 0.25, X * 1.5, -X) + 1e-3}, S, T)
+        before = F.native_stats()
+        for thr, k, c in ((0.5, 2.0, 0.125), (-1.0, 1.0 / 3.0, 7.0)):
+            got = F.run({"y": F.where(X > thr, X * k, -X) + c}, S, T)["y"]
+            want = torch.where(x > thr, x * k, -x) + c
+            assert_same("y", got.cpu().numpy(), want.cpu().numpy())
+        after = F.native_stats()
+        assert after["compiles"] == before["compiles"] and after["cached"] == before["cached"]
+    finally:
+        F.set_native(None)
