@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import struct
+from collections import OrderedDict
 from dataclasses import dataclass, field
 
 import torch
@@ -379,6 +380,94 @@ def _plan(outputs: list[tuple[str, Ex]]) -> list[Program]:
     return _plan(outputs[:h]) + _plan(outputs[h:])
 
 
+# ---- plan cache ----------------------------------------------------------
+# The strategies rebuild the same expression structure on every eager call
+# with new tensors. build() is a deterministic function of the canonical DAG,
+# the equality pattern of the operands and the constants' bits, so the plan is
+# cached under exactly that key; a hit only rebinds the operand tensors and
+# the output names (the register allocation and encoding are skipped).
+
+_PLAN_CACHE: OrderedDict = OrderedDict()
+_PLAN_CACHE_MAX = 512
+_PLAN_CACHE_ON = __import__("os").environ.get("BQ_FUSED_PLAN_CACHE", "1") != "0"
+_plan_stats = {"hits": 0, "misses": 0}
+
+
+@dataclass
+class _Template:
+    """A Program with its operands as slots of the request's distinct
+    operands and its outputs as positions in the request."""
+    ins: list
+    consts: list
+    n_loads: int
+    n_regs: int
+    slots: tuple
+    outs: tuple
+
+
+def _structure(outputs: list[tuple[str, Ex]]) -> tuple[tuple, list[torch.Tensor], dict]:
+    """(key, operands in slot order, slot of each operand key) of a request:
+    the canonical DAG with every load naming its operand's slot (first-seen
+    order) instead of the tensor, and each output's node and kind."""
+    order, mapped = _canon([e.node for _, e in outputs])
+    pos: dict[int, int] = {}
+    slot_of: dict = {}
+    tensors: list[torch.Tensor] = []
+    desc = []
+    for i, n in enumerate(order):
+        pos[id(n)] = i
+        op = n.op
+        if op == "LD":
+            k = n.key[1]   # _operand_key(n.tensor), computed when the load was made
+            s = slot_of.get(k)
+            if s is None:
+                s = slot_of[k] = len(tensors)
+                tensors.append(n.tensor)
+            desc.append(("LD", s, n.shift, _bits(n.value), n.tensor.dtype, n.tensor.dim()))
+        elif op == "CONST":
+            desc.append(("C", _bits(n.value)))
+        elif op == "INRANGE":
+            desc.append(("R", n.shift))
+        else:
+            desc.append((op,) + tuple(pos[id(a)] for a in n.args))
+    key = (tuple(desc), tuple((pos[id(mapped[id(e.node)])], e.kind) for _, e in outputs))
+    return key, tensors, slot_of
+
+
+def _plan_cached(outputs: list[tuple[str, Ex]]) -> list[Program]:
+    """_plan(outputs), reusing the plan of an earlier request of the same
+    structure (equal Programs: same instructions, constants, operand order)."""
+    if not _PLAN_CACHE_ON:
+        return _plan(outputs)
+    key, tensors, slot_of = _structure(outputs)
+    tpls = _PLAN_CACHE.get(key)
+    if tpls is None:
+        _plan_stats["misses"] += 1
+        progs = _plan(outputs)
+        where = {name: j for j, (name, _) in enumerate(outputs)}
+        tpls = [_Template(P.ins, P.consts, P.n_loads, P.n_regs,
+                          tuple(slot_of[_operand_key(t)] for t in P.inputs),
+                          tuple((where[name], kind) for name, kind in P.outputs)) for P in progs]
+        _PLAN_CACHE[key] = tpls
+        if len(_PLAN_CACHE) > _PLAN_CACHE_MAX:
+            _PLAN_CACHE.popitem(last=False)
+        return progs
+    _plan_stats["hits"] += 1
+    _PLAN_CACHE.move_to_end(key)
+    return [Program(ins=t.ins, n_loads=t.n_loads, n_regs=t.n_regs, consts=t.consts,
+                    inputs=[tensors[s] for s in t.slots],
+                    outputs=[(outputs[j][0], kind) for j, kind in t.outs]) for t in tpls]
+
+
+def plan_cache_stats() -> dict[str, int]:
+    return dict(_plan_stats, entries=len(_PLAN_CACHE))
+
+
+def clear_plan_cache() -> None:
+    _PLAN_CACHE.clear()
+    _plan_stats.update(hits=0, misses=0)
+
+
 def _operand(t: torch.Tensor, S: int, T: int, out: bool = False) -> _lib.BqFusedOperand:
     dt = _lib.FUSED_U8 if t.dtype == torch.bool else _lib.FUSED_F64
     if t.dim() == 1:
@@ -400,10 +489,8 @@ def _abi(P: Program, outs: list[torch.Tensor], S: int, T: int) -> _lib.BqFusedPr
     prog = _lib.BqFusedProgram()
     prog.n_ins, prog.n_loads, prog.n_regs = len(P.ins), P.n_loads, P.n_regs
     prog.n_in, prog.n_out, prog.n_const = len(P.inputs), len(outs), len(P.consts)
-    for i, w in enumerate(P.ins):
-        prog.ins[i] = w
-    for i, v in enumerate(P.consts):
-        prog.consts[i] = v
+    prog.ins[:len(P.ins)] = P.ins
+    prog.consts[:len(P.consts)] = P.consts
     for i, t in enumerate(P.inputs):
         prog.inp[i] = _operand(t, S, T)
     for i, t in enumerate(outs):
@@ -460,6 +547,7 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
     res: dict[str, torch.Tensor] = {}
     todo: list[tuple[str, Ex]] = []
     shapes = []
+    seen: set = set()   # shared subexpressions are walked once for all outputs
     for name, e in outputs.items():
         if isinstance(e, torch.Tensor):
             res[name] = e
@@ -470,7 +558,7 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
         if n.op == "LD" and n.shift == 0 and n.tensor.dim() == 2 and (e.kind == "b") == (n.tensor.dtype == torch.bool):
             res[name] = n.tensor   # identity (shape checked below with the others)
         todo.append((name, e))
-        _collect_shapes(n, shapes, set())
+        _collect_shapes(n, shapes, seen)
     if S is None or T is None:
         if not shapes:
             raise ValueError("cannot infer [S, T] from constants: pass S and T")
@@ -493,7 +581,7 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
     if torch.device(dev).type != "cuda":
         raise RuntimeError("fused evaluation needs a HIP device (no CPU fallback)")
     lib = _lib.load()
-    plans = _plan(todo)
+    plans = _plan_cached(todo)
     if _TRACE:
         import sys
         for P in plans:

@@ -108,3 +108,46 @@ def test_native_source_rejects_invalid_program():
     n = __import__("ctypes").c_int64()
     assert _lib.load().bq_fused_source(prog, None, 0, n) == _lib.BQ_EINVAL
     assert _lib.load().bq_fused_compile(prog) == _lib.BQ_EINVAL
+
+
+def _same_programs(a, b):
+    assert len(a) == len(b)
+    for p, q in zip(a, b):
+        assert list(p.ins) == list(q.ins) and list(p.consts) == list(q.consts)
+        assert (p.n_loads, p.n_regs, p.outputs) == (q.n_loads, q.n_regs, q.outputs)
+        assert len(p.inputs) == len(q.inputs) and all(s is t for s, t in zip(p.inputs, q.inputs))
+
+
+def test_plan_cache_rebinds_operands_exactly():
+    """A cached plan equals a fresh build for a new request of the same
+    structure (new tensors, new output names); operand aliasing and constant
+    values are part of the key."""
+    F.clear_plan_cache()
+    items = list(expressions(*_operands()).items())
+    _same_programs(F._plan_cached(items), F._plan(items))
+    assert F.plan_cache_stats()["misses"] == 1
+    # same structure over other tensors and names: a hit, equal to a fresh build
+    ops2 = [random_panel(S, T, seed=k + 20) for k in range(3)] + list(_operands()[3:])
+    items2 = [(name + "_2", e) for name, e in expressions(*ops2).items()]
+    got = F._plan_cached(items2)
+    assert F.plan_cache_stats()["hits"] == 1
+    _same_programs(got, F._plan(items2))
+    res = {}
+    for P in got:
+        res.update(interpret(P, S, T))
+    for name, e in items2:
+        assert_same(name[:-2], res[name], torch_eval(e, S, T).numpy())
+    # aliasing changes the program (one operand instead of two): a miss
+    x, y = random_panel(S, T, seed=1), random_panel(S, T, seed=2)
+    F._plan_cached([("s", F.inp(x) + F.inp(y))])
+    m = F.plan_cache_stats()["misses"]
+    P = F._plan_cached([("s", F.inp(x) + F.inp(x))])
+    assert F.plan_cache_stats()["misses"] == m + 1 and len(P[0].inputs) == 1
+    np.testing.assert_array_equal(interpret(P[0], S, T)["s"], (x + x).numpy())
+    # a new constant value is a new key
+    F._plan_cached([("s", F.inp(x) * 2.0)])
+    P = F._plan_cached([("s", F.inp(y) * 3.0)])
+    assert F.plan_cache_stats()["misses"] == m + 3
+    np.testing.assert_array_equal(interpret(P[0], S, T)["s"], (y * 3.0).numpy())
+    P = F._plan_cached([("t", F.inp(x) * 3.0)])
+    assert F.plan_cache_stats()["misses"] == m + 3 and P[0].inputs[0] is x
