@@ -407,31 +407,37 @@ class _Template:
 
 def _structure(outputs: list[tuple[str, Ex]]) -> tuple[tuple, list[torch.Tensor], dict]:
     """(key, operands in slot order, slot of each operand key) of a request:
-    the canonical DAG with every load naming its operand's slot (first-seen
-    order) instead of the tensor, and each output's node and kind."""
-    order, mapped = _canon([e.node for _, e in outputs])
+    the recorded DAG (post-order, shared nodes once) with every load naming
+    its operand's slot (first-seen order) instead of the tensor, and each
+    output's node and kind. _canon and build are deterministic functions of
+    exactly this, so equal keys give equal plans up to the operand tensors
+    (structurally equal but unshared subtrees only cost an extra miss)."""
     pos: dict[int, int] = {}
     slot_of: dict = {}
     tensors: list[torch.Tensor] = []
-    desc = []
-    for i, n in enumerate(order):
-        pos[id(n)] = i
-        op = n.op
-        if op == "LD":
+    desc: list = []
+
+    def visit(n: _Node) -> int:
+        p = pos.get(id(n))
+        if p is not None:
+            return p
+        if n.args:
+            d = (n.op,) + tuple(visit(a) for a in n.args)
+        elif n.op == "LD":
             k = n.key[1]   # _operand_key(n.tensor), computed when the load was made
             s = slot_of.get(k)
             if s is None:
                 s = slot_of[k] = len(tensors)
                 tensors.append(n.tensor)
-            desc.append(("LD", s, n.shift, _bits(n.value), n.tensor.dtype, n.tensor.dim()))
-        elif op == "CONST":
-            desc.append(("C", _bits(n.value)))
-        elif op == "INRANGE":
-            desc.append(("R", n.shift))
+            d = ("LD", s, n.shift, n.key[3], n.tensor.dtype, n.tensor.dim())
         else:
-            desc.append((op,) + tuple(pos[id(a)] for a in n.args))
-    key = (tuple(desc), tuple((pos[id(mapped[id(e.node)])], e.kind) for _, e in outputs))
-    return key, tensors, slot_of
+            d = n.key   # CONST bits / INRANGE shift
+        p = pos[id(n)] = len(desc)
+        desc.append(d)
+        return p
+
+    outs = tuple((visit(e.node), e.kind) for _, e in outputs)
+    return (tuple(desc), outs), tensors, slot_of
 
 
 def _plan_cached(outputs: list[tuple[str, Ex]]) -> list[Program]:

@@ -247,3 +247,51 @@ def test_integer_sum_matches_replayed_sum_bitwise(cuda, S, T):
         for (w, mp, sh), a in zip(jobs, got):
             ref = pd.DataFrame(xs.T).shift(sh).rolling(w, min_periods=mp).sum().to_numpy().T
             np.testing.assert_array_equal(a[:4].cpu().numpy(), ref, err_msg=f"pandas w={w}")
+
+
+def test_plan_cache_hits_are_bit_exact(cuda):
+    """Eager pipelines reuse cached fused plans (binquant_amd.fused plan
+    cache): a second panel of the same shape hits the cache (data-dependent
+    constants, if any, are new keys), and every output
+    equals the same call with the cache disabled, bit for bit."""
+    from binquant_amd import fused as F
+    from binquant_amd import signals, strategies
+    from binquant_amd.synth import device_panel
+
+    calls = {
+        "burst": lambda o, h, l, c, v: strategies.activity_burst_features(o, h, l, c, v, v * c),
+        "spike": lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c),
+        "pump": lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0].clone()),
+        "gainer": lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c),
+    }
+    for seed, (name, fn) in enumerate(calls.items()):
+        p = device_panel(48, 300, seed=seed)
+        args = [p[k] for k in ("open", "high", "low", "close", "volume")]
+        fn(*args)   # populates the cache
+        before = F.plan_cache_stats()
+        p2 = device_panel(48, 300, seed=seed + 100)
+        args2 = [p2[k] for k in ("open", "high", "low", "close", "volume")]
+        hot = fn(*args2)
+        after = F.plan_cache_stats()
+        assert after["hits"] > before["hits"], name
+        F._PLAN_CACHE_ON = False
+        try:
+            cold = fn(*args2)
+        finally:
+            F._PLAN_CACHE_ON = True
+        _assert_same_tree(hot, cold, name)
+
+
+def _assert_same_tree(a, b, path):
+    if isinstance(b, dict):
+        assert isinstance(a, dict) and set(a) == set(b), path
+        for k in b:
+            _assert_same_tree(a[k], b[k], f"{path}.{k}")
+    elif isinstance(b, (tuple, list)):
+        assert len(a) == len(b), path
+        for i, (x, y) in enumerate(zip(a, b)):
+            _assert_same_tree(x, y, f"{path}[{i}]")
+    else:
+        x, y = a.cpu().numpy(), b.cpu().numpy()
+        assert x.dtype == y.dtype, path
+        np.testing.assert_array_equal(x, y, err_msg=path)
