@@ -440,12 +440,13 @@ def _structure(outputs: list[tuple[str, Ex]]) -> tuple[tuple, list[torch.Tensor]
     return (tuple(desc), outs), tensors, slot_of
 
 
-def _plan_cached(outputs: list[tuple[str, Ex]]) -> list[Program]:
+def _plan_cached(outputs: list[tuple[str, Ex]], structure=None) -> list[Program]:
     """_plan(outputs), reusing the plan of an earlier request of the same
-    structure (equal Programs: same instructions, constants, operand order)."""
+    structure (equal Programs: same instructions, constants, operand order).
+    ``structure`` is _structure(outputs) when the caller already has it."""
     if not _PLAN_CACHE_ON:
         return _plan(outputs)
-    key, tensors, slot_of = _structure(outputs)
+    key, tensors, slot_of = structure if structure is not None else _structure(outputs)
     tpls = _PLAN_CACHE.get(key)
     if tpls is None:
         _plan_stats["misses"] += 1
@@ -552,8 +553,6 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
     [S, T] operand are returned as that tensor (no copy)."""
     res: dict[str, torch.Tensor] = {}
     todo: list[tuple[str, Ex]] = []
-    shapes = []
-    seen: set = set()   # shared subexpressions are walked once for all outputs
     for name, e in outputs.items():
         if isinstance(e, torch.Tensor):
             res[name] = e
@@ -564,30 +563,31 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
         if n.op == "LD" and n.shift == 0 and n.tensor.dim() == 2 and (e.kind == "b") == (n.tensor.dtype == torch.bool):
             res[name] = n.tensor   # identity (shape checked below with the others)
         todo.append((name, e))
-        _collect_shapes(n, shapes, seen)
+    # one walk gives the cache key and the distinct operands (their shapes
+    # broadcast to [S, T]; the first one names the device)
+    struct = _structure(todo) if todo else None
+    operands = struct[1] if struct else []
     if S is None or T is None:
-        if not shapes:
+        if not operands:
             raise ValueError("cannot infer [S, T] from constants: pass S and T")
+        shapes = [tuple(t.shape) if t.dim() == 2 else (1, t.shape[0]) for t in operands]
         S = max(sh[0] for sh in shapes) if S is None else S   # broadcast shape of the operands
         T = max(sh[1] for sh in shapes) if T is None else T
-    todo = [(k, e) for k, e in todo if not (k in res and tuple(res[k].shape) == (S, T))]
-    for k, _ in todo:
+    kept = [(k, e) for k, e in todo if not (k in res and tuple(res[k].shape) == (S, T))]
+    for k, _ in kept:
         res.pop(k, None)
-    if not todo:
+    if not kept:
         return res
+    if len(kept) != len(todo):
+        todo, struct = kept, _structure(kept)
     dev = device
     if dev is None:
-        for name, e in todo:
-            t = _first_tensor(e.node)
-            if t is not None:
-                dev = t.device
-                break
-    if dev is None:
-        dev = torch.device("cuda")
-    if torch.device(dev).type != "cuda":
+        dev = operands[0].device if operands else torch.device("cuda")
+    dev = torch.device(dev)
+    if dev.type != "cuda":
         raise RuntimeError("fused evaluation needs a HIP device (no CPU fallback)")
     lib = _lib.load()
-    plans = _plan_cached(todo)
+    plans = _plan_cached(todo, struct)
     if _TRACE:
         import sys
         for P in plans:
@@ -600,32 +600,10 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
             res[name] = t
             outs.append(t)
         for t in P.inputs:
-            if t.device != torch.device(dev) and not (t.is_cuda and torch.device(dev).type == "cuda"):
+            if not t.is_cuda:
                 raise ValueError("fused operands must be on the evaluation device")
         prog = _abi(P, outs, S, T)
         _lib.check(lib.bq_fused_eval(ctypes.byref(prog), S, T, engine._stream_handle(stream)), "bq_fused_eval")
         # keep the operands alive until the launch is ordered on the stream
         del prog
     return {k: res[k] for k in outputs}
-
-
-def _collect_shapes(n: _Node, acc: list, seen: set):
-    if id(n) in seen:
-        return
-    seen.add(id(n))
-    if n.op == "LD":
-        t = n.tensor
-        acc.append(tuple(t.shape) if t.dim() == 2 else (1, t.shape[0]))
-    for a in n.args:
-        _collect_shapes(a, acc, seen)
-
-
-def _first_tensor(n: _Node):
-    if n.op == "LD":
-        return n.tensor
-    for a in n.args:
-        t = _first_tensor(a)
-        if t is not None:
-            return t
-    return None
-
