@@ -380,6 +380,58 @@ __global__ __launch_bounds__(BR_TW * BR_NW) void breadth_kernel(const BreadthArg
   }
 }
 
+// Few timestamps (the live tick: T = 1). The kernel above gives one lane per
+// timestamp, so at T = 1 each of its 16 waves walks S / 16 symbols with one
+// active lane (≈0.5 ms at S = 10k). Here a workgroup of BS_NT threads owns one
+// timestamp: thread k sums symbols k, k + BS_NT, ... in ascending order, then
+// xor-butterflies over the wave and over the waves combine the threads. Again a
+// fixed, placement-independent order: bitwise reproducible run to run.
+constexpr int BS_NT = 1024;
+constexpr int BS_MAX_T = 256;
+
+__device__ __forceinline__ double wave_sum(double v, int width) {
+#pragma unroll
+  for (int d = WAVE / 2; d >= 1; d >>= 1)
+    if (d < width) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+
+__global__ __launch_bounds__(BS_NT) void breadth_small_kernel(const BreadthArgs A) {
+  __shared__ double sRed[BQ_NUM_PARTIALS][BS_NT / WAVE];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const int64_t t = blockIdx.x;
+  double acc[BQ_NUM_PARTIALS];
+#pragma unroll
+  for (int i = 0; i < BQ_NUM_PARTIALS; ++i) acc[i] = 0.0;
+  for (int64_t s = tid; s < A.S; s += BS_NT) {
+    const double r = A.f[BQ_F_RETURN][s * A.ld_f + t];
+    if (r != r) continue;   // no features at this t (history < 2 bars)
+    const double cl = A.c[s * A.ld_c + t];
+    acc[BQ_P_COUNT] += 1.0;
+    acc[BQ_P_ADV] += r > 0.0 ? 1.0 : 0.0;
+    acc[BQ_P_DEC] += r < 0.0 ? 1.0 : 0.0;
+    acc[BQ_P_ABOVE20] += cl > A.f[BQ_F_EMA20][s * A.ld_f + t] ? 1.0 : 0.0;
+    acc[BQ_P_ABOVE50] += cl > A.f[BQ_F_EMA50][s * A.ld_f + t] ? 1.0 : 0.0;
+    acc[BQ_P_SUM_RET] += r;
+    acc[BQ_P_SUM_TREND] += A.f[BQ_F_TREND][s * A.ld_f + t];
+    acc[BQ_P_SUM_ATR_PCT] += A.f[BQ_F_ATR_PCT][s * A.ld_f + t];
+    acc[BQ_P_SUM_BB_WIDTH] += A.f[BQ_F_BB_WIDTH][s * A.ld_f + t];
+  }
+#pragma unroll
+  for (int i = 0; i < BQ_NUM_PARTIALS; ++i) {
+    const double v = wave_sum(acc[i], WAVE);
+    if (lane == 0) sRed[i][w] = v;
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < BQ_NUM_PARTIALS; ++i) {
+      const double v = wave_sum(lane < BS_NT / WAVE ? sRed[i][lane] : 0.0, BS_NT / WAVE);
+      if (lane == 0) A.partial[t * BQ_NUM_PARTIALS + i] = v;
+    }
+  }
+}
+
 static double alpha_from_span(double span) {
   const double com = (span - 1.0) / 2.0;
   return 1.0 / (1.0 + com);
@@ -454,8 +506,12 @@ int bq_breadth_partial(const double* close, const double* const* feat, int64_t S
   A.ld_f = ld_feat;
   A.T = (int)T;
   A.partial = partial;
-  const unsigned blocks = (unsigned)((T + BR_TW - 1) / BR_TW);
-  hipLaunchKernelGGL(breadth_kernel, dim3(blocks), dim3(BR_TW * BR_NW), 0, (hipStream_t)stream, A);
+  if (T <= BS_MAX_T) {
+    hipLaunchKernelGGL(breadth_small_kernel, dim3((unsigned)T), dim3(BS_NT), 0, (hipStream_t)stream, A);
+  } else {
+    const unsigned blocks = (unsigned)((T + BR_TW - 1) / BR_TW);
+    hipLaunchKernelGGL(breadth_kernel, dim3(blocks), dim3(BR_TW * BR_NW), 0, (hipStream_t)stream, A);
+  }
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

@@ -123,3 +123,31 @@ def test_device_context_pipeline_matches_reference_golden(cuda, label):
                 assert got[k] == v, (k, got[k], v)
             else:
                 assert got[k] == pytest.approx(v, rel=1e-9, abs=1e-12), k
+
+
+@pytest.mark.parametrize("S,T", [(10_000, 1), (3000, 3), (1500, 256), (1500, 257), (5, 1)])
+def test_breadth_partial_few_timestamps(cuda, S, T):
+    """The few-timestamp path (T <= 256: one workgroup per timestamp, the live
+    tick's T = 1) and the boundary to the lane-per-timestamp path: counts
+    exact, sums within 1e-12 of numpy, NaN-return rows skipped, bitwise
+    reproducible run to run."""
+    g = np.random.default_rng(S + T)
+    c = g.uniform(1, 100, (S, T))
+    fn = {k: g.normal(0, 1, (S, T)) for k in FEATURE_COLUMNS}
+    fn["ema20"], fn["ema50"] = c * g.uniform(0.9, 1.1, (S, T)), c * g.uniform(0.9, 1.1, (S, T))
+    fn["return_pct"][g.random((S, T)) < 0.1] = np.nan
+    fn["return_pct"][:, 0][:3] = 0.0   # neither advancer nor decliner
+    f = {k: torch.from_numpy(v).cuda() for k, v in fn.items()}
+    part = engine.breadth_partial(torch.from_numpy(c).cuda(), f).cpu().numpy()
+    valid = ~np.isnan(fn["return_pct"])
+    np.testing.assert_array_equal(part[:, 0], valid.sum(axis=0))
+    np.testing.assert_array_equal(part[:, 1], (valid & (fn["return_pct"] > 0)).sum(axis=0))
+    np.testing.assert_array_equal(part[:, 2], (valid & (fn["return_pct"] < 0)).sum(axis=0))
+    np.testing.assert_array_equal(part[:, 3], (valid & (c > fn["ema20"])).sum(axis=0))
+    np.testing.assert_array_equal(part[:, 4], (valid & (c > fn["ema50"])).sum(axis=0))
+    for i, k in ((5, "return_pct"), (6, "trend_score"), (7, "atr_pct"), (8, "bb_width")):
+        want = np.where(valid, fn[k], 0.0).sum(axis=0)
+        assert_close(part[:, i], want, k, rtol=1e-12, scale=np.abs(np.where(valid, fn[k], 0)).sum(axis=0) + 1e-300)
+    np.testing.assert_array_equal(part[:, 9:], 0.0)
+    part2 = engine.breadth_partial(torch.from_numpy(c).cuda(), f).cpu().numpy()
+    np.testing.assert_array_equal(part, part2)
