@@ -271,27 +271,40 @@ struct FeatSel {
   double a20, om20, a50, om50;
 };
 
-__global__ __launch_bounds__(WAVE) void store_features_kernel(const StoreArgs V, const FeatSel F) {
+// Two waves per 64 symbols, one chain set each (the branch on the role is
+// wave-uniform): wave 0 replays the true range, the ATR roll_mean and both
+// EWMs, wave 1 the 20-bar roll_mean and roll_var of the close. The chains are
+// independent and each is the same operation sequence as one lane doing all of
+// them, so the results are unchanged bit for bit; a symbol's per-step work is
+// split over two waves (the replay is latency-bound: 10k symbols fill only 157
+// waves of 64). Wave 1 hands its mean / variance to wave 0 through LDS.
+constexpr int SF_NT = 2 * WAVE;
+
+__global__ __launch_bounds__(SF_NT) void store_features_kernel(const StoreArgs V, const FeatSel F) {
   __shared__ double sX[3][SF_CT * STG_PITCH];   // high, low, close chunk (transposed)
-  __shared__ double sTR[SF_ATR][WAVE];          // per-lane ring of true ranges
-  __shared__ double sCL[SF_BB][WAVE];           // per-lane ring of closes
+  __shared__ double sTR[SF_ATR][WAVE];          // per-symbol ring of true ranges (wave 0)
+  __shared__ double sCL[SF_BB][WAVE];           // per-symbol ring of closes (wave 1)
+  __shared__ double sMu[WAVE], sVar[WAVE];      // wave 1 -> wave 0 at the end
   __shared__ int sH[WAVE], sN[WAVE];
   __shared__ int64_t sRow[WAVE];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int role = threadIdx.x / WAVE;   // wave-uniform
   const int64_t i = (int64_t)blockIdx.x * WAVE + lane;
   const int M = V.M;
   int n = 0;
   if (i < F.n) {
     const int64_t s = F.slots[i];
     n = V.count[s];
-    sH[lane] = V.head[s];
-    sRow[lane] = s * (int64_t)M;
-  } else {
+    if (role == 0) {
+      sH[lane] = V.head[s];
+      sRow[lane] = s * (int64_t)M;
+    }
+  } else if (role == 0) {
     sH[lane] = 0;
     sRow[lane] = 0;
   }
-  sN[lane] = n;
-  int nmax = n;
+  if (role == 0) sN[lane] = n;
+  int nmax = n;   // equal in both waves: same symbols
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
   __syncthreads();
@@ -303,10 +316,10 @@ __global__ __launch_bounds__(WAVE) void store_features_kernel(const StoreArgs V,
   mid.init();
   double pc = qnan(), c_last = qnan(), c_prev = qnan();
   for (int t0 = 0; t0 < nmax; t0 += SF_CT) {
-    // coalesced chunk load: element e -> lane e / CT, candle e % CT of its ring
+    // coalesced chunk load: element e -> symbol e / CT, candle e % CT of its ring
 #pragma unroll
-    for (int q = 0; q < SF_CT; ++q) {
-      const int el = lane + WAVE * q;
+    for (int q = 0; q < SF_CT * WAVE / SF_NT; ++q) {
+      const int el = threadIdx.x + SF_NT * q;
       const int l = el / SF_CT, tt = el % SF_CT, t = t0 + tt;
       double vh = qnan(), vl = qnan(), vc = qnan();
       if (t < sN[l]) {
@@ -321,39 +334,51 @@ __global__ __launch_bounds__(WAVE) void store_features_kernel(const StoreArgs V,
     }
     __syncthreads();
     const int m = min(SF_CT, n - t0);
-    for (int j = 0; j < m; ++j) {
-      const int t = t0 + j;
-      const int x = j * STG_PITCH + lane;
-      const double h = sX[0][x], l = sX[1][x], c = sX[2][x];
-      const double tr = true_range(h, l, pc);
-      if (t == 0) var.init(c);
-      if (t >= SF_ATR) atr.remove(sTR[t % SF_ATR][lane]);
-      atr.add(tr);
-      sTR[t % SF_ATR][lane] = tr;
-      if (t >= SF_BB) {
-        const double old = sCL[t % SF_BB][lane];
-        mid.remove(old);
-        var.remove(old);
+    if (role == 0) {
+      for (int j = 0; j < m; ++j) {
+        const int t = t0 + j;
+        const int x = j * STG_PITCH + lane;
+        const double h = sX[0][x], l = sX[1][x], c = sX[2][x];
+        const double tr = true_range(h, l, pc);
+        if (t >= SF_ATR) atr.remove(sTR[t % SF_ATR][lane]);
+        atr.add(tr);
+        sTR[t % SF_ATR][lane] = tr;
+        e20.step(c, F.a20, F.om20);
+        e50.step(c, F.a50, F.om50);
+        c_prev = c_last;
+        c_last = c;
+        pc = c;
       }
-      mid.add(c);
-      var.add(c);
-      sCL[t % SF_BB][lane] = c;
-      e20.step(c, F.a20, F.om20);
-      e50.step(c, F.a50, F.om50);
-      c_prev = c_last;
-      c_last = c;
-      pc = c;
+    } else {
+      for (int j = 0; j < m; ++j) {
+        const int t = t0 + j;
+        const double c = sX[2][j * STG_PITCH + lane];
+        if (t == 0) var.init(c);
+        if (t >= SF_BB) {
+          const double old = sCL[t % SF_BB][lane];
+          mid.remove(old);
+          var.remove(old);
+        }
+        mid.add(c);
+        var.add(c);
+        sCL[t % SF_BB][lane] = c;
+      }
     }
     __syncthreads();
   }
-  if (i >= F.n) return;
+  if (role == 1) {
+    sMu[lane] = mid.value();
+    sVar[lane] = var.var0();
+  }
+  __syncthreads();
+  if (role != 0 || i >= F.n) return;
   double ret = qnan(), ema20 = qnan(), ema50 = qnan(), trend = qnan(), atr_pct = qnan(), bbw = qnan();
   if (n >= 2) {   // _compute_symbol_features returns None below 2 bars (:249-250)
     ema20 = e20.w;
     ema50 = e50.w;
     const double a = atr.value();
-    const double mu = mid.value();
-    double v = var.var0();
+    const double mu = sMu[lane];
+    double v = sVar[lane];
     const double sd = v == v ? sqrt(v) : 0.0;   // std(ddof=0).fillna(0)
     const double up = mu + (2.0 * sd), lo = mu - (2.0 * sd);
     ret = safe_pct(c_last, c_prev);
@@ -450,7 +475,7 @@ int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_s
   F.a50 = 1.0 / (1.0 + (50.0 - 1.0) / 2.0);
   F.om50 = 1.0 - F.a50;
   const unsigned blocks = (unsigned)((n_sel + WAVE - 1) / WAVE);
-  hipLaunchKernelGGL(store_features_kernel, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, to_args(st), F);
+  hipLaunchKernelGGL(store_features_kernel, dim3(blocks), dim3(SF_NT), 0, (hipStream_t)stream, to_args(st), F);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
