@@ -195,8 +195,11 @@ class DeviceMarketStateStore:
         cached = getattr(self, "_slot_cache", None)
         if cached is not None and cached[0] == key:
             return cached[1]
-        t = torch.tensor([self._slot(s) for s in symbols], dtype=torch.int64, device=self.device)
-        self._slot_cache = (key, t)
+        ids = [self._slot(s) for s in symbols]
+        t = torch.tensor(ids, dtype=torch.int64, device=self.device)
+        # strictly increasing ids (the symbols in registration order, as a
+        # steady feed sends them): one candle per slot, already in merge order
+        self._slot_cache = (key, t, all(a < b for a, b in zip(ids, ids[1:])))
         return t
 
     @property
@@ -204,35 +207,53 @@ class DeviceMarketStateStore:
         return len(self._names)
 
     # -- batched updates (device) ---------------------------------------------------
-    def update_slots(self, slots: torch.Tensor, ts: torch.Tensor, fields: Sequence[torch.Tensor], stream=None) -> None:
+    def update_slots(self, slots: torch.Tensor, ts: torch.Tensor, fields: Sequence[torch.Tensor], stream=None,
+                     unique_sorted: bool = False) -> None:
         """One launch for a batch of candles (arrival order; device tensors):
         rows with NaN close are dropped, each (slot, timestamp) keeps its LAST
-        row, runs are sorted by timestamp per slot, then merged into the rings."""
+        row, runs are sorted by timestamp per slot, then merged into the rings.
+        ``unique_sorted`` (internal: update_batch over a cached, strictly
+        increasing, registered slot list) skips the sorts and the dedupe, which
+        are the identity for such a batch."""
         slots = slots.to(self.device, torch.int64).reshape(-1)
         ts = ts.to(self.device, torch.int64).reshape(-1)
         fields = [x.to(self.device, torch.float64).reshape(-1) for x in fields]
         if len(fields) != len(INPUT_FIELDS) or any(x.numel() != slots.numel() for x in fields) or ts.numel() != slots.numel():
             raise ValueError("update_slots: slots, ts and the five OHLCV fields must have one entry per candle")
-        if slots.numel() and (int(slots.min()) < 0 or int(slots.max()) >= self.n_tracked):
-            raise ValueError("update_slots: slot out of range (register symbols first)")
         ok = ~torch.isnan(fields[INPUT_FIELDS.index("close")])
-        idx = torch.nonzero(ok).reshape(-1)
-        if idx.numel() == 0:
-            return
-        order = idx[torch.argsort(ts[idx], stable=True)]
-        order = order[torch.argsort(slots[order], stable=True)]
-        s2, t2 = slots[order], ts[order]
-        last_row = torch.ones_like(s2, dtype=torch.bool)
-        last_row[:-1] = (s2[1:] != s2[:-1]) | (t2[1:] != t2[:-1])
-        sel = order[last_row]
-        s3, t3 = slots[sel].contiguous(), ts[sel].contiguous()
-        f3 = [x[sel].contiguous() for x in fields]
-        _, counts = torch.unique_consecutive(s3, return_counts=True)
-        seg = torch.zeros(counts.numel() + 1, dtype=torch.int64, device=self.device)
-        seg[1:] = torch.cumsum(counts, 0)
+        if unique_sorted:
+            if not slots.numel():
+                return
+            if bool(ok.all()):
+                s3, t3, f3 = slots.contiguous(), ts.contiguous(), [x.contiguous() for x in fields]
+            else:
+                idx = torch.nonzero(ok).reshape(-1)
+                if idx.numel() == 0:
+                    return
+                s3, t3, f3 = slots[idx], ts[idx], [x[idx] for x in fields]
+            n_seg = s3.numel()
+            seg = torch.arange(n_seg + 1, dtype=torch.int64, device=self.device)
+        else:
+            if slots.numel() and (int(slots.min()) < 0 or int(slots.max()) >= self.n_tracked):
+                raise ValueError("update_slots: slot out of range (register symbols first)")
+            idx = torch.nonzero(ok).reshape(-1)
+            if idx.numel() == 0:
+                return
+            order = idx[torch.argsort(ts[idx], stable=True)]
+            order = order[torch.argsort(slots[order], stable=True)]
+            s2, t2 = slots[order], ts[order]
+            last_row = torch.ones_like(s2, dtype=torch.bool)
+            last_row[:-1] = (s2[1:] != s2[:-1]) | (t2[1:] != t2[:-1])
+            sel = order[last_row]
+            s3, t3 = slots[sel].contiguous(), ts[sel].contiguous()
+            f3 = [x[sel].contiguous() for x in fields]
+            _, counts = torch.unique_consecutive(s3, return_counts=True)
+            n_seg = counts.numel()
+            seg = torch.zeros(n_seg + 1, dtype=torch.int64, device=self.device)
+            seg[1:] = torch.cumsum(counts, 0)
         st = _lib.load().bq_store_update(
             ctypes.byref(self._view), ctypes.c_void_p(s3.data_ptr()), ctypes.c_void_p(t3.data_ptr()),
-            _lib.ptr_array([x.data_ptr() for x in f3]), ctypes.c_void_p(seg.data_ptr()), counts.numel(),
+            _lib.ptr_array([x.data_ptr() for x in f3]), ctypes.c_void_p(seg.data_ptr()), n_seg,
             engine._stream_handle(stream),
         )
         _lib.check(st, "bq_store_update")
@@ -242,7 +263,8 @@ class DeviceMarketStateStore:
         slots = self.slots_for(symbols)
         cols = torch.from_numpy(np.stack([np.asarray(x, dtype=np.float64) for x in (open_, high, low, close, volume)]))
         cols = cols.to(self.device)
-        self.update_slots(slots, torch.as_tensor(np.asarray(timestamp, dtype=np.int64)), list(cols))
+        self.update_slots(slots, torch.as_tensor(np.ascontiguousarray(timestamp, dtype=np.int64)), list(cols),
+                          unique_sorted=self._slot_cache[2])
 
     # -- reference API ----------------------------------------------------------------
     def update(self, symbol: str, candle: Mapping[str, Any] | pd.Series | pd.DataFrame) -> pd.DataFrame:

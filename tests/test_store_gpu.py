@@ -254,3 +254,37 @@ def test_sharded_accumulator_matches_single_rank(cuda):
     for r in range(2):
         for i, (a, b) in enumerate(zip(res[r], single)):
             compare_context(a, b, f"rank{r}.tick{i}")
+
+
+def test_batch_fast_path_equals_generic_update(cuda):
+    """update_batch over a repeated, registration-ordered symbol list (one
+    candle per slot: the sorts and the dedupe are skipped) leaves the same
+    rings as the generic sort / dedupe path, with NaN closes dropped and an
+    all-NaN tick ignored."""
+    from binquant_amd.market_regime.store import DeviceMarketStateStore
+
+    syms = [f"S{i:03d}USDT" for i in range(150)]
+    fast = DeviceMarketStateStore(max_bars_per_symbol=16, capacity=64)
+    slow = DeviceMarketStateStore(max_bars_per_symbol=16, capacity=64)
+    for s in syms:
+        fast._slot(s)
+        slow._slot(s)
+    rng = np.random.default_rng(7)
+    for k in range(24):
+        c = 100 * np.exp(rng.normal(0, 0.01, len(syms)))
+        if k % 5 == 2:
+            c[rng.random(len(syms)) < 0.2] = np.nan
+        if k == 9:
+            c[:] = np.nan
+        ts = np.full(len(syms), 900_000 * k)
+        fast.update_batch(syms, ts, c, c * 1.01, c * 0.99, c, np.full(len(syms), float(k)))
+        assert fast._slot_cache[2]
+        # the generic path: same candles, presented in reverse order
+        r = slice(None, None, -1)
+        slow.update_batch(syms[r], ts[r], c[r], (c * 1.01)[r], (c * 0.99)[r], c[r], np.full(len(syms), float(k)))
+        assert not slow._slot_cache[2]
+    a, b = fast.get_all_histories(), slow.get_all_histories()
+    assert set(a) == set(b) == set(syms)
+    for s in syms:
+        pd.testing.assert_frame_equal(a[s], b[s], check_exact=True)
+        assert len(a[s]) == 16
