@@ -71,9 +71,18 @@ class IndicatorParams:
         )
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+_cur_device = getattr(torch._C, "_cuda_getDevice", None)
+
+
 def _stream_handle(stream: torch.cuda.Stream | None) -> ctypes.c_void_p:
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+    """hipStream_t of `stream`, else of torch's current stream on the current
+    device (read without building a Stream object: this runs once per launch)."""
+    if stream is not None:
+        return ctypes.c_void_p(stream.cuda_stream)
+    if _raw_stream is not None and _cur_device is not None:
+        return ctypes.c_void_p(_raw_stream(_cur_device()))
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
 def _check_panel(x: torch.Tensor, name: str, shape=None) -> torch.Tensor:

@@ -136,3 +136,16 @@ def test_native_constants_are_arguments(cuda):
         assert after["compiles"] == before["compiles"] and after["cached"] == before["cached"]
     finally:
         F.set_native(None)
+
+
+def test_stream_handle_is_torch_current_stream(cuda):
+    """The launch stream read through the raw accessor is torch's current
+    stream, including inside a `torch.cuda.stream` context."""
+    from binquant_amd import engine
+
+    h = lambda st: engine._stream_handle(st).value or 0   # noqa: E731  (c_void_p(0).value is None)
+    assert h(None) == torch.cuda.current_stream().cuda_stream
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        assert h(None) == s.cuda_stream != 0
+    assert h(s) == s.cuda_stream
