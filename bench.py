@@ -1,20 +1,29 @@
 """Benchmark: symbol-candles/s for the full 14-column indicator set on MI355X.
 
-Workload per GPU (weak scaling): the C4 shard of BASELINE.json configs[3] —
-12 500 symbols x 10 000 candles of synthetic fp64 OHLCV resident in HBM; at 8
-GPUs that is the 100k x 10k configuration. One step = one bq_enrich launch
-over the rank's shard (reads 5 inputs, writes 14 columns). Ranks share no data
+Headline workload: BASELINE.json configs[3] — 100 000 symbols x 10 000 candles
+of synthetic fp64 OHLCV resident in HBM, sharded by symbol over the N ranks
+(contiguous blocks, market_regime.batch.shard_bounds). At N = 1 the whole
+100k x 10k panel sits on one GPU (5 inputs = 40 GB + 14 outputs = 112 GB of
+288 GB); at N = 8 each GPU holds the 12 500-symbol C4 shard. Total work is
+fixed as N grows ("scaling": "strong"). One step = one bq_enrich launch over
+the rank's shard (reads 5 inputs, writes 14 columns). Ranks share no data
 (symbols are independent); the only collective is the MAX of the timings.
 
 Also reported (same JSON line):
-  roofline     — algorithmic bytes (152 B/candle) / mean kernel time (HIP
-                 events on the launch stream) vs 8 TB/s HBM peak; traffic from
-                 the committed rocprofv3 PMC summary when present;
-  cpu_baseline — the oracle's pandas per-symbol path (the reference call
-                 pattern) on the host cores, rank 0 at N=1, time-bounded sample;
+  roofline     — algorithmic bytes (152 B/candle) / mean enrich_kernel time
+                 (HIP events on the launch stream) vs 8 TB/s HBM peak; traffic
+                 from the committed rocprofv3 PMC summary of this workload;
+  shard        — the fixed 12 500 x 10 000 C4 shard per GPU (weak-scaling
+                 figure, same kernel);
+  cpu_baseline — the oracle's pandas per-symbol path in the reference's call
+                 pattern at C1 (500-candle frame: indicators_enrichment +
+                 _compute_symbol_features per symbol) over a
+                 process pool sized to the host's CPU share, rank 0 at N=1,
+                 time-bounded sample;
   tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
                  latency p50/p99;
-  breadth      — C5 leg (market features + breadth partials + RCCL all-reduce);
+  breadth      — C5 leg (market features + breadth partials + ONE all-reduce
+                 of the [T x 10] partials, tracked count folded in);
   rows         — every other SURVEY §8 row on the device at 12 500 x 2 000
                  (HIP-event time per call, algorithmic bytes -> GB/s and
                  fraction of HBM peak) with a bounded CPU timing of the
@@ -40,6 +49,7 @@ sys.path.insert(0, ROOT)
 
 from binquant_amd import engine  # noqa: E402
 from binquant_amd._lib import ENRICH_COLUMNS  # noqa: E402
+from binquant_amd.market_regime.batch import reduce_partials, shard_bounds  # noqa: E402
 from binquant_amd.synth import device_panel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -51,16 +61,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--symbols", type=int, default=12_500, help="symbols per GPU")
+    ap.add_argument("--symbols", type=int, default=100_000, help="total symbols, sharded over the ranks")
     ap.add_argument("--candles", type=int, default=10_000)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--shard-symbols", type=int, default=12_500, help="per-GPU symbols of the weak-scaling leg")
+    ap.add_argument("--shard-steps", type=int, default=10)
+    ap.add_argument("--no-shard", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: the host's CPU share (see host_cores)")
+    ap.add_argument("--cpu-candles", type=int, default=500, help="C1 frame length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tick-symbols", type=int, default=10_000)
     ap.add_argument("--ticks", type=int, default=2000)
     ap.add_argument("--no-tick", action="store_true")
     ap.add_argument("--no-breadth", action="store_true")
-    ap.add_argument("--breadth-steps", type=int, default=5)
+    ap.add_argument("--breadth-steps", type=int, default=3)
     ap.add_argument("--no-rows", action="store_true")
     ap.add_argument("--row-symbols", type=int, default=12_500)
     ap.add_argument("--row-candles", type=int, default=2_000)
@@ -94,13 +108,18 @@ def max_over_ranks(x: float, world: int) -> float:
 
 
 def _cpu_worker(args):
-    """One host process: reference call pattern (one pandas frame per symbol,
-    oracle.indicators_ref.indicators_enrichment) until the time budget ends."""
+    """One host process: the reference's per-message call pattern at C1 — one
+    pandas frame per symbol through indicators_enrichment
+    (producers/context_evaluator.py:240-263, oracle restatement) plus
+    _compute_symbol_features on the store's last 400 bars
+    (market_regime/live_market_context_accumulator.py:244-297) — until the
+    time budget ends."""
     seed, T, budget = args
     import pandas as pd
 
     from binquant_amd.synth import numpy_symbol
     from oracle import indicators_ref as ref
+    from oracle import market_ref
 
     done, spent, s = 0, 0.0, 0
     while spent < budget:
@@ -108,16 +127,45 @@ def _cpu_worker(args):
         df = pd.DataFrame(sym)
         t0 = time.perf_counter()
         ref.indicators_enrichment(df)
+        market_ref.symbol_features(sym["high"][-400:], sym["low"][-400:], sym["close"][-400:])
         spent += time.perf_counter() - t0
         done += T
         s += 1
     return done, spent, s
 
 
-def cpu_baseline(args, T):
+def host_cores() -> dict:
+    """The host CPU share this process may use: the cgroup CPU quota when one
+    is set, else the scheduler affinity mask; os.cpu_count() (the whole
+    machine) is reported beside it. On the GPU pool the box's share is also
+    published as OMP_NUM_THREADS, which caps the count when present."""
+    total = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    share = quota if quota is not None else affinity
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    return {"os_cpu_count": total, "affinity": affinity, "cgroup_quota": quota,
+            "omp_num_threads": int(omp) if omp.isdigit() else None, "share": max(1, share)}
+
+
+def cpu_baseline(args):
     import multiprocessing as mp
 
-    workers = max(1, args.cpu_workers)
+    cores = host_cores()
+    workers = args.cpu_workers if args.cpu_workers > 0 else cores["share"]
+    T = args.cpu_candles
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
@@ -131,20 +179,26 @@ def cpu_baseline(args, T):
         "unit": "symbol-candles/s",
         "cores": workers,
         "kind": "port",
-        "sample": f"{syms} symbols x {T} candles, pandas per-symbol indicators_enrichment "
-        f"(oracle restatement), {workers} processes, ~{args.cpu_seconds:.0f}s each (wall {wall:.1f}s)",
+        "host": cores,
+        "sample": f"C1: {syms} symbols x {T}-candle frames, per symbol pandas indicators_enrichment (14 columns) "
+        f"+ _compute_symbol_features on the last 400 bars (oracle restatement of the reference call pattern), "
+        f"{workers} processes x ~{args.cpu_seconds:.0f}s (wall {wall:.1f}s)",
     }
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+def pmc_traffic(kernel: str, candles: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_traffic.json); null when the summary was taken on
+    another panel size."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("bytes_per_launch")
+            d = json.load(f).get(kernel, {})
     except (OSError, ValueError):
-        return None
+        return None, None
+    if d.get("candles_per_launch") != candles:
+        return None, d.get("source")
+    return d.get("bytes_per_launch"), d.get("source")
 
 
 def bench_tick(args, dev):
@@ -190,7 +244,9 @@ def bench_tick(args, dev):
 
 
 def bench_breadth(args, panel, world, dev):
-    """C5 leg: features -> partials -> RCCL all-reduce(sum) of [T x 10]."""
+    """C5 leg: features -> partials -> ONE all-reduce(sum) of the [T x 10]
+    partials (tracked-symbol count folded into the spare column;
+    market_regime.batch.reduce_partials, RCCL over xGMI at N > 1)."""
     h, l, c = panel["high"], panel["low"], panel["close"]
     S, T = c.shape
     feats = engine.market_features(h, l, c, max_bars=400)
@@ -201,16 +257,17 @@ def bench_breadth(args, panel, world, dev):
     for _ in range(steps):
         engine.market_features(h, l, c, max_bars=400, out=feats)
         engine.breadth_partial(c, feats, out=part)
-        if world > 1:
-            dist.all_reduce(part)
+        _, n_total = reduce_partials(part, S)
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world) / steps
+    del feats
     return {
-        "value": S * T * world / dt,
+        "value": n_total * T / dt,
         "unit": "symbol-candles/s",
         "ms_per_step": dt * 1e3,
+        "tracked_symbols": n_total,
         "workload": f"{S} symbols x {T} candles per GPU, max_bars 400, features + partials"
-        + (" + RCCL all_reduce [T x 10] fp64" if world > 1 else ""),
+        + (" + one RCCL all_reduce of [T x 10] fp64" if world > 1 else ""),
     }
 
 
@@ -377,37 +434,45 @@ def bench_store(args, dev):
     }
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", local)
-    S, T = args.symbols, args.candles
-    panel = device_panel(S, T, device=dev, seed=1234 + rank)
+def time_enrich(panel, steps: int, warmup: int, world: int):
+    """Wall time per step (barrier + synchronize on both sides, max over
+    ranks) and mean enrich_kernel time (HIP events on the launch stream)."""
+    S, T = panel["close"].shape
+    dev = panel["close"].device
     out = {k: torch.empty((S, T), dtype=torch.float64, device=dev) for k in ENRICH_COLUMNS}
     stream = torch.cuda.current_stream()
 
     def step():
         engine.enrich(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"], out=out)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     barrier(world)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         evs[i][0].record(stream)
         step()
         evs[i][1].record(stream)
     barrier(world)
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    wall = max_over_ranks(wall, world)
-    kern_ms = max_over_ranks(kern_ms, world)
-    ms_per_step = wall / args.steps * 1e3
-    value = S * T * world / (wall / args.steps)
+    del out
+    return max_over_ranks(wall, world) / steps, max_over_ranks(kern_ms, world)
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    lo, hi = shard_bounds(args.symbols, world, rank)
+    S, T = hi - lo, args.candles
+    panel = device_panel(S, T, device=dev, seed=1234 + rank)
+    step_s, kern_ms = time_enrich(panel, args.steps, args.warmup, world)
+    value = args.symbols * T / step_s
     bytes_launch = S * T * BYTES_PER_CANDLE
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic("enrich_kernel")
+    traffic, traffic_src = pmc_traffic("enrich_kernel", S * T)
 
     result = {
         "metric": "symbol-candles/s for full indicator set (14 fp64 columns)",
@@ -416,14 +481,16 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": step_s * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8d random-walk klines generated in HBM)",
         "config": {
-            "workload": f"C4 shard: {S} symbols x {T} candles per GPU ({S * world} x {T} total)",
+            "workload": f"configs[3]: {args.symbols} symbols x {T} candles, symbol-sharded over {world} GPU(s) "
+                        f"({S} symbols x {T} candles on rank 0)",
+            "symbols": args.symbols,
             "symbols_per_gpu": S,
             "candles": T,
             "columns": list(ENRICH_COLUMNS),
@@ -436,16 +503,31 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "enrich_kernel",
             "kernel_ms": kern_ms,
             "algorithmic_bytes_per_candle": BYTES_PER_CANDLE,
+            "candles_per_launch": S * T,
         },
     }
-    del out
     if not args.no_breadth:
         result["breadth"] = bench_breadth(args, panel, world, dev)
     del panel
     torch.cuda.empty_cache()
+    if not args.no_shard:
+        shard = device_panel(args.shard_symbols, T, device=dev, seed=4321 + rank)
+        sh_step, sh_kern = time_enrich(shard, args.shard_steps, 2, world)
+        result["shard"] = {
+            "workload": f"C4 shard: {args.shard_symbols} symbols x {T} candles per GPU (weak scaling)",
+            "value": args.shard_symbols * T * world / sh_step,
+            "unit": "symbol-candles/s",
+            "scaling": "weak",
+            "ms_per_step": sh_step * 1e3,
+            "kernel_ms": sh_kern,
+            "frac": args.shard_symbols * T * BYTES_PER_CANDLE / (sh_kern * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        }
+        del shard
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_tick:
         result["tick"] = bench_tick(args, dev)
         result["store"] = bench_store(args, dev)
@@ -453,7 +535,7 @@ def main():
         result["rows"] = bench_rows(args, dev)
         result["live"] = bench_live(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, T)
+        result["cpu_baseline"] = cpu_baseline(args)
     else:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -52,7 +52,7 @@ PARTIAL_COLUMNS = (
     "sum_trend",
     "sum_atr_pct",
     "sum_bb_width",
-    "reserved",
+    "tracked",   # 0 from the kernel; market_regime.batch.reduce_partials folds the shard's symbol count in
 )
 MAX_WINDOW = 126
 MAX_RESAMPLE_FIELDS = 12

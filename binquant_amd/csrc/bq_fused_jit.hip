@@ -347,11 +347,18 @@ int fused_native_eval(const bq_fused_program& P, int64_t S, int64_t T, hipStream
     if (m == e->mods.end()) {
       hipModule_t mod;
       if (hipModuleLoadData(&mod, e->code.data()) != hipSuccess) return BQ_EHIP;
+      // resolve every entry before caching the module: a failure leaves no
+      // half-initialised entry behind (and unloads the module)
+      const char* names[3] = {"bq_fk1", "bq_fk2", "bq_fk4"};
+      hipFunction_t got[3];
+      for (int i = 0; i < 3; ++i)
+        if (hipModuleGetFunction(&got[i], mod, names[i]) != hipSuccess) {
+          (void)hipModuleUnload(mod);
+          return BQ_EHIP;
+        }
       auto& slot = e->mods[dev];
       slot.first = mod;
-      const char* names[3] = {"bq_fk1", "bq_fk2", "bq_fk4"};
-      for (int i = 0; i < 3; ++i)
-        if (hipModuleGetFunction(&slot.second[i], mod, names[i]) != hipSuccess) return BQ_EHIP;
+      for (int i = 0; i < 3; ++i) slot.second[i] = got[i];
       m = e->mods.find(dev);
     }
     for (int i = 0; i < 3; ++i) fn[i] = m->second.second[i];

@@ -6,9 +6,12 @@
 // Here each symbol keeps device-resident state instead:
 //   * a ring of the last RING candles (o, h, l, c, v), slot-major [RING][S]
 //     so that lane = symbol reads are coalesced;
-//   * the five EMA carries (macd fast/slow, ema20, ema50, macd signal), updated
-//     with pandas' exact ewm(adjust=False) step, so tick EMAs equal the
-//     full-series pandas EMAs bit for bit once seeded;
+//   * the five EMA carries (macd fast/slow, ema20, ema50, macd signal) and
+//     their old weights, updated with pandas' exact ewm(adjust=False,
+//     ignore_na=False) step — a NaN candle (a symbol without a candle this
+//     tick) decays the old weight by (1 - alpha) and holds the value, as
+//     pandas does across a NaN gap — so tick EMAs equal the full-series
+//     pandas EMAs bit for bit once seeded;
 //   * rolling windows re-summed from the ring each tick (compensated), which
 //     keeps them drift-free; pandas' constant-window rules are applied.
 // One thread per symbol; a 10k-symbol tick is a single ~40-workgroup launch.
@@ -31,7 +34,7 @@ struct TickConsts {
   int ma[3];
   int rsi_w, bb_w, bb_ddof, atr_w, twap_w, mfi_w;
   double bb_k;
-  double alpha[5], om[5], den[5];   // 0 macd fast, 1 macd slow, 2 ema0, 3 ema1, 4 signal
+  double alpha[5], om[5];   // 0 macd fast, 1 macd slow, 2 ema0, 3 ema1, 4 signal
 };
 
 }  // namespace bq
@@ -41,7 +44,7 @@ struct bq_state {
   int64_t count;
   bq::TickConsts K;
   double* ring;   // [5][RING][S]
-  double* ema;    // [5][S]
+  double* ema;    // [10][S]: 5 EMA values, then their 5 old weights
 };
 
 namespace bq {
@@ -69,6 +72,29 @@ __device__ __forceinline__ double window_sum(F q, int64_t t, int w, bool& all_sa
   return s;
 }
 
+// One step of pandas' ewm(adjust=False, ignore_na=False) mean
+// (pandas/_libs/window/aggregations.pyx `ewm`; oracle/indicators_ref.py
+// ewm_scalar): y = weighted, w = old_wt. With no NaN gap w == 1 before the
+// decay and (om * y + al * x) / (om + al) is the plain update (om + al == 1.0
+// exactly for integer spans, so the divide is the identity).
+__device__ __forceinline__ void ewm_step(double& y, double& w, double x, double al, double om, bool first) {
+  if (first) {
+    y = x;
+    w = 1.0;
+    return;
+  }
+  const bool obs = x == x;
+  if (y == y) {
+    w *= om;
+    if (obs) {
+      if (y != x) y = (w * y + al * x) / (w + al);
+      w = 1.0;
+    }
+  } else if (obs) {
+    y = x;
+  }
+}
+
 __global__ __launch_bounds__(TK_NT) void tick_kernel(const TickConsts K, int64_t S, int64_t n, double* ring,
                                                      double* ema, const double* __restrict__ no,
                                                      const double* __restrict__ nh, const double* __restrict__ nl,
@@ -88,21 +114,14 @@ __global__ __launch_bounds__(TK_NT) void tick_kernel(const TickConsts K, int64_t
   }
   double y[5];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    double v = ema[(int64_t)e * S + s];
-    if (t == 0) v = x;
-    else if (v != x) v = (K.om[e] * v + K.alpha[e] * x) / K.den[e];
+  for (int e = 0; e < 5; ++e) {
+    double v = ema[(int64_t)e * S + s], wt = ema[(int64_t)(5 + e) * S + s];
+    ewm_step(v, wt, e < 4 ? x : y[0] - y[1], K.alpha[e], K.om[e], t == 0);
     y[e] = v;
     ema[(int64_t)e * S + s] = v;
+    ema[(int64_t)(5 + e) * S + s] = wt;
   }
   const double macd = y[0] - y[1];
-  {
-    double v = ema[(int64_t)4 * S + s];
-    if (t == 0) v = macd;
-    else if (v != macd) v = (K.om[4] * v + K.alpha[4] * macd) / K.den[4];
-    y[4] = v;
-    ema[(int64_t)4 * S + s] = v;
-  }
 
   auto O = [&](int64_t i) { return i < 0 ? qnan() : ring_at(ring, 0, S, i, s); };
   auto Hh = [&](int64_t i) { return i < 0 ? qnan() : ring_at(ring, 1, S, i, s); };
@@ -189,20 +208,18 @@ __global__ __launch_bounds__(TK_NT) void seed_kernel(const TickConsts K, int64_t
   const int64_t s = (int64_t)blockIdx.x * TK_NT + threadIdx.x;
   if (s >= S) return;
   const double* rc = ic + s * ld;
-  double y[5] = {0, 0, 0, 0, 0};
+  double y[5] = {0, 0, 0, 0, 0}, wt[5] = {1, 1, 1, 1, 1};
   for (int t = 0; t < T; ++t) {
     const double x = rc[t];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (t == 0) y[e] = x;
-      else if (y[e] != x) y[e] = (K.om[e] * y[e] + K.alpha[e] * x) / K.den[e];
-    }
-    const double m = y[0] - y[1];
-    if (t == 0) y[4] = m;
-    else if (y[4] != m) y[4] = (K.om[4] * y[4] + K.alpha[4] * m) / K.den[4];
+    for (int e = 0; e < 4; ++e) ewm_step(y[e], wt[e], x, K.alpha[e], K.om[e], t == 0);
+    ewm_step(y[4], wt[4], y[0] - y[1], K.alpha[4], K.om[4], t == 0);
   }
 #pragma unroll
-  for (int e = 0; e < 5; ++e) ema[(int64_t)e * S + s] = y[e];
+  for (int e = 0; e < 5; ++e) {
+    ema[(int64_t)e * S + s] = y[e];
+    ema[(int64_t)(5 + e) * S + s] = wt[e];
+  }
   const double* src[5] = {io + s * ld, ih + s * ld, il + s * ld, rc, iv + s * ld};
   const int first = T > RING ? T - RING : 0;
   for (int t = first; t < T; ++t)
@@ -252,13 +269,12 @@ int bq_state_create(bq_state** out, int64_t S, const bq_params* params) {
   for (int e = 0; e < 5; ++e) {
     K.alpha[e] = alpha_span(spans[e]);
     K.om[e] = 1.0 - K.alpha[e];
-    K.den[e] = K.om[e] + K.alpha[e];
   }
   if (hipMalloc(&st->ring, sizeof(double) * 5 * RING * S) != hipSuccess) {
     free(st);
     return BQ_EHIP;
   }
-  if (hipMalloc(&st->ema, sizeof(double) * 5 * S) != hipSuccess) {
+  if (hipMalloc(&st->ema, sizeof(double) * 10 * S) != hipSuccess) {
     (void)hipFree(st->ring);
     free(st);
     return BQ_EHIP;

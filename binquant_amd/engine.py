@@ -8,7 +8,9 @@ There is no CPU path: non-CUDA input raises.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import functools
 from dataclasses import dataclass, field
 
 import torch
@@ -85,6 +87,86 @@ def _stream_handle(stream: torch.cuda.Stream | None) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _cuda_tensors(obj, out: list) -> list:
+    """CUDA tensors among a call's arguments (tensors, and tensors inside
+    lists / tuples / dict values one level down)."""
+    if isinstance(obj, torch.Tensor):
+        if obj.is_cuda:
+            out.append(obj)
+    elif isinstance(obj, (list, tuple)):
+        for x in obj:
+            if isinstance(x, torch.Tensor) and x.is_cuda:
+                out.append(x)
+    elif isinstance(obj, dict):
+        for x in obj.values():
+            if isinstance(x, torch.Tensor) and x.is_cuda:
+                out.append(x)
+    elif isinstance(getattr(obj, "x", None), torch.Tensor) and obj.x.is_cuda:   # Roll / Ewm / Ffill specs
+        out.append(obj.x)
+    return out
+
+
+@contextlib.contextmanager
+def launch_scope(device: torch.device | None, stream: torch.cuda.Stream | None, tensors=()):
+    """Where and when a native launch runs.
+
+    * device — made current for the call: the C ABI launches on the current
+      device's stream, and the fused JIT resolves its module per current device.
+    * stream — when given, it first waits on the device's current stream (the
+      producers of the operands), the call runs under torch.cuda.stream(stream)
+      so outputs and temporaries are allocated and produced on it, and every
+      CUDA operand is recorded on it so the caching allocator does not hand
+      the memory out again before the stream has read it. Later use of the
+      outputs on another stream is the caller's to order, as with any torch
+      side stream.
+    """
+    if device is not None and device.type != "cuda":   # host tensors (CPU rehearsal of the collectives)
+        yield
+        return
+    if stream is None:
+        if device is None or device.index is None or device.index == (
+                _cur_device() if _cur_device else torch.cuda.current_device()):
+            yield
+            return
+        with torch.cuda.device(device):
+            yield
+        return
+    if device is not None and stream.device != device:
+        raise ValueError(f"stream is on {stream.device}, operands on {device}")
+    with torch.cuda.device(stream.device):
+        stream.wait_stream(torch.cuda.current_stream(stream.device))
+        for t in tensors:
+            t.record_stream(stream)
+        with torch.cuda.stream(stream):
+            yield
+
+
+def device_entry(fn):
+    """Decorator of the public entry points: runs `fn` on the device holding
+    its CUDA operands (all must share one device) and, for `stream=`, under
+    launch_scope's stream ordering. The wrapped body always launches on the
+    current stream."""
+
+    @functools.wraps(fn)
+    def wrapper(*args, stream: torch.cuda.Stream | None = None, **kw):
+        ts: list = []
+        for a in args:
+            _cuda_tensors(a, ts)
+        for a in kw.values():
+            _cuda_tensors(a, ts)
+        dev = ts[0].device if ts else None
+        if dev is not None:
+            for t in ts:
+                if t.device != dev:
+                    raise ValueError(f"{fn.__name__}: operands on {dev} and {t.device}; one device per call")
+        if stream is None and (dev is None or dev.index == (_cur_device() if _cur_device else -1)):
+            return fn(*args, **kw)
+        with launch_scope(dev, stream, ts):
+            return fn(*args, **kw)
+
+    return wrapper
+
+
 def _check_panel(x: torch.Tensor, name: str, shape=None) -> torch.Tensor:
     if not isinstance(x, torch.Tensor) or not x.is_cuda:
         raise ValueError(f"{name}: expected a float64 CUDA tensor (no CPU path)")
@@ -103,6 +185,7 @@ def _row_stride(x: torch.Tensor) -> int:
     return int(x.stride(0)) if x.shape[0] > 1 else int(x.shape[1])
 
 
+@device_entry
 def enrich(
     open_: torch.Tensor,
     high: torch.Tensor,
@@ -156,6 +239,7 @@ def enrich(
     return {n: out[n] for n in cols}
 
 
+@device_entry
 def market_features(
     high: torch.Tensor,
     low: torch.Tensor,
@@ -178,7 +262,11 @@ def market_features(
     for name in FEATURE_COLUMNS:
         if name not in out:
             out[name] = torch.empty((S, T), dtype=torch.float64, device=close.device)
+        else:
+            _check_panel(out[name], f"out[{name}]", (S, T))
     ld_out = _row_stride(out[FEATURE_COLUMNS[0]])
+    if any(_row_stride(out[n]) != ld_out for n in FEATURE_COLUMNS):
+        raise ValueError("all feature output columns must share one row stride")
     st = _lib.load().bq_market_features(
         _lib.ptr_array([t.data_ptr() for t in hlc]),
         S,
@@ -193,6 +281,7 @@ def market_features(
     return out
 
 
+@device_entry
 def breadth_partial(
     close: torch.Tensor,
     feats: dict[str, torch.Tensor],
@@ -209,6 +298,9 @@ def breadth_partial(
         raise ValueError("feature columns must share one row stride")
     if out is None:
         out = torch.empty((T, len(PARTIAL_COLUMNS)), dtype=torch.float64, device=close.device)
+    elif not (isinstance(out, torch.Tensor) and out.dtype == torch.float64 and out.device == close.device
+              and tuple(out.shape) == (T, len(PARTIAL_COLUMNS)) and out.is_contiguous()):
+        raise ValueError(f"out: expected a contiguous float64 [{T}, {len(PARTIAL_COLUMNS)}] tensor on {close.device}")
     st = _lib.load().bq_breadth_partial(
         ctypes.c_void_p(close.data_ptr()),
         _lib.ptr_array([t.data_ptr() for t in fs]),
@@ -230,6 +322,8 @@ class TickState:
         self._lib = _lib.load()
         self._h = ctypes.c_void_p()
         p = (params or IndicatorParams()).to_c()
+        # device memory of the state lives on the current device (bq_state_create)
+        self.device = torch.device("cuda", torch.cuda.current_device())
         _lib.check(self._lib.bq_state_create(ctypes.byref(self._h), int(n_symbols), ctypes.byref(p)), "bq_state_create")
         self.n_symbols = int(n_symbols)
 
@@ -243,23 +337,29 @@ class TickState:
     def count(self) -> int:
         return int(self._lib.bq_state_count(self._h))
 
+    @device_entry
     def seed(self, open_, high, low, close, volume, stream=None) -> None:
         close = _check_panel(close, "close")
         S, T = close.shape
         if S != self.n_symbols:
             raise ValueError(f"seed panel has {S} symbols, state has {self.n_symbols}")
+        if close.device != self.device:
+            raise ValueError(f"seed panel on {close.device}, state on {self.device}")
         ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip((open_, high, low, close, volume), INPUT_FIELDS)]
         st = self._lib.bq_state_seed(
             self._h, _lib.ptr_array([t.data_ptr() for t in ins]), T, T, _stream_handle(stream)
         )
         _lib.check(st, "bq_state_seed")
 
+    @device_entry
     def tick(self, new_ohlcv, out: dict[str, torch.Tensor] | None = None, columns=ENRICH_COLUMNS, stream=None):
         """new_ohlcv: sequence of 5 float64 CUDA vectors [S] (open, high, low, close, volume)."""
         vecs = []
         for t, n in zip(new_ohlcv, INPUT_FIELDS):
             if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.numel() == self.n_symbols):
                 raise ValueError(f"{n}: expected float64 CUDA vector of length {self.n_symbols}")
+            if t.device != self.device:
+                raise ValueError(f"{n}: on {t.device}, state on {self.device}")
             vecs.append(t.contiguous())
         out = dict(out or {})
         cols = tuple(columns)
@@ -267,6 +367,11 @@ class TickState:
         for n in cols:
             if n not in out:
                 out[n] = torch.empty(self.n_symbols, dtype=torch.float64, device=dev)
+            else:
+                o = out[n]
+                if not (isinstance(o, torch.Tensor) and o.dtype == torch.float64 and o.device == dev
+                        and o.numel() == self.n_symbols and o.is_contiguous()):
+                    raise ValueError(f"out[{n}]: expected a contiguous float64 vector of {self.n_symbols} on {dev}")
         st = self._lib.bq_tick(
             self._h,
             _lib.ptr_array([t.data_ptr() for t in vecs]),
@@ -277,6 +382,7 @@ class TickState:
         return {n: out[n] for n in cols}
 
 
+@device_entry
 def beta_corr(
     close: torch.Tensor,
     btc_close: torch.Tensor,
@@ -299,6 +405,7 @@ def beta_corr(
     return {"beta": beta, "corr": corr}
 
 
+@device_entry
 def rolling(
     x: torch.Tensor,
     window: int,
@@ -333,6 +440,7 @@ def rolling(
     return out
 
 
+@device_entry
 def ewm(
     x: torch.Tensor,
     alpha: float | None = None,
@@ -390,6 +498,7 @@ class Ffill:
     x: torch.Tensor
 
 
+@device_entry
 def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
     """Independent Roll / Ewm series over one [S, T] shape in as few launches
     as the kernel families allow (bq_rolling_batch): the lane-per-symbol
@@ -434,6 +543,7 @@ def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.
     return outs
 
 
+@device_entry
 def row_quantile(x: torch.Tensor, q: float, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """numpy.quantile(row[~isnan(row)], q) per row (numpy 'linear' method), as
     FailedSpikeFade.auto_calibrate (strategies/failed_spike_fade.py:229-257)
@@ -449,6 +559,7 @@ def row_quantile(x: torch.Tensor, q: float, stream: torch.cuda.Stream | None = N
     return out
 
 
+@device_entry
 def cooldown(label: torch.Tensor, bars: int, stream: torch.cuda.Stream | None = None):
     """FailedSpikeFade.apply_cooldown (strategies/failed_spike_fade.py:495-520):
     returns (kept, suppressed) bool [S, T] — a label within `bars` candles of
@@ -469,6 +580,7 @@ def cooldown(label: torch.Tensor, bars: int, stream: torch.cuda.Stream | None = 
     return kept, sup
 
 
+@device_entry
 def supertrend(
     high: torch.Tensor,
     low: torch.Tensor,
@@ -529,6 +641,7 @@ def _ptr(t: torch.Tensor | None) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
 
 
+@device_entry
 def resample(
     ts: torch.Tensor,
     fields: dict[str, torch.Tensor],
@@ -571,6 +684,7 @@ def resample(
     return out_ts, dict(zip(names, outs)), out_lens
 
 
+@device_entry
 def align(ts: torch.Tensor, bench_ts: torch.Tensor, bench_val: torch.Tensor, lens=None,
           stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """Benchmark value at each candle's timestamp (left merge on open_time,
@@ -589,6 +703,7 @@ def align(ts: torch.Tensor, bench_ts: torch.Tensor, bench_val: torch.Tensor, len
     return out
 
 
+@device_entry
 def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
                  lens=None, stream: torch.cuda.Stream | None = None):
     """Aligned (symbol, benchmark) log-return pairs of
@@ -610,6 +725,7 @@ def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, 
     return x, y, n
 
 
+@device_entry
 def beta_corr_pairs(x: torch.Tensor, y: torch.Tensor, window: int = 50,
                     stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
     """Rolling beta / corr over aligned return pairs (join_returns output):

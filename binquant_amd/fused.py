@@ -33,6 +33,12 @@ from . import _lib, engine
 
 _OPS = _lib.FUSED_OPS
 _TRACE = bool(__import__("os").environ.get("BQ_FUSED_TRACE"))
+# BQ_FUSED_MANIFEST=<file>: append the structure of every program launched
+# (what the generated HIP source depends on) so that build() can compile
+# them ahead of deployment (warm_cache)
+_MANIFEST = __import__("os").environ.get("BQ_FUSED_MANIFEST")
+_manifest_seen: set = set()
+MANIFEST_PATH = __import__("os").path.join(__import__("os").path.dirname(__file__), "fused_manifest.json")
 NAN = float("nan")
 
 
@@ -533,6 +539,71 @@ def native_compile(outputs: dict[str, Ex], S: int, T: int) -> int:
     return len(plans)
 
 
+def _tclass(stride_t: int) -> int:
+    """stride_t class the generated source specialises on (bq_fused_jit.hip):
+    1 contiguous along t, 0 one value per symbol, 2 any other stride."""
+    return 1 if stride_t == 1 else 0 if stride_t == 0 else 2
+
+
+def _structure_of(prog: _lib.BqFusedProgram) -> dict:
+    """Everything of an ABI program that the generated HIP source depends on
+    (pointers, row strides and constant values are kernel arguments)."""
+    return {
+        "ins": [int(w) for w in prog.ins[:prog.n_ins]], "n_loads": prog.n_loads, "n_regs": prog.n_regs,
+        "n_const": prog.n_const,
+        "inp": [[prog.inp[i].dtype, _tclass(prog.inp[i].stride_t)] for i in range(prog.n_in)],
+        "out": [[prog.out[i].dtype, _tclass(prog.out[i].stride_t)] for i in range(prog.n_out)],
+    }
+
+
+def _record_structure(prog: _lib.BqFusedProgram) -> None:
+    import json
+
+    rec = json.dumps(_structure_of(prog), sort_keys=True)
+    if rec in _manifest_seen:
+        return
+    _manifest_seen.add(rec)
+    with open(_MANIFEST, "a") as f:
+        f.write(rec + "\n")
+
+
+def _program_of(rec: dict) -> _lib.BqFusedProgram:
+    prog = _lib.BqFusedProgram()
+    prog.n_ins, prog.n_loads, prog.n_regs = len(rec["ins"]), rec["n_loads"], rec["n_regs"]
+    prog.n_in, prog.n_out, prog.n_const = len(rec["inp"]), len(rec["out"]), rec["n_const"]
+    prog.ins[:len(rec["ins"])] = rec["ins"]
+    # a placeholder address: compiling launches nothing (validation wants non-null)
+    for i, (dt, tc) in enumerate(rec["inp"]):
+        prog.inp[i] = _lib.BqFusedOperand(ctypes.c_void_p(256), 1, tc, dt, 0)
+    for i, (dt, tc) in enumerate(rec["out"]):
+        prog.out[i] = _lib.BqFusedOperand(ctypes.c_void_p(256), 1, tc, dt, 0)
+    return prog
+
+
+def warm_cache(path: str | None = None) -> int:
+    """Compile (hiprtc, gfx950; no device needed) every program structure of
+    the manifest into the on-disk code-object cache, so that the first
+    message after a deploy runs no hiprtc (__graft_entry__.build calls this).
+    The manifest (binquant_amd/fused_manifest.json, one JSON object per line)
+    is what the strategy / signal pipelines launch at the live and bench
+    shapes, recorded with BQ_FUSED_MANIFEST (tools/fused_manifest.py).
+    Returns the number of programs in the manifest."""
+    import json
+    import os
+
+    path = path or MANIFEST_PATH
+    if not os.path.exists(path):
+        return 0
+    lib = _lib.load()
+    n = 0
+    with open(path) as f:
+        for line in f:
+            if line.strip():
+                _lib.check(lib.bq_fused_compile(ctypes.byref(_program_of(json.loads(line)))), "bq_fused_compile")
+                n += 1
+    return n
+
+
 def native_stats() -> dict[str, int]:
     lib = _lib.load()
     v = [ctypes.c_int64() for _ in range(3)]
@@ -594,16 +665,21 @@ def run(outputs: dict[str, Ex | torch.Tensor], S: int | None = None, T: int | No
             print(f"[fused] ins={len(P.ins)} loads={P.n_loads} regs={P.n_regs} in={len(P.inputs)} "
                   f"out={len(P.outputs)} consts={len(P.consts)} S={S} T={T}", file=sys.stderr)
     for P in plans:
-        outs = []
-        for name, kind in P.outputs:
-            t = torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64, device=dev)
-            res[name] = t
-            outs.append(t)
         for t in P.inputs:
-            if not t.is_cuda:
-                raise ValueError("fused operands must be on the evaluation device")
-        prog = _abi(P, outs, S, T)
-        _lib.check(lib.bq_fused_eval(ctypes.byref(prog), S, T, engine._stream_handle(stream)), "bq_fused_eval")
-        # keep the operands alive until the launch is ordered on the stream
-        del prog
+            if not t.is_cuda or t.device != dev:
+                raise ValueError(f"fused operands must be on the evaluation device {dev}")
+    # launches on `dev` (current for the call), ordered per engine.launch_scope
+    with engine.launch_scope(dev, stream, operands):
+        for P in plans:
+            outs = []
+            for name, kind in P.outputs:
+                t = torch.empty((S, T), dtype=torch.bool if kind == "b" else torch.float64, device=dev)
+                res[name] = t
+                outs.append(t)
+            prog = _abi(P, outs, S, T)
+            if _MANIFEST:
+                _record_structure(prog)
+            _lib.check(lib.bq_fused_eval(ctypes.byref(prog), S, T, engine._stream_handle(None)), "bq_fused_eval")
+            # keep the operands alive until the launch is ordered on the stream
+            del prog
     return {k: res[k] for k in outputs}

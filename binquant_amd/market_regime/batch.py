@@ -62,15 +62,22 @@ def shard_bounds(n_symbols: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+TRACKED_COLUMN = 9   # PARTIAL_COLUMNS[9]: symbols tracked by the shard
+
+
 def reduce_partials(part: torch.Tensor, n_local: int, group=None) -> tuple[torch.Tensor, int]:
-    """all_reduce(sum) of the [T, 10] partials over the symbol shards (RCCL over
-    xGMI on GPUs, gloo on CPU) plus the total symbol count. Identity on one rank."""
+    """ONE all_reduce(sum) of the [T, 10] partials over the symbol shards (RCCL
+    over xGMI on GPUs, gloo on CPU). The shard's tracked-symbol
+    count rides in the spare column 9 of every row, so the admission gate's
+    total (live_market_context_accumulator.py:96-102) needs no second
+    collective. Returns (reduced partials, total tracked symbols); on one
+    rank the partials are returned with column 9 = n_local."""
+    part[:, TRACKED_COLUMN] = float(n_local)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
-        t = torch.tensor([n_local], dtype=torch.int64, device=part.device)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
-        return part, int(t.item())
-    return part, n_local
+        n_total = int(part[0, TRACKED_COLUMN].item()) if part.shape[0] else int(n_local)
+        return part, n_total
+    return part, int(n_local)
 
 
 def contexts_from_partials(partial: np.ndarray, btc_return: np.ndarray, btc_trend: np.ndarray,

@@ -24,6 +24,7 @@ in pandas on every message (O(S^2 * 400) per period).
 from __future__ import annotations
 
 import ctypes
+import functools
 from collections import deque
 from collections.abc import Mapping, Sequence
 from math import ceil
@@ -76,6 +77,22 @@ def _device(device) -> torch.device:
     if not torch.cuda.is_available():
         raise RuntimeError("DeviceMarketStateStore needs a HIP device (no CPU fallback)")
     return torch.device("cuda")
+
+
+def _on_device(fn):
+    """Run a store / accumulator method on the store's device (made current
+    for the call) and, for `stream=`, under engine.launch_scope's ordering."""
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, stream=None, **kw):
+        dev = self.device if hasattr(self, "device") else self.state_store.device
+        ts: list = []
+        for a in args:
+            engine._cuda_tensors(a, ts)
+        with engine.launch_scope(dev, stream, ts):
+            return fn(self, *args, **kw)
+
+    return wrapper
 
 
 class SortedNames(Sequence):
@@ -207,6 +224,7 @@ class DeviceMarketStateStore:
         return len(self._names)
 
     # -- batched updates (device) ---------------------------------------------------
+    @_on_device
     def update_slots(self, slots: torch.Tensor, ts: torch.Tensor, fields: Sequence[torch.Tensor], stream=None,
                      unique_sorted: bool = False) -> None:
         """One launch for a batch of candles (arrival order; device tensors):
@@ -258,6 +276,7 @@ class DeviceMarketStateStore:
         )
         _lib.check(st, "bq_store_update")
 
+    @_on_device
     def update_batch(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume) -> None:
         """Many symbols' candles (host arrays, arrival order) in one launch."""
         slots = self.slots_for(symbols)
@@ -267,6 +286,7 @@ class DeviceMarketStateStore:
                           unique_sorted=self._slot_cache[2])
 
     # -- reference API ----------------------------------------------------------------
+    @_on_device
     def update(self, symbol: str, candle: Mapping[str, Any] | pd.Series | pd.DataFrame) -> pd.DataFrame:
         normalized = normalize_candles(candle)
         s = self._slot(symbol)
@@ -283,6 +303,7 @@ class DeviceMarketStateStore:
             raise IndexError("MarketStateStore.update: no candle with a timestamp and a close")
         return history
 
+    @_on_device
     def _gather(self, slots: list[int]) -> tuple[np.ndarray, np.ndarray, dict[str, np.ndarray]]:
         M = self.max_bars_per_symbol
         sl = torch.tensor(slots, dtype=torch.int64, device=self.device)
@@ -325,6 +346,7 @@ class DeviceMarketStateStore:
     def get_tracked_symbols(self) -> list[str]:
         return sorted(self._names)
 
+    @_on_device
     def fresh_slots(self, timestamp: int) -> torch.Tensor:
         """Slots whose last closed candle is `timestamp` (ascending slot ids, device)."""
         n = self.n_tracked
@@ -335,6 +357,7 @@ class DeviceMarketStateStore:
         return {self._names[i] for i in self.fresh_slots(timestamp).cpu().tolist()}
 
     # -- features ---------------------------------------------------------------------------
+    @_on_device
     def features(self, slots: torch.Tensor, stream=None) -> tuple[dict[str, torch.Tensor], torch.Tensor]:
         """_compute_symbol_features of each slot's history (NaN rows where the
         reference returns None). Returns ({feature: [n]}, latest close [n])."""
@@ -369,10 +392,12 @@ class DeviceLiveMarketContextAccumulator:
         self.last_symbol_features: dict[str, np.ndarray] | None = None
 
     # -- reference API ------------------------------------------------------------------
+    @_on_device
     def on_closed_candle(self, symbol: str, candle) -> dict | None:
         history = self.state_store.update(symbol=symbol, candle=candle)
         return self.refresh_context_for_timestamp(int(history.iloc[-1]["timestamp"]))
 
+    @_on_device
     def on_closed_candles(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume,
                           at: int | None = None) -> dict | None:
         """A whole tick in one device update, then one context build (at the
@@ -393,6 +418,7 @@ class DeviceLiveMarketContextAccumulator:
             self._context_order.pop()
         return None
 
+    @_on_device
     def refresh_context_for_timestamp(self, timestamp: int) -> dict | None:
         context = self._build_context(int(timestamp))
         if context is None:

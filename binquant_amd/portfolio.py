@@ -84,7 +84,8 @@ def select_winners(cohort_keys, scores, symbols: Sequence[str], device=None, str
     names = sorted(set(symbols))
     rank_of = {s: i for i, s in enumerate(names)}
     ranks = torch.tensor([rank_of[s] for s in symbols], dtype=torch.int32, device=dev)
-    uniq, win = _cohort_winners(keys, sc, ranks, acc, stream)
+    with engine.launch_scope(dev, stream, (keys, sc, ranks, acc)):
+        uniq, win = _cohort_winners(keys, sc, ranks, acc)
     w = win.cpu().numpy()
     keep = w >= 0
     return Winners(acc.cpu().numpy(), uniq.cpu().numpy()[keep], w[keep])
@@ -129,36 +130,38 @@ def select_winners_sharded(cohort_keys, scores, symbol_ids, seq, group=None, dev
 
     dev = _device(device)
     pick = cohort_winners or _cohort_winners
-    keys = torch.as_tensor(np.asarray(cohort_keys, dtype=np.int64)).to(dev)
-    sc = torch.as_tensor(np.asarray(scores, dtype=np.float64)).to(dev)
-    sid = torch.as_tensor(np.asarray(symbol_ids, dtype=np.int64)).to(dev)
-    sq = torch.as_tensor(np.asarray(seq, dtype=np.int64)).to(dev)
-    # (1) acceptance needs the global arrival order of the cohort keys
-    pairs = _all_gather_rows(torch.stack([sq, keys], 1), group)
-    order = torch.argsort(pairs[:, 0])
-    gk = pairs[order, 1]
-    excl = torch.cat([gk[:1], torch.cummax(gk, 0).values[:-1]])   # running max before each arrival
-    pos = torch.searchsorted(pairs[order, 0].contiguous(), sq)
-    acc = keys >= excl[pos] if keys.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
-    # (2) local winners per cohort (ties inside one symbol resolved by arrival order)
-    local_order = torch.argsort(sq)
-    k_l, s_l, i_l, q_l, a_l = keys[local_order], sc[local_order], sid[local_order], sq[local_order], acc[local_order]
-    if k_l.numel():
-        uniq, win = pick(k_l, s_l, i_l, a_l, stream)
+    # every launch and collective on `dev`, ordered per engine.launch_scope
+    with engine.launch_scope(dev, stream):
+        keys = torch.as_tensor(np.asarray(cohort_keys, dtype=np.int64)).to(dev)
+        sc = torch.as_tensor(np.asarray(scores, dtype=np.float64)).to(dev)
+        sid = torch.as_tensor(np.asarray(symbol_ids, dtype=np.int64)).to(dev)
+        sq = torch.as_tensor(np.asarray(seq, dtype=np.int64)).to(dev)
+        # (1) acceptance needs the global arrival order of the cohort keys
+        pairs = _all_gather_rows(torch.stack([sq, keys], 1), group)
+        order = torch.argsort(pairs[:, 0])
+        gk = pairs[order, 1]
+        excl = torch.cat([gk[:1], torch.cummax(gk, 0).values[:-1]])   # running max before each arrival
+        pos = torch.searchsorted(pairs[order, 0].contiguous(), sq)
+        acc = keys >= excl[pos] if keys.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
+        # (2) local winners per cohort (ties inside one symbol resolved by arrival order)
+        local_order = torch.argsort(sq)
+        k_l, s_l, i_l, q_l, a_l = keys[local_order], sc[local_order], sid[local_order], sq[local_order], acc[local_order]
+        if k_l.numel():
+            uniq, win = pick(k_l, s_l, i_l, a_l, None)
+            ok = win >= 0
+            w = win[ok]
+            rows = torch.stack([uniq[ok], s_l[w].view(torch.int64), i_l[w], q_l[w]], 1)
+        else:
+            rows = torch.zeros((0, 4), dtype=torch.int64, device=dev)
+        # (3) merge the ranks' winners: sorted by seq so that index order is arrival order
+        allw = _all_gather_rows(rows, group)
+        allw = allw[torch.argsort(allw[:, 3])]
+        if allw.shape[0] == 0:
+            return Winners(acc.cpu().numpy(), np.zeros(0, np.int64), np.zeros(0, np.int64))
+        uniq, win = pick(allw[:, 0].contiguous(), allw[:, 1].contiguous().view(torch.float64), allw[:, 2].contiguous(),
+                         torch.ones(allw.shape[0], dtype=torch.bool, device=dev), None)
         ok = win >= 0
-        w = win[ok]
-        rows = torch.stack([uniq[ok], s_l[w].view(torch.int64), i_l[w], q_l[w]], 1)
-    else:
-        rows = torch.zeros((0, 4), dtype=torch.int64, device=dev)
-    # (3) merge the ranks' winners: sorted by seq so that index order is arrival order
-    allw = _all_gather_rows(rows, group)
-    allw = allw[torch.argsort(allw[:, 3])]
-    if allw.shape[0] == 0:
-        return Winners(acc.cpu().numpy(), np.zeros(0, np.int64), np.zeros(0, np.int64))
-    uniq, win = pick(allw[:, 0].contiguous(), allw[:, 1].contiguous().view(torch.float64), allw[:, 2].contiguous(),
-                     torch.ones(allw.shape[0], dtype=torch.bool, device=dev), stream)
-    ok = win >= 0
-    return Winners(acc.cpu().numpy(), uniq[ok].cpu().numpy(), allw[win[ok], 3].cpu().numpy())
+        return Winners(acc.cpu().numpy(), uniq[ok].cpu().numpy(), allw[win[ok], 3].cpu().numpy())
 
 
 class _CohortSelector:

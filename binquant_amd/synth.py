@@ -59,21 +59,33 @@ def numpy_panel(S: int, T: int, seed0: int = 0, edges: bool = True, scales: bool
     return out
 
 
-def device_panel(S: int, T: int, device="cuda", seed: int = 0):
-    """Same distributions, generated in HBM (no per-symbol seeds; for benches)."""
+def device_panel(S: int, T: int, device="cuda", seed: int = 0, chunk: int = 12_500):
+    """Same distributions, generated in HBM (no per-symbol seeds; for benches).
+
+    Symbols are drawn in blocks of `chunk` rows straight into the five [S, T]
+    outputs, so the generation temporaries stay at a few block-sized arrays
+    (the 100k x 10k headline panel is 40 GB of inputs; unchunked temporaries
+    would add as much again)."""
     import torch
 
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     f64 = dict(dtype=torch.float64, device=device)
-    scale = torch.pow(10.0, torch.empty((S, 1), **f64).uniform_(-4.0, 4.0, generator=g))
-    ret = torch.empty((S, T), **f64).normal_(0.0, 0.002, generator=g)
-    close = scale * torch.exp(torch.cumsum(ret, dim=1))
-    del ret
-    open_ = torch.empty_like(close)
-    open_[:, 0] = close[:, 0]
-    open_[:, 1:] = close[:, :-1]
-    high = torch.maximum(open_, close) * (1.0 + torch.empty_like(close).uniform_(0.0, 0.003, generator=g))
-    low = torch.minimum(open_, close) * (1.0 - torch.empty_like(close).uniform_(0.0, 0.003, generator=g))
-    volume = torch.exp(torch.empty_like(close).normal_(3.0, 1.0, generator=g))
-    return {"open": open_, "high": high, "low": low, "close": close, "volume": volume}
+    out = {f: torch.empty((S, T), **f64) for f in FIELDS}
+    for lo in range(0, S, max(1, chunk)):
+        hi = min(S, lo + max(1, chunk))
+        n = hi - lo
+        scale = torch.pow(10.0, torch.empty((n, 1), **f64).uniform_(-4.0, 4.0, generator=g))
+        close = out["close"][lo:hi]
+        torch.cumsum(torch.empty((n, T), **f64).normal_(0.0, 0.002, generator=g), dim=1, out=close)
+        close.exp_().mul_(scale)
+        open_ = out["open"][lo:hi]
+        open_[:, 0] = close[:, 0]
+        open_[:, 1:] = close[:, :-1]
+        u = torch.empty((n, T), **f64)
+        torch.mul(torch.maximum(open_, close), u.uniform_(0.0, 0.003, generator=g).add_(1.0), out=out["high"][lo:hi])
+        torch.mul(torch.minimum(open_, close), u.uniform_(0.0, 0.003, generator=g).neg_().add_(1.0),
+                  out=out["low"][lo:hi])
+        torch.exp(u.normal_(3.0, 1.0, generator=g), out=out["volume"][lo:hi])
+        del u
+    return out

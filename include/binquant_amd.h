@@ -120,6 +120,11 @@ int bq_device_arch(char* buf, int buflen);   /* e.g. "gfx950" */
  *   in[BQ_NUM_INPUTS]        device pointers, each [S][ld_in] fp64
  *   out[BQ_NUM_ENRICH_COLS]  device pointers, each [S][ld_out] fp64 (NULL = skip)
  * Warm-up rows are NaN exactly where pandas yields NaN (t < window-1).
+ * Input contract: finite candles. The panel is what Candles.pre_process /
+ * post_process leave (producers/context_evaluator.py:364-371), which has no
+ * NaN rows; a symbol missing candles is a ragged row (enrich_frames), not a
+ * NaN row. Missing candles in the live feed go through bq_tick, which keeps
+ * pandas' NaN-gap rules.
  */
 int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in,
               const bq_params* params, double* const* out, int64_t ld_out,
@@ -136,7 +141,12 @@ int bq_state_destroy(bq_state* st);
 int bq_state_seed(bq_state* st, const double* const* in, int64_t T, int64_t ld_in,
                   void* stream);
 /* Append one candle per symbol. new_ohlcv[BQ_NUM_INPUTS] device pointers of
- * length S; out[BQ_NUM_ENRICH_COLS] device pointers of length S (NULL skip). */
+ * length S; out[BQ_NUM_ENRICH_COLS] device pointers of length S (NULL skip).
+ * A symbol without a candle this tick passes NaN in all five fields: the
+ * outputs are then what pandas gives for a frame with that NaN row — EMAs
+ * hold their value and decay their old weight by (1 - alpha)
+ * (ewm(adjust=False, ignore_na=False)), windows containing the row are NaN,
+ * RSI/MFI count its move as 0 (delta.where(...) fills NaN with 0). */
 int bq_tick(bq_state* st, const double* const* new_ohlcv, double* const* out,
             void* stream);
 int64_t bq_state_symbols(const bq_state* st);

@@ -178,6 +178,25 @@ def enrich_panel(o, h, l, c, v, p: dict | None = None) -> dict[str, np.ndarray]:
     return out
 
 
+def ema_family_panel(c, p: dict | None = None) -> dict[str, np.ndarray]:
+    """The EMA-family columns (macd, macd_signal, ema20, ema50) of
+    indicators_enrichment for every row of a [S, T] close panel at once:
+    DataFrame.ewm runs pandas' ewm recursion column by column over a [T, S]
+    frame — the same Cython routine as the per-frame Series calls of macd()
+    and ema() above — so each row equals enrich_panel's bit for bit, at a
+    fraction of the per-symbol cost (the C3 10k-symbol checks)."""
+    p = {**DEFAULTS, **(p or {})}
+    close = pd.DataFrame(np.asarray(c, dtype=np.float64).T)
+    e_fast = close.ewm(span=p["macd_fast"], adjust=False).mean()
+    e_slow = close.ewm(span=p["macd_slow"], adjust=False).mean()
+    m = e_fast - e_slow
+    sig = m.ewm(span=p["macd_signal"], adjust=False).mean()
+    out = {"macd": m, "macd_signal": sig,
+           f"ema{p['ema_spans'][0]}": close.ewm(span=p["ema_spans"][0], adjust=False).mean(),
+           f"ema{p['ema_spans'][1]}": close.ewm(span=p["ema_spans"][1], adjust=False).mean()}
+    return {k: np.ascontiguousarray(v.to_numpy().T) for k, v in out.items()}
+
+
 def ewm_scalar(x, alpha: float) -> np.ndarray:
     """Pure-Python restatement of pandas' ewm(adjust=False, ignore_na=False)
     mean recursion (pandas/_libs/window/aggregations.pyx `ewm`), used to pin the

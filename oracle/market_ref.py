@@ -76,6 +76,55 @@ def panel_features_at(h, l, c, t: int, max_bars: int) -> dict | None:
     return symbol_features(h[s : t + 1], l[s : t + 1], c[s : t + 1])
 
 
+def window_features(h, l, c) -> dict[str, np.ndarray] | None:
+    """symbol_features for every row of [S, W] history windows at once (the
+    last column is the evaluated candle). The pandas rolling / ewm kernels run
+    column by column over a [W, S] frame — the same Cython recursions as the
+    per-symbol Series calls of symbol_features — and the scalar tail
+    (:273-297) is restated element-wise with the same IEEE operations, so each
+    row equals symbol_features(h[s], l[s], c[s]) bit for bit
+    (tests/test_oracle_golden.py pins this). For the C5-size checks, where a
+    per-symbol pandas loop over 12 500 symbols would take minutes."""
+    h, l, c = (np.asarray(x, dtype=np.float64) for x in (h, l, c))
+    if c.shape[1] < 2:
+        return None
+    closes, highs, lows = pd.DataFrame(c.T), pd.DataFrame(h.T), pd.DataFrame(l.T)
+    prev = closes.shift(1)
+    tr = np.fmax(np.fmax((highs - lows).to_numpy(), (highs - prev).abs().to_numpy()),
+                 (lows - prev).abs().to_numpy())   # concat(...).max(axis=1): skip-NaN max
+    ema20 = closes.ewm(span=20, adjust=False, min_periods=1).mean().to_numpy()[-1]
+    ema50 = closes.ewm(span=50, adjust=False, min_periods=1).mean().to_numpy()[-1]
+    atr = pd.DataFrame(tr).rolling(14, min_periods=1).mean().to_numpy()[-1]
+    mid = closes.rolling(20, min_periods=1).mean().to_numpy()[-1]
+    std = closes.rolling(20, min_periods=1).std(ddof=0).fillna(0.0).to_numpy()[-1]
+    upper, lower = mid + (2 * std), mid - (2 * std)
+    latest, prev_c = c[:, -1], c[:, -2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        atr_pct = np.where(latest != 0, atr / latest, 0.0)
+        bb_width = np.where(mid != 0, (upper - lower) / np.abs(mid), 0.0)
+        trend = np.where(ema50 != 0, (ema20 - ema50) / np.abs(ema50), 0.0)
+        ret = np.where(prev_c == 0, 0.0, (latest - prev_c) / np.abs(prev_c))
+    return dict(close=latest, return_pct=ret, ema20=ema20, ema50=ema50, above_ema20=latest > ema20,
+                above_ema50=latest > ema50, trend_score=trend, atr_pct=atr_pct, bb_width=bb_width)
+
+
+def panel_window_features_at(h, l, c, t: int, max_bars: int) -> dict[str, np.ndarray] | None:
+    """window_features of every symbol of a [S, T] panel at candle t under the
+    MarketStateStore(max_bars) cap."""
+    s = max(0, t - max_bars + 1)
+    return window_features(h[:, s : t + 1], l[:, s : t + 1], c[:, s : t + 1])
+
+
+def partials_from_features(f: dict[str, np.ndarray]) -> np.ndarray:
+    """The _build_context reductions (:135-163) of one timestamp as the
+    [10] partial row (count, advancers, decliners, above20, above50, sums of
+    return / trend / atr_pct / bb_width, 0), summed in symbol order."""
+    ret = f["return_pct"]
+    return np.array([ret.size, (ret > 0).sum(), (ret < 0).sum(), f["above_ema20"].sum(), f["above_ema50"].sum(),
+                     ret.sum(), f["trend_score"].sum(), f["atr_pct"].sum(), f["bb_width"].sum(), 0.0],
+                    dtype=np.float64)
+
+
 def build_context_from_features(
     feats: dict[str, dict],
     btc_symbol: str,

@@ -55,7 +55,20 @@ def _worker(rank, world, port, label, q):
         S = c.shape[0]
         lo, hi = shard_bounds(S, world, rank)
         part = torch.from_numpy(_partials(h, l, c, idx, sc["max_bars"], lo, hi))
-        part, n_total = reduce_partials(part, hi - lo)
+        calls = []
+        orig = dist.all_reduce
+
+        def counting(*a, **k):
+            calls.append(1)
+            return orig(*a, **k)
+
+        dist.all_reduce = counting
+        try:
+            part, n_total = reduce_partials(part, hi - lo)
+        finally:
+            dist.all_reduce = orig
+        # one collective per context build, tracked count folded in
+        assert len(calls) == 1 and n_total == S, (calls, n_total, S)
         b = sc["symbols"].index(sc["btc"])   # BTC replicated on every rank
         btc = [market_ref.panel_features_at(h[b], l[b], c[b], t, sc["max_bars"]) for t in idx]
         ret = np.array([np.nan if f is None else f["return_pct"] for f in btc])

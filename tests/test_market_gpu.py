@@ -151,3 +151,76 @@ def test_breadth_partial_few_timestamps(cuda, S, T):
     np.testing.assert_array_equal(part[:, 9:], 0.0)
     part2 = engine.breadth_partial(torch.from_numpy(c).cuda(), f).cpu().numpy()
     np.testing.assert_array_equal(part, part2)
+
+
+def test_c5_features_and_breadth_at_shard_size(cuda):
+    """BASELINE configs[4] (C5) per-GPU leg: bq_market_features +
+    bq_breadth_partial over the 12 500 x 10 000 C4 shard under the 400-bar
+    store cap. At sampled timestamps (warm-up rows, t < max_bars, the cap
+    boundary, the last t) every symbol's features are checked against the
+    oracle restatement of _compute_symbol_features
+    (live_market_context_accumulator.py:244-297, vectorised over symbols and
+    pinned bit-exact to the per-symbol form in tests/test_oracle_golden.py),
+    the partial counts exactly and the sums at 1e-9; 64 symbols also go
+    through the per-symbol oracle. Then host scoring of the partials equals
+    scoring of the oracle's partials (_build_context :96-242)."""
+    from binquant_amd.market_regime.batch import reduce_partials
+    from binquant_amd.synth import device_panel
+
+    S, T, M = 12_500, 10_000, 400
+    p = device_panel(S, T, seed=5150)
+    h, l, c = p["high"], p["low"], p["close"]
+    del p
+    f = engine.market_features(h, l, c, max_bars=M)
+    part = engine.breadth_partial(c, f)
+    part, n_total = reduce_partials(part, S)
+    torch.cuda.synchronize()
+    assert n_total == S
+    part = part.cpu().numpy()
+    sample_syms = np.unique(np.r_[0, S - 1, np.linspace(0, S - 1, 62).astype(int)])
+    for t in (0, 1, 13, 19, 20, 398, 399, 400, 401, 5_000, 9_998, 9_999):
+        s0 = max(0, t - M + 1)
+        hw, lw, cw = (x[:, s0 : t + 1].cpu().numpy() for x in (h, l, c))
+        got = {k: v[:, t].cpu().numpy() for k, v in f.items()}
+        want = market_ref.window_features(hw, lw, cw)
+        if want is None:   # a one-candle history: no features, nothing counted
+            assert all(np.isnan(v).all() for v in got.values()), t
+            np.testing.assert_array_equal(part[t, :9], 0.0)
+            continue
+        # price-valued columns scale with the close, the ratios are dimensionless
+        # (the scales of test_features_match_reference_restatement)
+        for k in FEATURE_COLUMNS:
+            scale = np.abs(cw[:, -1]) if k in ("ema20", "ema50") else 1e-3
+            assert_close(got[k], want[k], f"{k}@{t}", rtol=1e-9, scale=scale)
+        close_t = cw[:, -1]
+        for e in ("ema20", "ema50"):   # no close within tolerance of its EMA: counts are exact
+            assert not (np.abs(close_t - want[e]) <= 1e-9 * np.abs(close_t)).any(), (t, e)
+        wp = market_ref.partials_from_features(want)
+        np.testing.assert_array_equal(part[t, :5], wp[:5], err_msg=f"counts@{t}")
+        assert part[t, 9] == S
+        for i in (5, 6, 7, 8):
+            mag = {5: np.abs(want["return_pct"]), 6: np.abs(want["trend_score"]), 7: np.abs(want["atr_pct"]),
+                   8: np.abs(want["bb_width"])}[i].sum()
+            assert abs(part[t, i] - wp[i]) <= 1e-9 * mag + 1e-300, (t, i, part[t, i], wp[i])
+        for s in sample_syms[:: 4 if t < 9_998 else 1]:
+            one = market_ref.symbol_features(hw[s], lw[s], cw[s])
+            for k in FEATURE_COLUMNS:
+                sc = abs(one["close"]) if k in ("ema20", "ema50") else 1e-3
+                assert_close([got[k][s]], [one[k]], f"{k}[{s}]@{t}", rtol=1e-9, scale=[sc])
+        # host scoring of the device partials == scoring of the oracle partials
+        bf = market_ref.symbol_features(hw[0], lw[0], cw[0])
+        wp[9] = S
+        ctxs = []
+        for P in (part[t : t + 1], wp[None]):
+            b = score_contexts(P, np.array([bf["return_pct"]]), np.array([bf["trend_score"]]), np.array([True]),
+                               total_tracked=S, timestamps=np.array([t]))
+            annotate_market(b)
+            ctxs.append(b.context_at(0))
+        dev_ctx, ctx = ctxs
+        assert (dev_ctx is None) == (ctx is None)
+        if ctx is not None:
+            for k, v in ctx.items():
+                if isinstance(v, (bool, str, int)) or v is None:
+                    assert dev_ctx[k] == v, (t, k)
+                elif isinstance(v, float):
+                    assert dev_ctx[k] == pytest.approx(v, rel=1e-9, abs=1e-12), (t, k)

@@ -112,3 +112,37 @@ def test_rolling_replays_are_bit_exact_vs_pandas():
             s = pd.Series(x).rolling(w, min_periods=1)
             np.testing.assert_array_equal(roll_mean_replay(x, w), s.mean().to_numpy())
             np.testing.assert_array_equal(roll_var_replay(x, w), s.var(ddof=0).to_numpy())
+
+
+# ---- vectorised oracle forms used by the C3 / C5 size checks --------------------
+def test_window_features_equal_per_symbol_features():
+    """market_ref.window_features (all symbols at once) == symbol_features per
+    symbol, bit for bit, incl. 2-bar windows, constant runs and zero closes."""
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(24, 460, seed0=5)
+    p["close"][3, 200:] = p["close"][3, 200]
+    p["high"][3, 200:] = p["low"][3, 200:] = p["close"][3, 200]
+    p["close"][4, -1] = 0.0
+    p["close"][5, -2] = 0.0
+    for t, M in ((1, 400), (13, 400), (459, 400), (300, 50), (459, 2)):
+        f = market_ref.panel_window_features_at(p["high"], p["low"], p["close"], t, M)
+        for s in range(24):
+            want = market_ref.panel_features_at(p["high"][s], p["low"][s], p["close"][s], t, M)
+            for k in ("return_pct", "ema20", "ema50", "trend_score", "atr_pct", "bb_width", "above_ema20",
+                      "above_ema50", "close"):
+                assert f[k][s] == want[k] or (np.isnan(f[k][s]) and np.isnan(want[k])), (t, M, s, k)
+        assert market_ref.panel_window_features_at(p["high"], p["low"], p["close"], 0, 400) is None
+
+
+def test_ema_family_panel_equals_per_frame_enrichment():
+    from binquant_amd.synth import numpy_panel
+    from oracle import indicators_ref as ref
+
+    p = numpy_panel(12, 300, seed0=8)
+    p["close"][2, 50] = np.nan   # NaN gap: old weight decays (ignore_na=False)
+    p["close"][3, 0] = np.nan    # NaN first value
+    want = ref.enrich_panel(p["open"], p["high"], p["low"], p["close"], p["volume"])
+    got = ref.ema_family_panel(p["close"])
+    for k in ("macd", "macd_signal", "ema20", "ema50"):
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
