@@ -62,6 +62,32 @@ constexpr int EN_H = 128;             // halo >= BQ_MAX_WINDOW + 2
 constexpr int EN_R = EN_H + EN_TT;    // 1152
 static_assert(EN_K % 2 == 0 && EN_TT >= EN_H && EN_K * WAVE > BQ_MAX_WINDOW, "tile shape");
 
+#ifndef BQ_EN_LDSPERM
+#define BQ_EN_LDSPERM 1   // lane-interleaved LDS ring layout (bank-conflict free)
+#endif
+// LDS ring position -> physical slot. A lane owns EN_K consecutive ring
+// positions, so in the natural layout the 64 lanes of a wave access slots
+// EN_K doubles apart (8 dwords): every ds_read/ds_write_b64 of the ring
+// serialises 4-way on the 64 banks. Storing position i at
+// (i % EN_K) * (R / EN_K) + i / EN_K puts the lanes' k-th candles side by side
+// (2 dwords apart, conflict free); every window walk reads the same residue
+// class on all lanes at each step (lane positions differ by multiples of
+// EN_K), so it stays conflict free too.
+#if BQ_EN_LDSPERM
+#define LX(i) ((((i) & (EN_K - 1)) * (EN_R / EN_K)) + ((i) >> 2))
+// slot of ring position pb + x for the lane whose first position is pb
+// (pb % EN_K == 0, lb = pb / EN_K): lb + LX(x), x may be negative (the shift
+// floors). Window offsets x are wave-uniform, so LX(x) is scalar arithmetic
+// and each access is one VGPR base + an SGPR / immediate offset.
+#define RS(x) (lb + LX(x))
+#define RS1(x) (pb / EN_K + LX(x))
+#else
+#define LX(i) (i)
+#define RS(x) (pb + (x))
+#define RS1(x) (pb + (x))
+#endif
+static_assert(!BQ_EN_LDSPERM || (EN_K == 4 && EN_R % EN_K == 0), "LX assumes 4 candles per lane");
+
 // EMA slots in the scan state
 enum { E_FAST = 0, E_SLOW, E_SIG, E_0, E_1, NE };
 
@@ -268,11 +294,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
     sA = A;
   }
   if (tid < EN_H) {   // candles before the series start: NaN close, zero sums
-    sP[tid] = 0.0;
-    sC[tid] = qnan();
-    sTR[tid] = 0.0;
-    sO4[tid] = 0.0;
-    sMF[tid] = 0.0;
+    sP[LX(tid)] = 0.0;
+    sC[LX(tid)] = qnan();
+    sTR[LX(tid)] = 0.0;
+    sO4[LX(tid)] = 0.0;
+    sMF[LX(tid)] = 0.0;
   }
   __syncthreads();
 
@@ -306,10 +332,10 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const double c = cu.c[k];
         const double tp = typical_price(cu.h[k], cu.l[k], c);
         const double mf = tp * cu.v[k];
-        sC[pb + k] = c;
-        sTR[pb + k] = true_range(cu.h[k], cu.l[k], pc);
-        sO4[pb + k] = ohlc4(cu.o[k], cu.h[k], cu.l[k], c);
-        sMF[pb + k] = tp > tpp ? mf : (tp < tpp ? -mf : 0.0);
+        sC[RS1(k)] = c;
+        sTR[RS1(k)] = true_range(cu.h[k], cu.l[k], pc);
+        sO4[RS1(k)] = ohlc4(cu.o[k], cu.h[k], cu.l[k], c);
+        sMF[RS1(k)] = tp > tpp ? mf : (tp < tpp ? -mf : 0.0);
         if (t == 0 || c != pc) run = t;
         lcl[k] = run;
         pc = c;
@@ -332,7 +358,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
       for (int k = 0; k < EN_K; ++k) {
         acc = dd_add1(acc, cu.c[k]);
         Ploc[k] = dd_round(acc);
-        sP[pb + k] = Ploc[k];
+        sP[RS1(k)] = Ploc[k];
       }
     }
     // EMA state scan: thread map from the zero state, then wave inclusive scan
@@ -473,6 +499,8 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
     auto windows = [&](auto fullc) {
       constexpr bool FULL = decltype(fullc)::value;
       const int gstart = EN_H - t0;   // ring position of candle 0 (tile 0 only)
+      const int lb = pb / EN_K;
+      (void)lb;
       auto warm = [&](int t, int win) { return !FULL && t < win - 1; };
       auto put = [&](double* col, const double (&x)[EN_K]) {
         if (FULL) store4(col + orow, tb, T, true, x);
@@ -486,13 +514,13 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         if (lcl[k] <= t - win + 1) return cu.c[k];
         const int q = p - win;
         const double base = q >= wstart ? wbw : wbp;
-        return div_exact((Ploc[k] + wbw) - (sP[q] + base), (double)win, inv);
+        return div_exact((Ploc[k] + wbw) - (sP[RS(k - win)] + base), (double)win, inv);
       };
       double res[EN_K];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         if (P.out[BQ_MA_FAST + i]) {
-          const int win = P.ma[i];
+          const int win = __builtin_amdgcn_readfirstlane(P.ma[i]);
           const double inv = P.inv_ma[i];
 #pragma unroll
           for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, inv, k);
@@ -503,13 +531,13 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         // mean from the prefix; variance from sliding sums of (c - r), (c - r)^2
         // with the lane-local reference r = close at the lane's first candle.
         double up[EN_K], mid[EN_K], lo[EN_K];
-        const int win = P.bb_w;
+        const int win = __builtin_amdgcn_readfirstlane(P.bb_w);
         const double bk = P.bb_k, invw = P.inv_bb, invdv = P.inv_bb_dv;
         const bool okdv = win > P.bb_ddof;
         const double r = cu.c[0];
         double s1 = 0.0, s2 = 0.0;
-        for (int i = FULL ? pb - win + 1 : max(pb - win + 1, gstart); i <= pb; ++i) {
-          const double d = sC[i] - r;
+        for (int x = FULL ? 1 - win : max(1 - win, gstart - pb); x <= 0; ++x) {
+          const double d = sC[RS(x)] - r;
           s1 += d;
           s2 = fma(d, d, s2);
         }
@@ -518,7 +546,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
           const int t = tb + k, p = pb + k;
           if (k > 0) {
             const double dn = cu.c[k] - r;
-            const double dol = (FULL || p - win >= gstart) ? sC[p - win] - r : 0.0;
+            const double dol = (FULL || p - win >= gstart) ? sC[RS(k - win)] - r : 0.0;
             s1 = (s1 + dn) - dol;
             s2 = fma(-dol, dol, fma(dn, dn, s2));
           }
@@ -544,11 +572,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         // c_t - c_{t-w} (telescoping): RSI = 50 (1 + D / A). Counts of up
         // and down moves make the all-gain (100), all-loss (0) and flat (NaN)
         // windows exact. d of candle 0 is NaN -> contributes nothing.
-        const int win = P.rsi_w;
-        double A = 0.0, prev = sC[pb - win];
+        const int win = __builtin_amdgcn_readfirstlane(P.rsi_w);
+        double A = 0.0, prev = sC[RS(-win)];
         int nup = 0, ndn = 0;
-        for (int i = pb - win + 1; i <= pb; ++i) {
-          const double c = sC[i], d = c - prev;
+        for (int x = 1 - win; x <= 0; ++x) {
+          const double c = sC[RS(x)], d = c - prev;
           A += fmax(fabs(d), 0.0);   // fmax drops the NaN of candle 0
           nup += d > 0.0;
           ndn += d < 0.0;
@@ -559,7 +587,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
           const int t = tb + k, p = pb + k;
           if (k > 0) {
             const double d = cu.c[k] - cu.c[k - 1];
-            const double dold = sC[p - win] - sC[p - win - 1];
+            const double dold = sC[RS(k - win)] - sC[RS(k - win - 1)];
             A = (A + fabs(d)) - fmax(fabs(dold), 0.0);
             nup += (d > 0.0) - (dold > 0.0);
             ndn += (d < 0.0) - (dold < 0.0);
@@ -568,8 +596,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
             res[k] = qnan();
             continue;
           }
-          const int q0 = FULL ? p - win : max(p - win, gstart);
-          const double D = cu.c[k] - sC[q0];
+          const double D = cu.c[k] - sC[FULL ? RS(k - win) : (p - win >= gstart ? RS(k - win) : LX(gstart))];
           double v;
           if (nup == 0 && ndn == 0) v = qnan();
           else if (ndn == 0) v = 100.0;
@@ -580,12 +607,13 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         put(P.out[BQ_RSI], res);
       }
       // sliding mean of a per-candle ring array with the same-value rule
-      auto smean = [&](const double* Q, int win, double inv, bool nonneg) {
+      auto smean = [&](const double* Q, int win_, double inv, bool nonneg) {
+        const int win = __builtin_amdgcn_readfirstlane(win_);
         const double wd = (double)win;
         double sum = 0.0, pq = qnan();
         int run = 0;
-        for (int i = pb - win + 1; i <= pb; ++i) {
-          const double q = Q[i];
+        for (int x = 1 - win; x <= 0; ++x) {
+          const double q = Q[RS(x)];
           sum += q;
           run = q == pq ? run + 1 : 1;
           pq = q;
@@ -594,8 +622,8 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k, p = pb + k;
           if (k > 0) {
-            const double q = Q[p];
-            sum = (sum + q) - Q[p - win];
+            const double q = Q[RS(k)];
+            sum = (sum + q) - Q[RS(k - win)];
             run = q == pq ? run + 1 : 1;
             pq = q;
           }
@@ -616,11 +644,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         // MFI = 100 pos / (pos + neg) with pos + neg = B = sum|f| and
         // pos - neg = F = sum f (f = signed flow): MFI = 50 (1 + F / B);
         // counts of up/down flows make the one-sided and empty windows exact.
-        const int win = P.mfi_w;
+        const int win = __builtin_amdgcn_readfirstlane(P.mfi_w);
         double B = 0.0, F = 0.0;
         int nup = 0, ndn = 0;
-        for (int i = pb - win + 1; i <= pb; ++i) {
-          const double f = sMF[i];
+        for (int x = 1 - win; x <= 0; ++x) {
+          const double f = sMF[RS(x)];
           B += fabs(f);
           F += f;
           nup += f > 0.0;
@@ -630,7 +658,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k, p = pb + k;
           if (k > 0) {
-            const double f = sMF[p], fo = sMF[p - win];
+            const double f = sMF[RS(k)], fo = sMF[RS(k - win)];
             B = (B + fabs(f)) - fabs(fo);
             F = (F + f) - fo;
             nup += (f > 0.0) - (fo > 0.0);
@@ -658,12 +686,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
       if (pb >= EN_TT) {
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
-          const int d = pb + k - EN_TT;
-          sP[d] = Ploc[k] - plast;   // re-based: halo prefix ends at 0
-          sC[d] = sC[pb + k];
-          sTR[d] = sTR[pb + k];
-          sO4[d] = sO4[pb + k];
-          sMF[d] = sMF[pb + k];
+          sP[RS1(k - EN_TT)] = Ploc[k] - plast;   // re-based: halo prefix ends at 0
+          sC[RS1(k - EN_TT)] = sC[RS1(k)];
+          sTR[RS1(k - EN_TT)] = sTR[RS1(k)];
+          sO4[RS1(k - EN_TT)] = sO4[RS1(k)];
+          sMF[RS1(k - EN_TT)] = sMF[RS1(k)];
         }
       }
       if (tid == EN_NT - 1) {

@@ -108,6 +108,27 @@ def window_features(h, l, c) -> dict[str, np.ndarray] | None:
                 above_ema50=latest > ema50, trend_score=trend, atr_pct=atr_pct, bb_width=bb_width)
 
 
+def exact_bb_width(closes) -> float:
+    """bb_width of _compute_symbol_features (:269-281) over the last
+    min(20, n) closes in exact rational arithmetic, rounded once at the end
+    (sqrt in float64 of the exactly computed population variance). pandas'
+    online roll_var (add / remove Welford steps over the whole history)
+    drifts from this by up to ~1e-6 relative when std << mean (a window
+    right after a halted stretch); the parity tests use this value to show
+    such a deviation is pandas' rounding, not the kernel's."""
+    from fractions import Fraction
+    from math import sqrt
+
+    w = [Fraction(float(x)) for x in np.asarray(closes, dtype=np.float64)[-20:]]
+    m = sum(w) / len(w)
+    var = sum((x - m) ** 2 for x in w) / len(w)
+    mid = float(m)
+    if mid == 0:
+        return 0.0
+    sd = sqrt(float(var))
+    return ((mid + 2 * sd) - (mid - 2 * sd)) / abs(mid)
+
+
 def panel_window_features_at(h, l, c, t: int, max_bars: int) -> dict[str, np.ndarray] | None:
     """window_features of every symbol of a [S, T] panel at candle t under the
     MarketStateStore(max_bars) cap."""

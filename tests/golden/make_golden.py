@@ -29,6 +29,19 @@ Fixtures:
   beta_corr.npz         ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:154-194)
                         on every prefix (last-row value), BTC pct_change(96) (:427-430).
                         round_numbers is stubbed to identity: values are unrounded.
+  ohlcv_pins.npz        the frames of the reference's own make_ohlcv_df(n=50, oversold=...)
+                        (tests/test_coinrule_price_tracker.py:148-189) behind its
+                        Indicators.mfi pins (:226-248) and the docstring's RSI < 30 /
+                        MACD < 0 claim for the oversold frame
+  strategy_panel.npz    64 symbols x 1100 candles (tests/golden/panel_gen.py, inputs
+                        regenerated from seeds, digest stored) through the real
+                        ActivityBurstPump.compute_indicators, LiquidationSweepPump
+                        .compute_pump_score, FailedSpikeFade.detect,
+                        _compute_symbol_features (400-bar store window) and the a20
+                        helpers; outputs recorded at 48 sampled positions per symbol
+                        (panel_gen.sample_positions: last rows, tile boundary, random)
+
+Usage: python tests/golden/make_golden.py [--only pins,panel]
 """
 
 from __future__ import annotations
@@ -137,7 +150,13 @@ def write_shim(root: Path) -> None:
 # ---------------------------------------------------------------------------
 # child process: runs with PYTHONPATH=<shim>:/root/reference
 # ---------------------------------------------------------------------------
-def child(out_dir: Path) -> None:
+def child(out_dir: Path, only: set[str] | None = None) -> None:
+    if only:
+        if "pins" in only:
+            ohlcv_pins(out_dir)
+        if "panel" in only:
+            strategy_panel(out_dir)
+        return
     import numpy as np
     import pandas as pd
     from types import SimpleNamespace
@@ -427,7 +446,129 @@ def child(out_dir: Path) -> None:
     store_sequence(out_dir, context_dict)
     # ---- 10. candidate scoring and portfolio selection ------------------------------
     scoring_and_selection(out_dir)
+    # ---- 11. the reference's own pybinbot-boundary frames --------------------------
+    ohlcv_pins(out_dir)
+    # ---- 12. panel-size fixtures ------------------------------------------------------
+    strategy_panel(out_dir)
     print("golden fixtures written to", out_dir)
+
+
+def ohlcv_pins(out_dir: Path) -> None:
+    """The frames of make_ohlcv_df (reference tests/test_coinrule_price_tracker.py:148-189),
+    imported from the reference test module itself."""
+    import importlib.util
+
+    import numpy as np
+
+    spec = importlib.util.spec_from_file_location("ref_test_price_tracker",
+                                                  REFERENCE / "tests" / "test_coinrule_price_tracker.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = {}
+    for case, oversold in (("oversold", True), ("uptrend", False)):
+        df = mod.make_ohlcv_df(n=50, oversold=oversold)
+        for col in ("open", "high", "low", "close", "volume", "close_time"):
+            out[f"{case}__{col}"] = df[col].to_numpy(dtype=float)
+    np.savez(out_dir / "ohlcv_pins.npz", **out)
+
+
+def strategy_panel(out_dir: Path) -> None:
+    """64 x 1100 panel through the reference's per-symbol functions."""
+    from types import SimpleNamespace
+
+    import numpy as np
+    import pandas as pd
+
+    sys.path.insert(0, str(HERE))
+    import panel_gen
+
+    from market_regime.live_market_context_accumulator import LiveMarketContextAccumulator
+    from strategies.activity_burst_pump import ActivityBurstPump
+    from strategies.failed_spike_fade import FailedSpikeFade
+    from strategies.liquidation_sweep_pump import LiquidationSweepPump
+    from strategies.mean_reversion_fade import MeanReversionFade
+    from strategies.range_bb_rsi_mean_reversion import RangeBbRsiMeanReversion
+    from strategies.top_gainer_early_momentum import TopGainerEarlyMomentum
+
+    S, T = 64, 1100
+    P = panel_gen.strategy_panel(S, T)
+    keep, btc = panel_gen.btc_series(T)
+    idx = panel_gen.sample_positions(S, T)
+    out = {"digest": np.array(panel_gen.digest(P)), "positions": idx, "btc_keep": keep}
+    open_time = 1_700_000_000_000 + 900_000 * np.arange(T, dtype=np.int64)
+    dfb = pd.DataFrame({"open_time": open_time[keep], "close": btc[keep]})
+
+    ctx_ns = SimpleNamespace(config=SimpleNamespace(env="test"), symbol="TESTUSDT", kucoin_symbol="TEST-USDT",
+                             exchange=None, binbot_api=None, telegram_consumer=None, market_type=None,
+                             at_consumer=None, _breadth_cross_tolerance=0.05, _autotrade_stress_threshold=0.35,
+                             current_symbol_data=None, price_precision=8, qty_precision=8)
+    abp = ActivityBurstPump(ctx_ns)
+    lsp = object.__new__(LiquidationSweepPump)
+    rec: dict[str, list] = {}
+
+    def put(name, s, series):
+        a = np.asarray(series, dtype=float)
+        rec.setdefault(name, [None] * S)[s] = a[idx[s]]
+
+    tg_keys = ["close", "previous_high", "return_1h", "return_2h", "return_6h", "extension_return",
+               "extension_window_bars", "extension_cap", "candle_return", "volume_ratio", "quote_volume_ratio",
+               "range_position", "upper_wick_fraction", "ema20", "ema50", "atr"]
+    feat_cols = ["close", "return_pct", "ema20", "ema50", "above_ema20", "above_ema50", "trend_score", "atr_pct",
+                 "bb_width"]
+    calib = np.zeros((S, 2))
+    for s in range(S):
+        o, h, l, c, v, qv = (P[f][s] for f in panel_gen.FIELDS)
+        df = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v})
+        if s % 2 == 0:   # with and without quote_asset_volume (activity_burst_pump.py:69-133)
+            df["quote_asset_volume"] = qv
+        for col, ser in abp.compute_indicators(df.copy()).items():
+            if col not in df.columns:
+                put(f"abp__{col}", s, ser)
+        dfl = pd.DataFrame({"open_time": open_time, "open": o, "high": h, "low": l, "close": c, "volume": v})
+        for col, ser in lsp.compute_pump_score(dfl, dfb).items():
+            if col not in dfl.columns:
+                put(f"lsp__{col}", s, ser)
+        dff = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v, "quote_asset_volume": qv})
+        ns = SimpleNamespace(symbol="TESTUSDT", market_type=None, df_15m=dff, telegram_consumer=None,
+                             at_consumer=None, current_symbol_data=None, price_precision=8,
+                             market_breadth_data=None, strategy_cooldowns={}, strategy_states={})
+        fsf = FailedSpikeFade(ns)
+        for col, ser in fsf.detect().items():
+            if col not in dff.columns:
+                put(f"fsf__{col}", s, ser)
+        calib[s] = [fsf.volume_cluster_min_ratio, fsf.price_break_base_threshold]
+        put("a20__rsi", s, MeanReversionFade._rsi(pd.Series(c)))
+        trend, adx, z, feats = [], [], [], []
+        tg = np.full((idx.shape[1], len(tg_keys)), np.nan)
+        st = []
+        dft = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v,
+                            "open_time": open_time, "quote_asset_volume": qv})
+        for j, t in enumerate(idx[s]):
+            trend.append(MeanReversionFade._trend_score(dft["close"].iloc[: t + 1]))
+            adx.append(RangeBbRsiMeanReversion._compute_adx(dft.iloc[: t + 1], 14))
+            z.append(RangeBbRsiMeanReversion._compute_zscore(dft.iloc[: t + 1], 20))
+            vals, status = TopGainerEarlyMomentum._features(dft.iloc[: t + 1])
+            st.append(status)
+            if vals is not None:
+                tg[j] = [vals[k] for k in tg_keys]
+            lo = max(0, t - 400 + 1)   # MarketStateStore(400) history at candle t
+            dfm = pd.DataFrame({"timestamp": open_time[lo : t + 1], "open": o[lo : t + 1], "high": h[lo : t + 1],
+                                "low": l[lo : t + 1], "close": c[lo : t + 1], "volume": v[lo : t + 1]})
+            f = LiveMarketContextAccumulator._compute_symbol_features("SYMUSDT", dfm)
+            feats.append(np.full(len(feat_cols), np.nan) if f is None
+                         else [float(getattr(f, k)) for k in feat_cols])
+        rec.setdefault("a20__trend_score", [None] * S)[s] = np.array(trend, dtype=float)
+        rec.setdefault("a20__adx", [None] * S)[s] = np.array(adx, dtype=float)
+        rec.setdefault("a20__zscore", [None] * S)[s] = np.array(z, dtype=float)
+        rec.setdefault("tg__values", [None] * S)[s] = tg
+        rec.setdefault("tg__status", [None] * S)[s] = np.array(st)
+        rec.setdefault("features", [None] * S)[s] = np.array(feats, dtype=float)
+    for k, rows in rec.items():
+        out[k] = np.stack(rows)
+    out["fsf_calibrated"] = calib
+    out["tg_keys"] = np.array(tg_keys)
+    out["feature_columns"] = np.array(feat_cols)
+    np.savez_compressed(out_dir / "strategy_panel.npz", **out)
 
 
 def scoring_and_selection(out_dir: Path) -> None:
@@ -630,8 +771,11 @@ def pd_frame(rows):
 
 def main() -> None:
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
-        child(Path(sys.argv[2]))
+        child(Path(sys.argv[2]), set(sys.argv[3].split(",")) if len(sys.argv) > 3 and sys.argv[3] else None)
         return
+    only = ""
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        only = sys.argv[2]
     if not REFERENCE.exists():
         sys.exit("make_golden.py runs only where /root/reference is mounted")
     with tempfile.TemporaryDirectory(prefix="bq_shim_") as tmp:
@@ -642,7 +786,7 @@ def main() -> None:
         env["PYTHONDONTWRITEBYTECODE"] = "1"
         env["ENV"] = "ci"
         env["PYTHONHASHSEED"] = "0"   # the accumulator iterates symbol sets: fixed order, stable last bits
-        subprocess.run([sys.executable, __file__, "--child", str(HERE)], check=True, env=env, cwd=tmp)
+        subprocess.run([sys.executable, __file__, "--child", str(HERE), only], check=True, env=env, cwd=tmp)
 
 
 if __name__ == "__main__":

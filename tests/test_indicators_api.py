@@ -68,6 +68,56 @@ def test_enrichment_composition_and_ragged_batch(cuda):
         assert_close(one[c].to_numpy(), w[c].to_numpy(), c, scale=1.0)
 
 
+def _pin_frame(case):
+    """The reference's own make_ohlcv_df(n=50, oversold=...) frame
+    (tests/test_coinrule_price_tracker.py:148-189; tests/golden/ohlcv_pins.npz)."""
+    from pathlib import Path
+
+    z = np.load(Path(__file__).resolve().parent / "golden" / "ohlcv_pins.npz")
+    return pd.DataFrame({k: z[f"{case}__{k}"] for k in ("open", "high", "low", "close", "volume", "close_time")})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["oversold", "uptrend"])
+def test_reference_make_ohlcv_df_pins(cuda, case):
+    """The reference's Indicators.mfi pins (test_coinrule_price_tracker.py:226-248:
+    a float in [0, 100], < 50 on the oversold frame) and make_ohlcv_df's
+    docstring (the oversold frame gives RSI < 30 and a negative MACD; the
+    uptrend "will not be below 30"), through the GPU drop-in on the
+    reference's own frames, and equal to the oracle restatement."""
+    df = _pin_frame(case)
+    m = Indicators.mfi(df.copy())
+    assert isinstance(m, float) and 0.0 <= m <= 100.0
+    assert m == pytest.approx(ref.mfi(df.copy()), rel=1e-9, abs=1e-9)
+    rsi = Indicators.rsi(df=df.copy())["rsi"].iloc[-1]
+    macd = Indicators.macd(df=df.copy())["macd"].iloc[-1]
+    assert rsi == pytest.approx(ref.rsi(df.copy())["rsi"].iloc[-1], rel=1e-9, abs=1e-9)
+    assert macd == pytest.approx(ref.macd(df.copy())["macd"].iloc[-1], rel=1e-9, abs=1e-12)
+    if case == "oversold":
+        assert m < 50.0 and rsi < 30.0 and macd < 0.0
+    else:
+        assert rsi >= 30.0 and macd > 0.0
+    full = indicators_enrichment(df.copy())
+    want = ref.indicators_enrichment(df.copy())
+    for c in ref.CANONICAL:
+        assert_close(full[c].to_numpy(), want[c].to_numpy(), c, scale=100.0)
+
+
+def test_oracle_on_reference_make_ohlcv_df_pins():
+    """The oracle restatement itself satisfies the reference's pins on the
+    reference's frames (CPU): MFI float in [0, 100], < 50 oversold; RSI < 30
+    and MACD < 0 oversold."""
+    for case in ("oversold", "uptrend"):
+        df = _pin_frame(case)
+        m = ref.mfi(df.copy())
+        assert isinstance(m, float) and 0.0 <= m <= 100.0
+        e = ref.indicators_enrichment(df.copy())
+        if case == "oversold":
+            assert m < 50.0 and e["rsi"].iloc[-1] < 30.0 and e["macd"].iloc[-1] < 0.0
+        else:
+            assert e["rsi"].iloc[-1] >= 30.0 and e["macd"].iloc[-1] > 0.0
+
+
 @pytest.mark.gpu
 def test_mfi_bounds_like_reference_test(cuda):
     """tests/test_coinrule_price_tracker.py:226-248: MFI in [0, 100] and < 50

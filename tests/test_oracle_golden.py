@@ -146,3 +146,16 @@ def test_ema_family_panel_equals_per_frame_enrichment():
     got = ref.ema_family_panel(p["close"])
     for k in ("macd", "macd_signal", "ema20", "ema50"):
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+def test_strategy_panel_inputs_regenerate_bit_exact():
+    """tests/golden/strategy_panel.npz records the reference's outputs for the
+    panel_gen inputs; the inputs are regenerated from seeds (digest pinned)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("panel_gen", Path(__file__).resolve().parent / "golden" / "panel_gen.py")
+    pg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pg)
+    z = np.load(Path(__file__).resolve().parent / "golden" / "strategy_panel.npz")
+    assert pg.digest(pg.strategy_panel(*z["positions"].shape[:1], 1100)) == str(z["digest"])
+    np.testing.assert_array_equal(pg.sample_positions(64, 1100), z["positions"])
