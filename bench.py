@@ -429,8 +429,9 @@ def bench_store(args, dev):
         "features_kernel_ms": fms,
         "features_GBps": S * M * 24 / (fms * 1e-3) / 1e9,
         "context_valid": ctx is not None,
-        "includes": "host candle arrays -> one bq_store_update + fresh slots + bq_store_features + breadth + "
-                    "host scoring/annotation, synchronized",
+        "includes": "host candle arrays -> pinned H2D + one bq_store_update, then the context pass as one "
+                    "replayed hipGraph (fresh mask + bq_store_context_features over all slots + breadth + micro "
+                    "regime), one D2H of the reduced partials, host scoring/annotation; synchronized",
     }
 
 

@@ -206,6 +206,8 @@ SIGNATURES: dict[str, tuple] = {
     "bq_beta_corr_pairs": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
+    "bq_store_context_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _I64, _P, _I64, _I32, _PP, _P, _P,
+                                                 _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
     "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
     "bq_fused_eval": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), _I64, _I64, _P]),

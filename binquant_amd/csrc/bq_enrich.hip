@@ -620,7 +620,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         }
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
-          const int t = tb + k, p = pb + k;
+          const int t = tb + k;
           if (k > 0) {
             const double q = Q[RS(k)];
             sum = (sum + q) - Q[RS(k - win)];
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         }
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
-          const int t = tb + k, p = pb + k;
+          const int t = tb + k;
           if (k > 0) {
             const double f = sMF[RS(k)], fo = sMF[RS(k - win)];
             B = (B + fabs(f)) - fabs(fo);

@@ -25,6 +25,8 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <string.h>
+
 namespace bq {
 
 struct StoreArgs {
@@ -73,6 +75,9 @@ __global__ __launch_bounds__(SU_NT) void store_update_kernel(const StoreArgs V, 
   const int64_t b = U.seg[blockIdx.x], e = U.seg[blockIdx.x + 1];
   const int k = (int)(e - b);
   if (k <= 0) return;
+  // a single candle without a close is dropped (market_state_store.py:84);
+  // longer runs arrive compacted by the host
+  if (k == 1 && !(U.f[BQ_CLOSE][b] == U.f[BQ_CLOSE][b])) return;
   const int64_t s = U.slot[b];
   const int M = V.M;
   const int n = V.count[s], h = V.head[s];
@@ -239,52 +244,68 @@ struct RollVar {
   }
 };
 
-// pandas ewm(adjust=False, min_periods=1) over a NaN-free close series
+// pandas ewm(adjust=False, min_periods=1) state over a NaN-free close series
+// (the step is ewm_step below)
 struct Ewm {
   double w, old_wt;
   bool have;
-  __device__ __forceinline__ void step(double x, double alpha, double om) {
-    if (!have) {
-      w = x;
-      have = x == x;
-      old_wt = 1.0;
-      return;
-    }
-    if (x != x) {   // NaN gap: decay only (closes are NaN-free in the store)
-      old_wt *= om;
-      return;
-    }
-    old_wt *= om;
-    if (w != x) {
-      w = old_wt * w + alpha * x;
-      w /= old_wt + alpha;
-    }
-    old_wt = 1.0;
-  }
 };
 
 struct FeatSel {
-  const int64_t* slots;
+  const int64_t* slots;   // selected slots; NULL = slots [0, n) (context mode)
   int64_t n;
   double* feat[BQ_NUM_FEATURES];
   double* close;
   double a20, om20, a50, om50;
+  int ema_div;            // om + alpha != 1.0 for a span: keep pandas' divide
+  // context mode (bq_store_context_features)
+  const int64_t* fresh_ts;   // device scalar: fresh = last == *fresh_ts && count > 0
+  double* fresh;             // [n] 1.0 / 0.0 per counted fresh slot
+  double* btc_out;           // [8] benchmark features, close, fresh flag
+  int64_t btc_slot;
+  int btc_counted;
 };
 
-// Two waves per 64 symbols, one chain set each (the branch on the role is
-// wave-uniform): wave 0 replays the true range, the ATR roll_mean and both
-// EWMs, wave 1 the 20-bar roll_mean and roll_var of the close. The chains are
-// independent and each is the same operation sequence as one lane doing all of
-// them, so the results are unchanged bit for bit; a symbol's per-step work is
-// split over two waves (the replay is latency-bound: 10k symbols fill only 157
-// waves of 64). Wave 1 hands its mean / variance to wave 0 through LDS.
-constexpr int SF_NT = 2 * WAVE;
+// Four waves per 64 symbols, one recurrence chain each (the branch on the
+// role is wave-uniform): wave 0 replays the true range and the ATR roll_mean,
+// wave 1 both EWMs, wave 2 the 20-bar roll_mean, wave 3 the 20-bar roll_var.
+// The chains are independent and each is the same operation sequence as one
+// lane doing all of them, so the results are the pandas values bit for bit;
+// a symbol's per-step work is spread over four waves (the replay is a
+// latency-bound dependent chain per symbol: 10k symbols fill 157 blocks). The
+// next chunk of the rings is loaded into registers while the current one is
+// replayed from LDS. Waves 1-3 hand their results to wave 0 through LDS.
+constexpr int SF_NT = 4 * WAVE;
+constexpr int SF_LD = SF_CT * WAVE / SF_NT;   // elements per thread per field and chunk
 
+template <bool EDIV>
+__device__ __forceinline__ void ewm_step(Ewm& e, double x, double alpha, double om) {
+  if (!e.have) {
+    e.w = x;
+    e.have = x == x;
+    e.old_wt = 1.0;
+    return;
+  }
+  if (x != x) {   // NaN gap: decay only (closes are NaN-free in the store)
+    e.old_wt *= om;
+    return;
+  }
+  e.old_wt *= om;
+  if (e.w != x) {
+    e.w = e.old_wt * e.w + alpha * x;
+    // old_wt + alpha == om + alpha == 1.0 exactly for the store's spans
+    // (checked on the host, EDIV = false): the divide is the identity
+    if (EDIV || e.old_wt != om) e.w /= e.old_wt + alpha;
+  }
+  e.old_wt = 1.0;
+}
+
+template <bool EDIV>
 __global__ __launch_bounds__(SF_NT) void store_features_kernel(const StoreArgs V, const FeatSel F) {
   __shared__ double sX[3][SF_CT * STG_PITCH];   // high, low, close chunk (transposed)
   __shared__ double sTR[SF_ATR][WAVE];          // per-symbol ring of true ranges (wave 0)
-  __shared__ double sCL[SF_BB][WAVE];           // per-symbol ring of closes (wave 1)
-  __shared__ double sMu[WAVE], sVar[WAVE];      // wave 1 -> wave 0 at the end
+  __shared__ double sCL[2][SF_BB][WAVE];        // per-symbol rings of closes (waves 2, 3)
+  __shared__ double sRes[6][WAVE];              // mean, var, ema20, ema50, last close, previous close
   __shared__ int sH[WAVE], sN[WAVE];
   __shared__ int64_t sRow[WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
@@ -292,9 +313,11 @@ __global__ __launch_bounds__(SF_NT) void store_features_kernel(const StoreArgs V
   const int64_t i = (int64_t)blockIdx.x * WAVE + lane;
   const int M = V.M;
   int n = 0;
+  bool fresh = false;
   if (i < F.n) {
-    const int64_t s = F.slots[i];
+    const int64_t s = F.slots ? F.slots[i] : i;
     n = V.count[s];
+    fresh = !F.fresh_ts || (n > 0 && V.last[s] == *F.fresh_ts);
     if (role == 0) {
       sH[lane] = V.head[s];
       sRow[lane] = s * (int64_t)M;
@@ -303,96 +326,136 @@ __global__ __launch_bounds__(SF_NT) void store_features_kernel(const StoreArgs V
     sH[lane] = 0;
     sRow[lane] = 0;
   }
+  // context mode: non-fresh slots are not replayed (except the benchmark,
+  // whose features are needed whatever its freshness)
+  const bool need = fresh || (F.fresh_ts && i == F.btc_slot);
+  if (!need) n = 0;
   if (role == 0) sN[lane] = n;
-  int nmax = n;   // equal in both waves: same symbols
+  int nmax = n;   // equal in every wave: same symbols
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) nmax = max(nmax, __shfl_xor(nmax, d, WAVE));
   __syncthreads();
 
   Ewm e20 = {0.0, 1.0, false}, e50 = {0.0, 1.0, false};
-  RollMean atr, mid;
+  RollMean rm;
   RollVar var;
-  atr.init();
-  mid.init();
+  rm.init();
   double pc = qnan(), c_last = qnan(), c_prev = qnan();
-  for (int t0 = 0; t0 < nmax; t0 += SF_CT) {
-    // coalesced chunk load: element e -> symbol e / CT, candle e % CT of its ring
+  double rh[SF_LD], rl[SF_LD], rc[SF_LD];
+  auto load = [&](int t0) {
 #pragma unroll
-    for (int q = 0; q < SF_CT * WAVE / SF_NT; ++q) {
+    for (int q = 0; q < SF_LD; ++q) {
       const int el = threadIdx.x + SF_NT * q;
-      const int l = el / SF_CT, tt = el % SF_CT, t = t0 + tt;
-      double vh = qnan(), vl = qnan(), vc = qnan();
+      const int l = el / SF_CT, t = t0 + el % SF_CT;
+      rh[q] = rl[q] = rc[q] = qnan();
       if (t < sN[l]) {
         const int64_t p = sRow[l] + ring_at(sH[l], t, M);
-        vh = V.f[BQ_HIGH][p];
-        vl = V.f[BQ_LOW][p];
-        vc = V.f[BQ_CLOSE][p];
+        rh[q] = V.f[BQ_HIGH][p];
+        rl[q] = V.f[BQ_LOW][p];
+        rc[q] = V.f[BQ_CLOSE][p];
       }
-      sX[0][tt * STG_PITCH + l] = vh;
-      sX[1][tt * STG_PITCH + l] = vl;
-      sX[2][tt * STG_PITCH + l] = vc;
+    }
+  };
+  if (nmax > 0) load(0);
+  for (int t0 = 0; t0 < nmax; t0 += SF_CT) {
+#pragma unroll
+    for (int q = 0; q < SF_LD; ++q) {
+      const int el = threadIdx.x + SF_NT * q;
+      const int x = (el % SF_CT) * STG_PITCH + el / SF_CT;
+      sX[0][x] = rh[q];
+      sX[1][x] = rl[q];
+      sX[2][x] = rc[q];
     }
     __syncthreads();
+    if (t0 + SF_CT < nmax) load(t0 + SF_CT);   // in flight during the replay below
     const int m = min(SF_CT, n - t0);
     if (role == 0) {
       for (int j = 0; j < m; ++j) {
         const int t = t0 + j;
         const int x = j * STG_PITCH + lane;
-        const double h = sX[0][x], l = sX[1][x], c = sX[2][x];
-        const double tr = true_range(h, l, pc);
-        if (t >= SF_ATR) atr.remove(sTR[t % SF_ATR][lane]);
-        atr.add(tr);
+        const double tr = true_range(sX[0][x], sX[1][x], pc);
+        if (t >= SF_ATR) rm.remove(sTR[t % SF_ATR][lane]);
+        rm.add(tr);
         sTR[t % SF_ATR][lane] = tr;
-        e20.step(c, F.a20, F.om20);
-        e50.step(c, F.a50, F.om50);
+        pc = sX[2][x];
+      }
+    } else if (role == 1) {
+      for (int j = 0; j < m; ++j) {
+        const double c = sX[2][j * STG_PITCH + lane];
+        ewm_step<EDIV>(e20, c, F.a20, F.om20);
+        ewm_step<EDIV>(e50, c, F.a50, F.om50);
         c_prev = c_last;
         c_last = c;
-        pc = c;
+      }
+    } else if (role == 2) {
+      for (int j = 0; j < m; ++j) {
+        const int t = t0 + j;
+        const double c = sX[2][j * STG_PITCH + lane];
+        if (t >= SF_BB) rm.remove(sCL[0][t % SF_BB][lane]);
+        rm.add(c);
+        sCL[0][t % SF_BB][lane] = c;
       }
     } else {
       for (int j = 0; j < m; ++j) {
         const int t = t0 + j;
         const double c = sX[2][j * STG_PITCH + lane];
         if (t == 0) var.init(c);
-        if (t >= SF_BB) {
-          const double old = sCL[t % SF_BB][lane];
-          mid.remove(old);
-          var.remove(old);
-        }
-        mid.add(c);
+        if (t >= SF_BB) var.remove(sCL[1][t % SF_BB][lane]);
         var.add(c);
-        sCL[t % SF_BB][lane] = c;
+        sCL[1][t % SF_BB][lane] = c;
       }
     }
     __syncthreads();
   }
   if (role == 1) {
-    sMu[lane] = mid.value();
-    sVar[lane] = var.var0();
+    sRes[2][lane] = e20.w;
+    sRes[3][lane] = e50.w;
+    sRes[4][lane] = c_last;
+    sRes[5][lane] = c_prev;
+  } else if (role == 2) {
+    sRes[0][lane] = rm.value();
+  } else if (role == 3) {
+    sRes[1][lane] = var.var0();
   }
   __syncthreads();
   if (role != 0 || i >= F.n) return;
   double ret = qnan(), ema20 = qnan(), ema50 = qnan(), trend = qnan(), atr_pct = qnan(), bbw = qnan();
+  const double cl = sRes[4][lane], cp = sRes[5][lane];
   if (n >= 2) {   // _compute_symbol_features returns None below 2 bars (:249-250)
-    ema20 = e20.w;
-    ema50 = e50.w;
-    const double a = atr.value();
-    const double mu = sMu[lane];
-    double v = sVar[lane];
+    ema20 = sRes[2][lane];
+    ema50 = sRes[3][lane];
+    const double a = rm.value();
+    const double mu = sRes[0][lane];
+    const double v = sRes[1][lane];
     const double sd = v == v ? sqrt(v) : 0.0;   // std(ddof=0).fillna(0)
     const double up = mu + (2.0 * sd), lo = mu - (2.0 * sd);
-    ret = safe_pct(c_last, c_prev);
-    atr_pct = c_last != 0.0 ? a / c_last : 0.0;
+    ret = safe_pct(cl, cp);
+    atr_pct = cl != 0.0 ? a / cl : 0.0;
     bbw = mu != 0.0 ? (up - lo) / fabs(mu) : 0.0;
     trend = ema50 != 0.0 ? (ema20 - ema50) / fabs(ema50) : 0.0;
   }
-  if (F.feat[BQ_F_RETURN]) F.feat[BQ_F_RETURN][i] = ret;
-  if (F.feat[BQ_F_EMA20]) F.feat[BQ_F_EMA20][i] = ema20;
-  if (F.feat[BQ_F_EMA50]) F.feat[BQ_F_EMA50][i] = ema50;
-  if (F.feat[BQ_F_TREND]) F.feat[BQ_F_TREND][i] = trend;
-  if (F.feat[BQ_F_ATR_PCT]) F.feat[BQ_F_ATR_PCT][i] = atr_pct;
-  if (F.feat[BQ_F_BB_WIDTH]) F.feat[BQ_F_BB_WIDTH][i] = bbw;
-  if (F.close) F.close[i] = n >= 1 ? c_last : qnan();
+  const double close = n >= 1 ? cl : qnan();
+  if (F.fresh_ts && i == F.btc_slot && F.btc_out) {
+    F.btc_out[0] = ret;
+    F.btc_out[1] = ema20;
+    F.btc_out[2] = ema50;
+    F.btc_out[3] = trend;
+    F.btc_out[4] = atr_pct;
+    F.btc_out[5] = bbw;
+    F.btc_out[6] = close;
+    F.btc_out[7] = fresh ? 1.0 : 0.0;
+  }
+  // context mode: a row is a counted fresh symbol or NaN
+  const bool row = !F.fresh_ts || (fresh && (i != F.btc_slot || F.btc_counted));
+  if (F.fresh) F.fresh[i] = row ? 1.0 : 0.0;
+  const double nan = qnan();
+  if (F.feat[BQ_F_RETURN]) F.feat[BQ_F_RETURN][i] = row ? ret : nan;
+  if (F.feat[BQ_F_EMA20]) F.feat[BQ_F_EMA20][i] = row ? ema20 : nan;
+  if (F.feat[BQ_F_EMA50]) F.feat[BQ_F_EMA50][i] = row ? ema50 : nan;
+  if (F.feat[BQ_F_TREND]) F.feat[BQ_F_TREND][i] = row ? trend : nan;
+  if (F.feat[BQ_F_ATR_PCT]) F.feat[BQ_F_ATR_PCT][i] = row ? atr_pct : nan;
+  if (F.feat[BQ_F_BB_WIDTH]) F.feat[BQ_F_BB_WIDTH][i] = row ? bbw : nan;
+  if (F.close) F.close[i] = row ? close : nan;
 }
 
 // ---- ordered export -------------------------------------------------------------
@@ -459,24 +522,55 @@ int bq_store_update(const bq_store_view* st, const int64_t* slot, const int64_t*
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
+static int bq_launch_features_impl(const bq_store_view* st, bq::FeatSel& F, void* stream) {
+  using namespace bq;
+  // pandas: comass = (span - 1) / 2, alpha = 1 / (1 + comass)
+  F.a20 = 1.0 / (1.0 + (20.0 - 1.0) / 2.0);
+  F.om20 = 1.0 - F.a20;
+  F.a50 = 1.0 / (1.0 + (50.0 - 1.0) / 2.0);
+  F.om50 = 1.0 - F.a50;
+  F.ema_div = (F.om20 + F.a20) != 1.0 || (F.om50 + F.a50) != 1.0;
+  const unsigned blocks = (unsigned)((F.n + WAVE - 1) / WAVE);
+  if (F.ema_div)
+    hipLaunchKernelGGL(store_features_kernel<true>, dim3(blocks), dim3(SF_NT), 0, (hipStream_t)stream, to_args(st), F);
+  else
+    hipLaunchKernelGGL(store_features_kernel<false>, dim3(blocks), dim3(SF_NT), 0, (hipStream_t)stream, to_args(st), F);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
 int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_sel, double* const* feat,
                       double* close_out, void* stream) {
   using namespace bq;
   if (!view_ok(st) || !slots || !feat || n_sel < 0) return BQ_EINVAL;
   if (n_sel == 0) return BQ_OK;
   FeatSel F;
+  memset(&F, 0, sizeof F);
   F.slots = slots;
   F.n = n_sel;
   for (int i = 0; i < BQ_NUM_FEATURES; ++i) F.feat[i] = feat[i];
   F.close = close_out;
-  // pandas: comass = (span - 1) / 2, alpha = 1 / (1 + comass)
-  F.a20 = 1.0 / (1.0 + (20.0 - 1.0) / 2.0);
-  F.om20 = 1.0 - F.a20;
-  F.a50 = 1.0 / (1.0 + (50.0 - 1.0) / 2.0);
-  F.om50 = 1.0 - F.a50;
-  const unsigned blocks = (unsigned)((n_sel + WAVE - 1) / WAVE);
-  hipLaunchKernelGGL(store_features_kernel, dim3(blocks), dim3(SF_NT), 0, (hipStream_t)stream, to_args(st), F);
-  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+  F.btc_slot = -1;
+  return bq_launch_features_impl(st, F, stream);
+}
+
+int bq_store_context_features(const bq_store_view* st, int64_t n, const int64_t* fresh_ts, int64_t btc_slot,
+                              int btc_counted, double* const* feat, double* close_out, double* fresh_out,
+                              double* btc_out, void* stream) {
+  using namespace bq;
+  if (!view_ok(st) || !fresh_ts || !feat || n < 0 || n > st->capacity || btc_slot >= n) return BQ_EINVAL;
+  if (n == 0) return BQ_OK;
+  FeatSel F;
+  memset(&F, 0, sizeof F);
+  F.slots = nullptr;
+  F.n = n;
+  for (int i = 0; i < BQ_NUM_FEATURES; ++i) F.feat[i] = feat[i];
+  F.close = close_out;
+  F.fresh_ts = fresh_ts;
+  F.fresh = fresh_out;
+  F.btc_out = btc_slot >= 0 ? btc_out : nullptr;
+  F.btc_slot = btc_slot;
+  F.btc_counted = btc_counted;
+  return bq_launch_features_impl(st, F, stream);
 }
 
 int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,

@@ -94,9 +94,12 @@ def _cuda_tensors(obj, out: list) -> list:
         if obj.is_cuda:
             out.append(obj)
     elif isinstance(obj, (list, tuple)):
-        for x in obj:
-            if isinstance(x, torch.Tensor) and x.is_cuda:
-                out.append(x)
+        # sequences of operands are homogeneous: a list whose first entry is
+        # not a tensor (e.g. 10k symbol names of a store tick) is not walked
+        if obj and isinstance(obj[0], torch.Tensor):
+            for x in obj:
+                if isinstance(x, torch.Tensor) and x.is_cuda:
+                    out.append(x)
     elif isinstance(obj, dict):
         for x in obj.values():
             if isinstance(x, torch.Tensor) and x.is_cuda:

@@ -96,21 +96,24 @@ def _on_device(fn):
 
 
 class SortedNames(Sequence):
-    """sorted(names), computed on first access (metadata["fresh_symbols"])."""
+    """sorted(names), computed on first access (metadata["fresh_symbols"]);
+    `names` is an array or a SymbolFeatureRows (whose names are resolved
+    lazily too)."""
 
-    def __init__(self, names: np.ndarray):
-        self._names, self._sorted = names, None
+    def __init__(self, names):
+        self._src, self._sorted = names, None
 
     def _get(self) -> list[str]:
         if self._sorted is None:
-            self._sorted = sorted(self._names.tolist())
+            src = self._src.names if isinstance(self._src, SymbolFeatureRows) else self._src
+            self._sorted = sorted(src.tolist())
         return self._sorted
 
     def __getitem__(self, i):
         return self._get()[i]
 
     def __len__(self) -> int:
-        return int(self._names.size)
+        return len(self._src) if isinstance(self._src, SymbolFeatureRows) else int(self._src.size)
 
     def __eq__(self, other) -> bool:
         return list(self._get()) == list(other)
@@ -119,14 +122,56 @@ class SortedNames(Sequence):
 class SymbolFeatureRows(Mapping):
     """LiveMarketContext.symbol_features as a read-only mapping symbol -> dict
     (the SymbolMarketFeatures fields of market_regime/models.py:53-83 plus the
-    micro-regime annotation), backed by column arrays (`.arrays`, `.slots`,
-    `.names`): the per-symbol dict is only built when a symbol is looked up."""
+    micro-regime annotation), backed by the context pass's per-slot row block,
+    which stays in HBM (one device copy per context) until first use: then one
+    D2H, `.slots` / `.names` / `.arrays` / `.codes` are cut from it, and a
+    per-symbol dict is only built when a symbol is looked up. `rows` may also
+    be a host array."""
 
-    def __init__(self, names: np.ndarray, slots: np.ndarray, arrays: dict[str, np.ndarray], timestamp: int,
-                 codes: np.ndarray | None = None):
-        self.names, self.slots, self.arrays, self.timestamp = names, slots, arrays, timestamp
-        self.codes = codes   # int8 micro-regime codes (bq_micro_regime), chained into the next context
+    def __init__(self, all_names: np.ndarray, rows, count: int, timestamp: int):
+        self._all_names, self._rows_t, self._count, self.timestamp = all_names, rows, int(count), timestamp
+        self._host = self._slots = self._names = self._arrays = self._codes = None
         self._row: dict[str, int] | None = None
+
+    def _block(self) -> np.ndarray:
+        if self._host is None:
+            r = self._rows_t
+            self._host = r.cpu().numpy() if isinstance(r, torch.Tensor) else np.asarray(r)
+            self._rows_t = None
+        return self._host
+
+    @property
+    def slots(self) -> np.ndarray:
+        if self._slots is None:
+            R = self._block()
+            self._slots = np.flatnonzero((R[_R_FRESH] > 0) & ~np.isnan(R[0]))
+        return self._slots
+
+    @property
+    def names(self) -> np.ndarray:
+        if self._names is None:
+            self._names = self._all_names[self.slots]
+        return self._names
+
+    @property
+    def codes(self) -> np.ndarray:   # int8 micro-regime codes (bq_micro_regime)
+        if self._codes is None:
+            self._codes = self._block()[_R_REG, self.slots].astype(np.int8)
+        return self._codes
+
+    @property
+    def arrays(self) -> dict[str, np.ndarray]:
+        if self._arrays is None:
+            sel = self._block()[:, self.slots]
+            nf = len(FEATURE_COLUMNS)
+            a = dict(zip(FEATURE_COLUMNS, sel[:nf]))
+            a.update(close=sel[_R_CLOSE], relative_strength_vs_btc=sel[_R_RS], above_ema20=sel[_R_A20] > 0,
+                     above_ema50=sel[_R_A50] > 0, micro_regime=labels(self.codes),
+                     micro_regime_strength=sel[_R_REG_S],
+                     micro_regime_transition=labels(sel[_R_TR].astype(np.int8), MICRO_TRANSITIONS),
+                     micro_regime_transition_strength=sel[_R_TR_S])
+            self._arrays = a
+        return self._arrays
 
     def _index(self) -> dict[str, int]:
         if self._row is None:
@@ -144,7 +189,7 @@ class SymbolFeatureRows(Mapping):
         return iter(self.names.tolist())
 
     def __len__(self) -> int:
-        return int(self.names.size)
+        return self._count
 
 
 class DeviceMarketStateStore:
@@ -238,22 +283,18 @@ class DeviceMarketStateStore:
         fields = [x.to(self.device, torch.float64).reshape(-1) for x in fields]
         if len(fields) != len(INPUT_FIELDS) or any(x.numel() != slots.numel() for x in fields) or ts.numel() != slots.numel():
             raise ValueError("update_slots: slots, ts and the five OHLCV fields must have one entry per candle")
-        ok = ~torch.isnan(fields[INPUT_FIELDS.index("close")])
         if unique_sorted:
+            # one candle per slot in slot order: the kernel drops a candle
+            # without a close itself (no host round trip)
             if not slots.numel():
                 return
-            if bool(ok.all()):
-                s3, t3, f3 = slots.contiguous(), ts.contiguous(), [x.contiguous() for x in fields]
-            else:
-                idx = torch.nonzero(ok).reshape(-1)
-                if idx.numel() == 0:
-                    return
-                s3, t3, f3 = slots[idx], ts[idx], [x[idx] for x in fields]
+            s3, t3, f3 = slots.contiguous(), ts.contiguous(), [x.contiguous() for x in fields]
             n_seg = s3.numel()
-            seg = torch.arange(n_seg + 1, dtype=torch.int64, device=self.device)
+            seg = self._arange(n_seg + 1)
         else:
             if slots.numel() and (int(slots.min()) < 0 or int(slots.max()) >= self.n_tracked):
                 raise ValueError("update_slots: slot out of range (register symbols first)")
+            ok = ~torch.isnan(fields[INPUT_FIELDS.index("close")])
             idx = torch.nonzero(ok).reshape(-1)
             if idx.numel() == 0:
                 return
@@ -276,14 +317,49 @@ class DeviceMarketStateStore:
         )
         _lib.check(st, "bq_store_update")
 
+    def _arange(self, n: int) -> torch.Tensor:
+        a = getattr(self, "_arange_buf", None)
+        if a is None or a.numel() < n:
+            a = self._arange_buf = torch.arange(max(n, 1024), dtype=torch.int64, device=self.device)
+        return a[:n]
+
+    def _staging(self, n: int) -> dict:
+        """Two pinned host / device staging slots for update_batch: host
+        writes go into the slot whose previous H2D copy has completed (its
+        event), so a tick never waits on the device and never races a copy."""
+        st = getattr(self, "_stage", None)
+        if st is None or st[0]["n"] != n:
+            st = self._stage = [dict(n=n, hf=torch.empty((len(INPUT_FIELDS), n), dtype=torch.float64).pin_memory(),
+                                     ht=torch.empty(n, dtype=torch.int64).pin_memory(),
+                                     df=torch.empty((len(INPUT_FIELDS), n), dtype=torch.float64, device=self.device),
+                                     dt=torch.empty(n, dtype=torch.int64, device=self.device), ev=None)
+                                for _ in range(2)]
+            self._stage_i = 0
+        self._stage_i ^= 1
+        slot = st[self._stage_i]
+        if slot["ev"] is not None:
+            slot["ev"].synchronize()
+        return slot
+
     @_on_device
     def update_batch(self, symbols: Sequence[str], timestamp, open_, high, low, close, volume) -> None:
-        """Many symbols' candles (host arrays, arrival order) in one launch."""
+        """Many symbols' candles (host arrays, arrival order) in one launch:
+        one pinned H2D of the five columns and the timestamps, one
+        bq_store_update, no host synchronisation."""
         slots = self.slots_for(symbols)
-        cols = torch.from_numpy(np.stack([np.asarray(x, dtype=np.float64) for x in (open_, high, low, close, volume)]))
-        cols = cols.to(self.device)
-        self.update_slots(slots, torch.as_tensor(np.ascontiguousarray(timestamp, dtype=np.int64)), list(cols),
-                          unique_sorted=self._slot_cache[2])
+        n = slots.numel()
+        if n == 0:
+            return
+        st = self._staging(n)
+        hf = st["hf"].numpy()
+        for i, x in enumerate((open_, high, low, close, volume)):
+            hf[i] = x
+        st["ht"].numpy()[:] = timestamp
+        st["df"].copy_(st["hf"], non_blocking=True)
+        st["dt"].copy_(st["ht"], non_blocking=True)
+        ev = st["ev"] = st["ev"] or torch.cuda.Event()
+        ev.record()
+        self.update_slots(slots, st["dt"], list(st["df"]), unique_sorted=self._slot_cache[2])
 
     # -- reference API ----------------------------------------------------------------
     @_on_device
@@ -389,7 +465,7 @@ class DeviceLiveMarketContextAccumulator:
         self.group = group
         self._contexts_by_timestamp: dict[int, dict] = {}
         self._context_order: deque[int] = deque(maxlen=64)
-        self.last_symbol_features: dict[str, np.ndarray] | None = None
+        self._regimes: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
 
     # -- reference API ------------------------------------------------------------------
     @_on_device
@@ -441,50 +517,113 @@ class DeviceLiveMarketContextAccumulator:
     def _sharded(self) -> bool:
         return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1
 
+    def _bufs(self) -> "_ContextBuffers":
+        """Persistent device / pinned buffers of the context pass for the
+        store's current shape (re-made when symbols are registered or the
+        rings are re-allocated, which also drops a captured graph)."""
+        store = self.state_store
+        btc_slot = store.slot_of(self.btc_symbol)
+        btc_counted = btc_slot is not None and (not self._sharded() or dist.get_rank(self.group) == 0)
+        key = (store.n_tracked, store._view.ts, btc_slot, btc_counted)
+        b = getattr(self, "_ctx_bufs", None)
+        if b is None or b.key != key:
+            tracked = store.n_tracked - (0 if btc_counted or btc_slot is None else 1)
+            b = _ContextBuffers(key, store.n_tracked, btc_slot, btc_counted, tracked, store.device)
+            self._ctx_bufs = b
+        return b
+
+    def _device_pass(self, b: "_ContextBuffers") -> None:
+        """Everything of one context build that runs on the device, with no
+        host synchronisation (so it can be captured and replayed as one
+        hipGraph): fresh mask + features of every tracked slot
+        (bq_store_context_features), the breadth partial over the fresh rows
+        (bq_breadth_partial, T = 1), the fresh count, relative strength vs
+        the benchmark, above-EMA flags, the micro regime with the previous
+        context's regimes by slot (bq_micro_regime), and one pinned D2H of the
+        per-symbol rows. The timestamp is read from b.ts (device)."""
+        store = self.state_store
+        n = b.n
+        F = b.feat
+        st = _lib.load().bq_store_context_features(
+            ctypes.byref(store._view), n, ctypes.c_void_p(b.ts.data_ptr()),
+            -1 if b.btc_slot is None else int(b.btc_slot), int(b.btc_counted),
+            _lib.ptr_array([F[i].data_ptr() for i in range(len(FEATURE_COLUMNS))]),
+            ctypes.c_void_p(b.close.data_ptr()), ctypes.c_void_p(b.fresh.data_ptr()),
+            ctypes.c_void_p(b.small[_BTC0:].data_ptr()), engine._stream_handle(None))
+        _lib.check(st, "bq_store_context_features")
+        npart = len(_lib.PARTIAL_COLUMNS)
+        fz = {k: F[i].view(n, 1) for i, k in enumerate(FEATURE_COLUMNS)}
+        engine.breadth_partial(b.close.view(n, 1), fz, out=b.small[:npart].view(1, npart))
+        torch.sum(b.fresh, 0, keepdim=True, out=b.small[npart : npart + 1])
+        ret, e20, e50 = F[0], F[1], F[2]
+        btc_ret = b.small[_BTC0 : _BTC0 + 1]
+        btc_ok = btc_ret == btc_ret
+        rs = torch.where(btc_ok, ret - btc_ret, torch.zeros_like(ret))
+        if b.btc_slot is not None:
+            rs.narrow(0, b.btc_slot, 1).fill_(0.0)   # the benchmark's own relative strength stays 0 (:117-123)
+        a20, a50 = b.close > e20, b.close > e50
+        ann = micro_regime(F[3], a20, a50, rs, F[5], F[4], ret, prev_regime=b.prev_code,
+                           prev_strength=b.prev_strength, device=store.device)
+        rows = b.rows
+        rows[: len(FEATURE_COLUMNS)].copy_(F)
+        rows[_R_CLOSE].copy_(b.close)
+        rows[_R_RS].copy_(rs)
+        rows[_R_A20].copy_(a20)
+        rows[_R_A50].copy_(a50)
+        rows[_R_REG].copy_(ann["micro_regime"])
+        rows[_R_REG_S].copy_(ann["micro_regime_strength"])
+        rows[_R_TR].copy_(ann["micro_regime_transition"])
+        rows[_R_TR_S].copy_(ann["micro_regime_transition_strength"])
+        rows[_R_FRESH].copy_(b.fresh)
+        listed = (b.fresh > 0) & (ret == ret)   # the rows of symbol_features
+        torch.where(listed, ann["micro_regime"], torch.full_like(ann["micro_regime"], -1), out=b.code)
+        b.strength.copy_(ann["micro_regime_strength"])
+        torch.sum(listed, 0, keepdim=True, dtype=torch.float64, out=b.small[_N_LISTED : _N_LISTED + 1])
+
     def _build_context(self, timestamp: int) -> dict | None:
         store = self.state_store
-        dev = store.device
-        fresh = store.fresh_slots(timestamp)
-        btc_slot = store.slot_of(self.btc_symbol)
-        btc_fresh = btc_slot is not None and bool((fresh == btc_slot).any())
-        # the benchmark is replicated on every rank: only rank 0 counts it
-        btc_counted = btc_slot is not None and (not self._sharded() or dist.get_rank(self.group) == 0)
-        if btc_slot is not None and not btc_counted:
-            fresh = fresh[fresh != btc_slot]
-        n_fresh = fresh.numel()
-        sel = fresh if btc_slot is None else torch.cat([fresh, torch.tensor([btc_slot], dtype=torch.int64, device=dev)])
-        feats, close = store.features(sel)
-        fz = {k: v[:n_fresh].reshape(n_fresh, 1) for k, v in feats.items()}
-        npart = len(_lib.PARTIAL_COLUMNS)
-        red = torch.zeros(npart + 2, dtype=torch.float64, device=dev)
-        if n_fresh:
-            engine.breadth_partial(close[:n_fresh].reshape(n_fresh, 1), fz, out=red[:npart].view(1, -1))
-        red[npart] = float(n_fresh)
-        red[npart + 1] = float(store.n_tracked - (0 if btc_counted or btc_slot is None else 1))
-        if self._sharded():
+        b = self._bufs()
+        n = b.n
+        previous = self._get_previous_context(timestamp)
+        prev = self._regimes.get(previous["timestamp"]) if previous is not None else None
+        b.set_previous(prev)
+        b.ts_host[0] = int(timestamp)
+        b.ts.copy_(b.ts_host, non_blocking=True)
+        sharded = self._sharded()
+        if n and not sharded and _GRAPHS:
+            b.run(lambda: self._device_pass(b))
+        elif n:
+            self._device_pass(b)
+        small = b.small
+        if sharded:
+            # reduce a copy: b.small keeps this rank's tracked count for the next build
+            small = small.clone()
+            npart = len(_lib.PARTIAL_COLUMNS)
+            red = small[: npart + 2]
             if dist.get_backend(self.group) == "gloo":   # CPU rehearsal of the sharded path
                 red_c = red.cpu()
                 dist.all_reduce(red_c, op=dist.ReduceOp.SUM, group=self.group)
-                red = red_c
+                red.copy_(red_c)
             else:   # RCCL over xGMI: one all-reduce of 12 doubles
                 dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group)
-        red_h = red.cpu().numpy()
+        b.small_host.copy_(small, non_blocking=True)
+        rows_dev = b.rows.clone()   # this context's row block stays in HBM (read on access)
+        torch.cuda.current_stream(store.device).synchronize()
+        red_h = b.small_host.numpy()
+        npart = len(_lib.PARTIAL_COLUMNS)
         total_fresh, total_tracked = int(red_h[npart]), int(red_h[npart + 1])
         required = max(REQUIRED_FRESH_SYMBOLS, ceil(total_tracked * MIN_COVERAGE_RATIO))
         if total_fresh < required:
             return None
-        if btc_slot is not None:
-            btc_ret = float(feats["return_pct"][n_fresh])
-            btc_trend = float(feats["trend_score"][n_fresh])
-        else:
-            btc_ret = btc_trend = float("nan")
+        btc_ret = float(red_h[_BTC0]) if b.btc_slot is not None else float("nan")
+        btc_trend = float(red_h[_BTC0 + 3]) if b.btc_slot is not None else float("nan")
         btc_valid = not np.isnan(btc_ret)
+        btc_fresh = b.btc_slot is not None and bool(red_h[_BTC0 + 7] > 0)
         batch = score_contexts(
             red_h[None, :npart], np.array([btc_ret if btc_valid else 0.0]),
             np.array([btc_trend if btc_valid else 0.0]), np.array([btc_valid]), total_tracked=total_tracked,
             fresh_count=np.array([total_fresh]), timestamps=np.array([timestamp]),
         )
-        previous = self._get_previous_context(timestamp)
         batch = annotate_market(batch, previous)
         ctx = batch.context_at(0)
         if ctx is None:
@@ -492,48 +631,95 @@ class DeviceLiveMarketContextAccumulator:
         ctx["btc_symbol"] = self.btc_symbol
         ctx["confidence"] = 1.0
         ctx["is_provisional"] = False
-        # this rank's fresh symbols with relative strength + micro regime
-        # (regime_transitions.py:162-232), previous micro regime chained by
-        # slot; everything vectorised, per-symbol dicts built on access only
-        # micro regime of every fresh symbol on the device (bq_micro_regime);
-        # the previous context's regimes are matched by slot on the host
-        slots = fresh.cpu().numpy()
-        prev_sf = (previous or {}).get("symbol_features")
-        prev_code = np.full(slots.size, -1, dtype=np.int8)
-        prev_str = np.zeros(slots.size)
-        if isinstance(prev_sf, SymbolFeatureRows) and prev_sf.slots.size:
-            j = np.minimum(np.searchsorted(prev_sf.slots, slots), prev_sf.slots.size - 1)
-            hit = prev_sf.slots[j] == slots
-            prev_code[hit] = prev_sf.codes[j[hit]]
-            prev_str[hit] = prev_sf.arrays["micro_regime_strength"][j[hit]]
-        fd = {k: v[:n_fresh] for k, v in feats.items()}
-        cd = close[:n_fresh]
-        rs_d = fd["return_pct"] - btc_ret if btc_valid else torch.zeros_like(fd["return_pct"])
-        if btc_slot is not None:
-            rs_d = torch.where(fresh == btc_slot, torch.zeros_like(rs_d), rs_d)
-        a20, a50 = cd > fd["ema20"], cd > fd["ema50"]
-        ann = micro_regime(fd["trend_score"], a20, a50, rs_d, fd["bb_width"], fd["atr_pct"], fd["return_pct"],
-                           prev_regime=prev_code, prev_strength=prev_str, device=dev)
-        stacked = torch.stack([fd[k] for k in FEATURE_COLUMNS] + [
-            cd, rs_d, a20.double(), a50.double(), ann["micro_regime"].double(), ann["micro_regime_strength"],
-            ann["micro_regime_transition"].double(), ann["micro_regime_transition_strength"]]).cpu().numpy()
-        nf = len(FEATURE_COLUMNS)
-        ok = ~np.isnan(stacked[0])
-        stacked, slots = stacked[:, ok], slots[ok]
-        codes = stacked[nf + 4].astype(np.int8)
-        arrays = dict(zip(FEATURE_COLUMNS, stacked[:nf]))
-        arrays.update(close=stacked[nf], relative_strength_vs_btc=stacked[nf + 1], above_ema20=stacked[nf + 2] > 0,
-                      above_ema50=stacked[nf + 3] > 0, micro_regime=labels(codes),
-                      micro_regime_strength=stacked[nf + 5],
-                      micro_regime_transition=labels(stacked[nf + 6].astype(np.int8), MICRO_TRANSITIONS),
-                      micro_regime_transition_strength=stacked[nf + 7])
-        names = store.names_array()[slots]
-        sym = SymbolFeatureRows(names, slots, arrays, int(timestamp), codes)
+        # this rank's counted fresh symbols with features: per-symbol rows with
+        # relative strength + micro regime (regime_transitions.py:162-232),
+        # cut from the row block on access
+        sym = SymbolFeatureRows(store.names_array(), rows_dev, int(red_h[_N_LISTED]), int(timestamp))
         ctx["symbol_features"] = sym
         ctx["metadata"] = {
             "btc_fresh": btc_fresh,
             "btc_used_for_regime": btc_valid,
-            "fresh_symbols": SortedNames(sym.names),
+            "fresh_symbols": SortedNames(sym),
             "fresh_symbol_count": int(ctx["fresh_count"]),
         }
+        # this context's micro regimes by slot (-1 outside its symbol_features),
+        # for the next context's transitions
+        self._regimes[int(timestamp)] = (b.code.clone(), b.strength.clone())
+        keep = set(self._context_order) | {int(timestamp)}
+        for t in [t for t in self._regimes if t not in keep]:
+            del self._regimes[t]
         return ctx
+
+
+# rows of the per-symbol D2H block (_ContextBuffers.rows)
+_R_CLOSE, _R_RS, _R_A20, _R_A50, _R_REG, _R_REG_S, _R_TR, _R_TR_S, _R_FRESH = range(6, 15)
+_N_ROWS = 15
+# small buffer: [10 partials, fresh, tracked, 8 benchmark values, rows listed in symbol_features]
+_BTC0 = len(_lib.PARTIAL_COLUMNS) + 2
+_N_LISTED = _BTC0 + 8
+_GRAPHS = __import__("os").environ.get("BQ_STORE_GRAPH", "1") != "0"
+
+
+class _ContextBuffers:
+    """Fixed-address buffers of one store shape (n tracked slots) for the
+    context pass, and its captured hipGraph (built on the second build of the
+    same shape: the first runs eagerly and warms the allocator and caches)."""
+
+    def __init__(self, key, n: int, btc_slot, btc_counted: bool, tracked: int, dev) -> None:
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.key, self.n, self.btc_slot, self.btc_counted = key, n, btc_slot, btc_counted
+        self.ts = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ts_host = torch.zeros(1, dtype=torch.int64).pin_memory()
+        self.feat = torch.empty((len(FEATURE_COLUMNS), max(n, 1)), **f64)[:, :n]
+        self.close = torch.empty(n, **f64)
+        self.fresh = torch.empty(n, **f64)
+        self.small = torch.full((_N_LISTED + 1,), float("nan"), **f64)
+        self.small[: _BTC0].zero_()
+        self.small[_BTC0 - 1] = float(tracked)
+        self.small[_N_LISTED] = 0.0
+        self.small_host = torch.zeros(_N_LISTED + 1, dtype=torch.float64).pin_memory()
+        self.prev_code = torch.full((n,), -1, dtype=torch.int8, device=dev)
+        self.prev_strength = torch.zeros(n, **f64)
+        self.code = torch.full((n,), -1, dtype=torch.int8, device=dev)
+        self.strength = torch.zeros(n, **f64)
+        self.rows = torch.empty((_N_ROWS, n), **f64)
+        self.graph = None
+        self.runs = 0
+
+    def set_previous(self, prev) -> None:
+        """Copy the previous context's regimes (by slot) into the fixed
+        buffers the pass reads; -1 / 0 for slots it did not have."""
+        if prev is None:
+            self.prev_code.fill_(-1)
+            self.prev_strength.zero_()
+            return
+        code, strength = prev
+        m = min(self.n, code.numel())
+        self.prev_code[:m].copy_(code[:m])
+        self.prev_strength[:m].copy_(strength[:m])
+        if m < self.n:
+            self.prev_code[m:].fill_(-1)
+            self.prev_strength[m:].zero_()
+
+    def run(self, fn) -> None:
+        self.runs += 1
+        if self.graph is not None:
+            self.graph.replay()
+            return
+        if self.runs < 2:
+            fn()
+            return
+        s = torch.cuda.Stream(device=self.ts.device)
+        s.wait_stream(torch.cuda.current_stream(self.ts.device))
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            fn()   # warm-up on the capture stream
+            s.synchronize()
+            g.capture_begin()
+            try:
+                fn()
+            finally:
+                g.capture_end()
+        torch.cuda.current_stream(self.ts.device).wait_stream(s)
+        self.graph = g
+        g.replay()

@@ -389,6 +389,23 @@ int bq_store_update(const bq_store_view* st, const int64_t* slot, const int64_t*
 int bq_store_features(const bq_store_view* st, const int64_t* slots, int64_t n_sel, double* const* feat,
                       double* close_out, void* stream);
 /*
+ * The per-symbol pass of one live context build
+ * (LiveMarketContextAccumulator._build_context,
+ * market_regime/live_market_context_accumulator.py:95-133) over ALL n tracked
+ * slots [0, n): a slot is fresh when its last closed candle is *fresh_ts
+ * (MarketStateStore.get_fresh_symbols, market_state_store.py:49-54; fresh_ts
+ * is a device pointer, so a captured graph reads the tick's timestamp).
+ * feat / close_out rows: the features of counted fresh slots, NaN otherwise
+ * (the benchmark's row only when btc_counted: a sharded store replicates the
+ * benchmark and counts it on one rank); fresh_out[n]: 1.0 / 0.0 for those
+ * rows; btc_out[8]: the benchmark's features, latest close (whatever its
+ * freshness, :105-106) and 1.0 / 0.0 = fresh (unwritten when btc_slot < 0). Same replay as
+ * bq_store_features (pandas bit for bit); non-fresh slots are not replayed.
+ */
+int bq_store_context_features(const bq_store_view* st, int64_t n, const int64_t* fresh_ts, int64_t btc_slot,
+                              int btc_counted, double* const* feat, double* close_out, double* fresh_out,
+                              double* btc_out, void* stream);
+/*
  * MarketStateStore.get_symbol_history / get_all_histories: time-ordered copy
  * of n_sel slots into ts_out / out[BQ_NUM_INPUTS] [n_sel][ld_out]
  * (ld_out >= max_bars; NaN / 0 past each slot's count; NULL = skip).
