@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/${1:-gpurun_out/pmc}
 mkdir -p $OUT
 cd /tmp
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-tick --no-breadth --no-rows"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-tick --no-breadth --no-rows --no-shard"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \

@@ -4,7 +4,7 @@ numbers for one kernel; writes the `traffic` figure bench.py reports.
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half
 of the bytes of a wide (16 B/lane) coalesced streaming read, so it is doubled;
 WRITE_SIZE is exact for 16-B-per-lane streaming stores. Units: KiB.
-Usage: python tools/pmc_summary.py <pmc_dir> <kernel_substring> <out.json> [label]
+Usage: python tools/pmc_summary.py <pmc_dir> <kernel_substring> <out.json> [label] [candles_per_launch]
 """
 import csv
 import glob
@@ -14,6 +14,7 @@ from collections import defaultdict
 
 pmc_dir, kern, out = sys.argv[1], sys.argv[2], sys.argv[3]
 label = sys.argv[4] if len(sys.argv) > 4 else pmc_dir
+candles = int(sys.argv[5]) if len(sys.argv) > 5 else None
 agg = defaultdict(lambda: defaultdict(float))
 for f in sorted(glob.glob(f"{pmc_dir}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
@@ -30,6 +31,7 @@ except (OSError, ValueError):
 allk[kern] = {
     "source": label,
     "bytes_per_launch": fetch + write,
+    "candles_per_launch": candles,
     "fetch_bytes_corrected": fetch,
     "write_bytes": write,
     "counters_mean_per_dispatch": mean,
