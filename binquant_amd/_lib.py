@@ -203,6 +203,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_resample": (ctypes.c_int, [_P, _PP, _P, _I32, _P, _I64, _I64, _I64, _I64, _P, _PP, _I64, _P]),
     "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),
     "bq_join_returns": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
+    "bq_beta_corr_bret": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_beta_corr_pairs": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),
@@ -216,6 +217,9 @@ SIGNATURES: dict[str, tuple] = {
     "bq_fused_source": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), ctypes.c_char_p, _I64, ctypes.POINTER(_I64)]),
     "bq_fused_compile": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram)]),
     "bq_fused_stats": (ctypes.c_int, [ctypes.POINTER(_I64)] * 3),
+    "bq_wilder_rsi": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _I64, _P]),
+    "bq_zscore": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _I64, _P]),
+    "bq_adx": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _I64, _P]),
     "bq_micro_regime": (ctypes.c_int, [_I64] + [_P] * 13 + [_P]),
     "bq_context_score": (ctypes.c_int, [_I64, _P, _P, _P, _P, ctypes.POINTER(BqContextScalars),
                                         ctypes.POINTER(BqScorerWeights), _P, _I64, _P]),

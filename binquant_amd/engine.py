@@ -400,12 +400,59 @@ def beta_corr(
     btc = _check_panel(btc_close.reshape(1, -1), "btc_close", (1, T)).contiguous()
     beta = torch.empty((S, T), dtype=torch.float64, device=close.device)
     corr = torch.empty_like(beta)
-    st = _lib.load().bq_beta_corr(
-        ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(btc.data_ptr()), S, T, _row_stride(close),
+    # the benchmark's log returns once per call (log(c / c.shift(1)), :166-169),
+    # shared by every symbol row of the kernel (bq_beta_corr_bret)
+    bret = torch.full((T,), float("nan"), dtype=torch.float64, device=close.device)
+    if T > 1:
+        torch.log(btc[0, 1:] / btc[0, :-1], out=bret[1:])
+    scratch = torch.empty(2 * T, dtype=torch.float64, device=close.device)   # benchmark window stats
+    st = _lib.load().bq_beta_corr_bret(
+        ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(bret.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+        S, T, _row_stride(close),
         int(window), ctypes.c_void_p(beta.data_ptr()), ctypes.c_void_p(corr.data_ptr()), T, _stream_handle(stream),
     )
-    _lib.check(st, "bq_beta_corr")
+    _lib.check(st, "bq_beta_corr_bret")
     return {"beta": beta, "corr": corr}
+
+
+def _signal_launch(name: str, ins: list[torch.Tensor], window: int, stream) -> torch.Tensor:
+    S, T = ins[-1].shape
+    ld = _row_stride(ins[0])
+    if any(_row_stride(t) != ld for t in ins):
+        ins = [t.contiguous() for t in ins]
+        ld = T
+    out = torch.empty((S, T), dtype=torch.float64, device=ins[0].device)
+    st = getattr(_lib.load(), name)(*[ctypes.c_void_p(t.data_ptr()) for t in ins], S, T, ld, int(window),
+                                    ctypes.c_void_p(out.data_ptr()), T, _stream_handle(stream))
+    _lib.check(st, name)
+    return out
+
+
+@device_entry
+def wilder_rsi(close: torch.Tensor, window: int = 14, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """MeanReversionFade._rsi (strategies/mean_reversion_fade.py:88-109) at
+    every t, time-parallel (bq_wilder_rsi; 1e-9 of pandas, finite closes)."""
+    close = _check_panel(close, "close")
+    return _signal_launch("bq_wilder_rsi", [close], window, stream)
+
+
+@device_entry
+def zscore(close: torch.Tensor, window: int = 20, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """RangeBbRsiMeanReversion._compute_zscore (strategies/range_bb_rsi_mean_reversion.py:132-138)
+    at every t, time-parallel (bq_zscore)."""
+    close = _check_panel(close, "close")
+    return _signal_launch("bq_zscore", [close], window, stream)
+
+
+@device_entry
+def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int = 14,
+        stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """RangeBbRsiMeanReversion._compute_adx (strategies/range_bb_rsi_mean_reversion.py:101-130)
+    at every t, time-parallel (bq_adx, window <= 64)."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    return _signal_launch("bq_adx", [_check_panel(high, "high", (S, T)), _check_panel(low, "low", (S, T)), close],
+                          window, stream)
 
 
 @device_entry

@@ -18,9 +18,12 @@ prefix frame df.iloc[:t + 1]:
                      (strategies/top_gainer_early_momentum.py:92-160)
 * mean_reversion_features  the entry inputs of MeanReversionFade (:240-255)
 
-Everything runs through the bq_rolling / bq_ewm kernels plus fused
-element-wise programs (binquant_amd.fused) in the reference's operation order;
-there is no CPU path.
+wilder_rsi, zscore and adx default to the time-parallel kernels of
+bq_signals.hip (one launch each, 1e-9 of pandas); exact=True runs the
+replay composition instead — the bq_rolling / bq_ewm kernels plus fused
+element-wise programs (binquant_amd.fused) in the reference's operation
+order, equal to pandas bit for bit. The other helpers use that composition.
+There is no CPU path.
 """
 
 from __future__ import annotations
@@ -57,9 +60,11 @@ def _rsi_ex(close: torch.Tensor, window: int) -> F.Ex:
     return F.where(den != 0, 100 * AG / den, 50.0)
 
 
-def wilder_rsi(close: torch.Tensor, window: int = 14) -> torch.Tensor:
+def wilder_rsi(close: torch.Tensor, window: int = 14, exact: bool = False) -> torch.Tensor:
     """Wilder RSI: ewm(alpha=1/window, min_periods=window, adjust=False) of
     gains/losses, 100*g/(g+l), 50 where g+l == 0 (NaN warm-up kept)."""
+    if not exact:
+        return engine.wilder_rsi(close, window)
     return F.run({"rsi": _rsi_ex(close, window)})["rsi"]
 
 
@@ -74,9 +79,12 @@ def trend_score(close: torch.Tensor, fast: int = 20, slow: int = 50) -> torch.Te
     return F.run({"t": _trend_ex(close, fast, slow)})["t"]
 
 
-def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int = 14) -> torch.Tensor:
+def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int = 14,
+        exact: bool = False) -> torch.Tensor:
     """_compute_adx at every t: rolling-sum DI+/DI-, dx NaN -> 0, mean over
     `window`; NaN (short history) -> 100."""
+    if not exact and window <= 64:
+        return engine.adx(high, low, close, window)
     H, L, C = F.inp(high), F.inp(low), F.inp(close)
     hd = F.diff(H, 1)
     ld = -F.diff(L, 1)
@@ -99,9 +107,11 @@ def adx(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor, window: int 
     return F.run({"adx": F.fillna(a, 100.0)})["adx"]
 
 
-def zscore(close: torch.Tensor, window: int = 20) -> torch.Tensor:
+def zscore(close: torch.Tensor, window: int = 20, exact: bool = False) -> torch.Tensor:
     """_compute_zscore at every t: (c - mean) / std(ddof=0); 0 where std is 0
     or NaN."""
+    if not exact:
+        return engine.zscore(close, window)
     mean, std = engine.rolling_many(engine.Roll(close, window, "mean"), engine.Roll(close, window, "std0"))
     SD = F.inp(std)
     bad = (SD == 0) | F.isnan(SD)

@@ -347,6 +347,14 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
  * prefix of each row): beta/corr of rolling(window) at every row, NaN for
  * rows < window - 1.
  */
+/* bq_beta_corr with the benchmark given as its log returns (btc_returns[T],
+ * btc_returns[t] = log(btc[t] / btc[t-1]), NaN at t = 0): the returns are
+ * formed once per call instead of once per symbol row (engine.beta_corr).
+ * scratch: NULL, or 2*T doubles of device memory in which the benchmark's
+ * window mean / variance are computed once (a one-workgroup pre-pass) instead
+ * of in every symbol's workgroup. */
+int bq_beta_corr_bret(const double* close, const double* btc_returns, double* scratch, int64_t S, int64_t T,
+                      int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
 int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in, int32_t window,
                        double* beta, double* corr, int64_t ld_out, void* stream);
 
@@ -412,6 +420,29 @@ int bq_store_context_features(const bq_store_view* st, int64_t n, const int64_t*
  */
 int bq_store_gather(const bq_store_view* st, const int64_t* slots, int64_t n_sel, int64_t* ts_out,
                     double* const* out, int64_t ld_out, void* stream);
+
+/* ---- signal-generator helpers, time-parallel (bq_signals.hip) --------------- */
+/*
+ * The inline helpers of the signal generators at every candle of a [S][T]
+ * panel (column t = the helper on df.iloc[:t + 1]), split along the time axis
+ * (tolerance-exact, 1e-9 relative; the bit-exact replay of the same helpers is
+ * the binquant_amd.signals composition with exact=True). Finite prices in,
+ * out [S][ld_out] fp64 device pointers.
+ *   bq_wilder_rsi  MeanReversionFade._rsi (strategies/mean_reversion_fade.py:88-109):
+ *                  ewm(alpha=1/window, min_periods=window, adjust=False) of
+ *                  gains / losses, 100 g / (g + l), 50 where g + l == 0
+ *   bq_zscore      RangeBbRsiMeanReversion._compute_zscore
+ *                  (strategies/range_bb_rsi_mean_reversion.py:132-138): 0 where
+ *                  the ddof-0 std is 0 or NaN (warm-up included)
+ *   bq_adx         RangeBbRsiMeanReversion._compute_adx (:101-130): 100 where
+ *                  the window mean of dx is NaN; window <= 64
+ */
+int bq_wilder_rsi(const double* close, int64_t S, int64_t T, int64_t ld_in, int32_t window, double* out,
+                  int64_t ld_out, void* stream);
+int bq_zscore(const double* close, int64_t S, int64_t T, int64_t ld_in, int32_t window, double* out, int64_t ld_out,
+              void* stream);
+int bq_adx(const double* high, const double* low, const double* close, int64_t S, int64_t T, int64_t ld_in,
+           int32_t window, double* out, int64_t ld_out, void* stream);
 
 /* ---- regime annotation, candidate scoring, portfolio selection -------------- */
 enum bq_micro_regime_code {   /* models.py:15-21 MicroRegime; -1 = None */

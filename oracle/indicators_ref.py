@@ -283,3 +283,21 @@ def supertrend(df: pd.DataFrame, multiplier: float = 3.0, period: int = 10) -> p
     df["supertrend_upper"] = upper
     df["supertrend_lower"] = lower
     return df
+
+
+def exact_zscore(window_closes) -> float:
+    """RangeBbRsiMeanReversion._compute_zscore (strategies/range_bb_rsi_mean_reversion.py:132-138)
+    of the last close against its window, in exact rational arithmetic (mean
+    and ddof-0 variance exact, one sqrt and one division in float64). pandas'
+    online roll_var drifts from this by up to ~1e-6 relative in windows that
+    are nearly constant (e.g. one candle off a flat run: z = sqrt(w - 1));
+    the parity tests use it to show such a deviation is pandas' rounding."""
+    from fractions import Fraction
+    from math import sqrt
+
+    w = [Fraction(float(v)) for v in np.asarray(window_closes, dtype=np.float64)]
+    m = sum(w) / len(w)
+    var = sum((v - m) ** 2 for v in w) / len(w)
+    if var == 0:
+        return 0.0
+    return float(w[-1] - m) / sqrt(float(var))

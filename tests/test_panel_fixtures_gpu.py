@@ -123,7 +123,19 @@ def test_signal_helpers_panel(cuda, fx):
     _cmp("rsi", _at(z, signals.wilder_rsi(d["close"]).cpu().numpy()), z["a20__rsi"])
     _cmp("trend_score", _at(z, signals.trend_score(d["close"]).cpu().numpy()), z["a20__trend_score"])
     _cmp("adx", _at(z, signals.adx(d["high"], d["low"], d["close"]).cpu().numpy()), z["a20__adx"])
-    _cmp("zscore", _at(z, signals.zscore(d["close"]).cpu().numpy()), z["a20__zscore"])
+    # zscore: nearly constant windows (halted stretches) are computed exactly
+    # by the kernel; pandas' online variance drifts there (tests/util.py)
+    from oracle import indicators_ref
+
+    zs = signals.zscore(d["close"]).cpu().numpy()
+    w = z["a20__zscore"]
+    bad = ~(np.abs(_at(z, zs) - w) <= 1e-9 * np.abs(w) + 1e-11)
+    assert bad.sum() <= 8, int(bad.sum())
+    for s, j in np.argwhere(bad):
+        t = int(z["positions"][s, j])
+        ex = indicators_ref.exact_zscore(P["close"][s, t - 19 : t + 1])
+        assert abs(zs[s, t] - ex) <= 1e-9 * max(abs(ex), 1.0) and abs(w[s, j] - ex) > abs(zs[s, t] - ex), (s, t)
+    np.testing.assert_array_equal(_at(z, signals.zscore(d["close"], exact=True).cpu().numpy()), w)
 
 
 def test_top_gainer_panel(cuda, fx):

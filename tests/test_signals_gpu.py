@@ -9,7 +9,8 @@ import numpy as np
 import pytest
 import torch
 
-from tests.util import assert_close
+from oracle import indicators_ref
+from tests.util import assert_close, assert_close_or_exact
 
 G = Path(__file__).resolve().parent / "golden"
 pytestmark = pytest.mark.gpu
@@ -27,22 +28,25 @@ def _close(got, want, name):
     assert_close(got.cpu().numpy().ravel(), want, name, rtol=1e-9, scale=scale)
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("case", CASES)
-def test_wilder_rsi_and_trend(cuda, case):
+def test_wilder_rsi_and_trend(cuda, case, exact):
     from binquant_amd import signals
 
     z, col = _load(case)
-    _close(signals.wilder_rsi(col("close")), z[f"{case}__rsi"], f"{case}.rsi")
+    _close(signals.wilder_rsi(col("close"), exact=exact), z[f"{case}__rsi"], f"{case}.rsi")
     _close(signals.trend_score(col("close")), z[f"{case}__trend_score"], f"{case}.trend")
 
 
+@pytest.mark.parametrize("exact", [False, True])
 @pytest.mark.parametrize("case", CASES)
-def test_adx_and_zscore(cuda, case):
+def test_adx_and_zscore(cuda, case, exact):
     from binquant_amd import signals
 
     z, col = _load(case)
-    _close(signals.adx(col("high"), col("low"), col("close")), z[f"{case}__adx"], f"{case}.adx")
-    _close(signals.zscore(col("close")), z[f"{case}__zscore"], f"{case}.zscore")
+    _close(signals.adx(col("high"), col("low"), col("close"), exact=exact), z[f"{case}__adx"], f"{case}.adx")
+    assert_close_or_exact(signals.zscore(col("close"), exact=exact).cpu().numpy().ravel(), z[f"{case}__zscore"],
+                          z[f"{case}__close"], 20, indicators_ref.exact_zscore, f"{case}.zscore", max_cases=0 if exact else 8)
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -77,3 +81,32 @@ def test_helpers_batched_equal_rows(cuda):
         one = signals.adx(pan["high"][r:r + 1], pan["low"][r:r + 1], pan["close"][r:r + 1]).cpu().numpy()
         np.testing.assert_array_equal(both[r], one[0])
         np.testing.assert_array_equal(rsi[r], signals.wilder_rsi(pan["close"][r:r + 1]).cpu().numpy()[0])
+
+
+@pytest.mark.parametrize("T", [700, 2048, 2049, 5000])
+def test_time_parallel_helpers_match_exact_replay(cuda, T):
+    """bq_wilder_rsi / bq_zscore / bq_adx (tiles of 2048 candles, carries
+    across tiles) vs the bit-exact replay composition (= pandas) on a
+    multi-wave panel with per-symbol price scales and constant stretches:
+    1e-9 relative; the zscore sign and the RSI 30 / 70 and ADX 25 cuts equal
+    away from a 1e-9 band."""
+    from binquant_amd import signals
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(70, T, seed0=T)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    for name, fast, exact in (
+        ("rsi", signals.wilder_rsi(d["close"]), signals.wilder_rsi(d["close"], exact=True)),
+        ("adx", signals.adx(d["high"], d["low"], d["close"]), signals.adx(d["high"], d["low"], d["close"], exact=True)),
+        ("zscore", signals.zscore(d["close"]), signals.zscore(d["close"], exact=True)),
+    ):
+        g, w = fast.cpu().numpy(), exact.cpu().numpy()
+        scale = 100.0 if name != "zscore" else 1.0
+        if name == "zscore":   # nearly constant windows: pandas' drift, arbitrated by the exact value
+            assert_close_or_exact(g, w, p["close"], 20, indicators_ref.exact_zscore, name, scale=scale)
+        else:
+            assert_close(g, w, name, rtol=1e-9, scale=scale)
+        cuts = {"rsi": (30.0, 70.0), "adx": (25.0,), "zscore": (0.0,)}[name]
+        for c in cuts:
+            far = np.abs(w - c) > 1e-9 * np.maximum(np.abs(w), 1.0)
+            np.testing.assert_array_equal((g > c)[far], (w > c)[far], err_msg=f"{name} cut {c}")
