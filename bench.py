@@ -84,12 +84,22 @@ def parse():
 
 
 def setup_dist(args):
+    """One process per GPU, RCCL ("nccl") over xGMI. BQ_BENCH_BACKEND=gloo
+    rehearses the multi-rank path on fewer GPUs (ranks share devices round-robin,
+    collectives over gloo on host copies): same sharding, same single
+    all-reduce per breadth build, same timing reduction."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("BQ_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -102,7 +112,8 @@ def barrier(world):
 def max_over_ranks(x: float, world: int) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -58,6 +58,7 @@ constexpr int EN_NT = BQ_EN_NT;
 constexpr int EN_NW = EN_NT / WAVE;
 constexpr int EN_K = BQ_EN_K;
 constexpr int EN_TT = EN_NT * EN_K;   // 1024
+constexpr int EN_LK = EN_K == 2 ? 1 : EN_K == 4 ? 2 : 3;   // log2(EN_K)
 constexpr int EN_H = 128;             // halo >= BQ_MAX_WINDOW + 2
 constexpr int EN_R = EN_H + EN_TT;    // 1152
 static_assert(EN_K % 2 == 0 && EN_TT >= EN_H && EN_K * WAVE > BQ_MAX_WINDOW, "tile shape");
@@ -74,7 +75,7 @@ static_assert(EN_K % 2 == 0 && EN_TT >= EN_H && EN_K * WAVE > BQ_MAX_WINDOW, "ti
 // class on all lanes at each step (lane positions differ by multiples of
 // EN_K), so it stays conflict free too.
 #if BQ_EN_LDSPERM
-#define LX(i) ((((i) & (EN_K - 1)) * (EN_R / EN_K)) + ((i) >> 2))
+#define LX(i) ((((i) & (EN_K - 1)) * (EN_R / EN_K)) + ((i) >> EN_LK))
 // slot of ring position pb + x for the lane whose first position is pb
 // (pb % EN_K == 0, lb = pb / EN_K): lb + LX(x), x may be negative (the shift
 // floors). Window offsets x are wave-uniform, so LX(x) is scalar arithmetic
@@ -86,7 +87,7 @@ static_assert(EN_K % 2 == 0 && EN_TT >= EN_H && EN_K * WAVE > BQ_MAX_WINDOW, "ti
 #define RS(x) (pb + (x))
 #define RS1(x) (pb + (x))
 #endif
-static_assert(!BQ_EN_LDSPERM || (EN_K == 4 && EN_R % EN_K == 0), "LX assumes 4 candles per lane");
+static_assert(!BQ_EN_LDSPERM || ((1 << EN_LK) == EN_K && EN_R % EN_K == 0), "LX: power-of-two candles per lane");
 
 // EMA slots in the scan state
 enum { E_FAST = 0, E_SLOW, E_SIG, E_0, E_1, NE };

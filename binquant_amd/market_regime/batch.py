@@ -74,7 +74,12 @@ def reduce_partials(part: torch.Tensor, n_local: int, group=None) -> tuple[torch
     rank the partials are returned with column 9 = n_local."""
     part[:, TRACKED_COLUMN] = float(n_local)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
+        if part.is_cuda and dist.get_backend(group) == "gloo":   # CPU rehearsal of the RCCL path
+            host = part.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            part.copy_(host)
+        else:   # RCCL over xGMI
+            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
         n_total = int(part[0, TRACKED_COLUMN].item()) if part.shape[0] else int(n_local)
         return part, n_total
     return part, int(n_local)
