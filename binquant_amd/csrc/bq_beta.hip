@@ -12,18 +12,23 @@
 //   corr = cov / (var_x * var_y) ** 0.5                 (roll_var, ddof 1)
 // NaN where the window is incomplete (t < window).
 //
-// One 256-thread workgroup per symbol walks the row in tiles of 1024 candles
-// (4 per lane). Per candle the five window sums come from tile-local prefix
-// sums (wave DPP scans + LDS across waves) kept in an LDS ring with a
-// 128-candle halo re-based to end at 0: a window sum is one difference, O(1)
-// per candle whatever the window (the per-lane window walk this replaces cost
-// w + K steps per K candles). The squares are summed about row-constant
-// references (the row's first return) so the variances do not cancel; the
-// means follow pandas' roll_mean including its same-value rule (runs of
-// equal values, tracked with block max-scans), so constant-return windows
-// (a halted symbol: returns exactly 0) give pandas' exact 0 covariance / NaN
-// correlation. The benchmark's return at candle t is the same for every row
-// (index-aligned mode): it is recomputed per block (one log per candle).
+// One wave per symbol walks the row in tiles of 256 candles (4 per lane), with
+// no cross-wave step: waves of different symbols never wait for each other,
+// so one's latency hides behind another's arithmetic (the 256-thread block
+// walker this replaces spent most of its time in barriers). Per candle the
+// window sums come from tile-local prefix sums (wave DPP scans) in an LDS ring
+// of 512 candles: a window sum is one difference, O(1) per candle whatever the
+// window. At the end of a tile the lanes holding its last 128 prefixes write
+// them back re-based to the next tile's frame (minus the tile total), so the
+// prefixes never grow past one tile (no cancellation on long rows) and a read
+// needs no frame test. The squares are summed about row-constant references
+// (the row's first return) so the variances do not cancel; the means follow
+// pandas' roll_mean including its same-value rule (runs of equal values,
+// tracked with wave max-scans and a per-tile carry), so constant-return
+// windows (a halted symbol: returns exactly 0) give pandas' exact 0
+// covariance / NaN correlation. The previous candle of lane 0 and the run /
+// total carries come from the previous tile through readlane; the next tile's
+// prices are in flight while the current one computes.
 #include "bq_device.h"
 #include "binquant_amd.h"
 
@@ -31,15 +36,14 @@
 
 namespace bq {
 
-constexpr int BC_NT = 256;
+constexpr int BC_NT = 256;   // beta_btc_stats_kernel block
 constexpr int BC_NW = BC_NT / WAVE;
-constexpr int BC_K = 4;
+constexpr int BC_K = 4;      // candles per lane
 constexpr int BC_TT = BC_NT * BC_K;
 constexpr int BC_H = 128;
 constexpr int BC_R = BC_H + BC_TT;
 constexpr int BC_Q = BC_R / BC_K;
-constexpr int BC_NS = 5;
-static_assert(BC_R % BC_K == 0 && BC_H >= BQ_MAX_WINDOW + 2, "ring shape");   // prefix series: x, y, x*y, (x - rx)^2, (y - ry)^2
+static_assert(BC_R % BC_K == 0 && BC_H >= BQ_MAX_WINDOW + 2, "ring shape");
 // ring position -> slot, lane-interleaved (in the natural layout the lanes'
 // candles are K apart: multi-way bank conflicts on every access)
 __device__ __forceinline__ int bslot(int p) { return (p % BC_K) * BC_Q + p / BC_K; }
@@ -49,13 +53,12 @@ struct BetaArgs {
   const double* btc;     // PAIRS: benchmark returns, same row stride
   double* beta;
   double* corr;
-  const double* ystat;   // MODE 3: [2][T] benchmark window mean, variance (ddof 1)
+  const double* ystat;   // MODE 3: [3][T] benchmark window mean, variance (ddof 1), 1 / variance
   int64_t ld_in, ld_out;
   int T, win;
   double inv_w, inv_w1, bias;   // 1/w, 1/(w-1), w/(w-1)
+  int vin, vbtc, vout;   // 16-byte aligned rows: close / btc loads, beta / corr stores
 };
-
-__device__ __forceinline__ double log_return(double c, double p) { return log(c / p); }
 
 // 1 / v with the hardware reciprocal and two Newton steps (v > 0)
 __device__ __forceinline__ double rcp_nr(double v) {
@@ -66,11 +69,32 @@ __device__ __forceinline__ double rcp_nr(double v) {
 
 // 1 / sqrt(v) for v >= 0 (+inf at 0) with two Newton steps
 __device__ __forceinline__ double rsq_nr(double v) {
-  double r = __builtin_amdgcn_rsq(v);
-  if (!(v > 0.0)) return r;
+  const double r0 = __builtin_amdgcn_rsq(v);
   const double h = 0.5 * v;
+  double r = r0 * fma(-h * r0, r0, 1.5);
   r = r * fma(-h * r, r, 1.5);
-  return r * fma(-h * r, r, 1.5);
+  return v > 0.0 ? r : r0;   // select, not a branch
+}
+
+// log(c / p) as pandas forms it (the IEEE quotient, then its log). A 15-minute
+// ratio is almost always within 1/8 of 1: there log(m) = 2 atanh(s),
+// s = (m - 1) / (m + 1), m - 1 exact, seven odd terms to below half an ulp of
+// the sum (|s| <= 1/15, s^16 / 17 < 2^-66): ~20 double ops against ~76 for
+// the library log, within 2 ulp of it. Larger moves, zero / negative / NaN
+// prices take the library log (a branch, skipped when no lane needs it).
+__device__ __forceinline__ double log_return(double c, double p) {
+  const double m = c / p;
+  const double d = m - 1.0;
+  if (__builtin_expect(!(fabs(d) <= 0.125), 0)) return log(m);
+  const double s = d * rcp_nr(2.0 + d), z = s * s;
+  double r = 1.0 / 15.0;
+  r = fma(r, z, 1.0 / 13.0);
+  r = fma(r, z, 1.0 / 11.0);
+  r = fma(r, z, 1.0 / 9.0);
+  r = fma(r, z, 1.0 / 7.0);
+  r = fma(r, z, 1.0 / 5.0);
+  r = fma(r, z, 1.0 / 3.0);
+  return (2.0 * s) * fma(r, z, 1.0);
 }
 
 // inclusive wave prefix sum of a double (DPP row scans + readlane row carries)
@@ -85,22 +109,62 @@ __device__ __forceinline__ double wave_scan_f64(double x, int lane) {
   return x + c;
 }
 
+// A lane's 4 consecutive candles: two 16-byte accesses where the row allows
+// (each instruction then fills half of every line it touches instead of a
+// quarter; nontemporal loads measured slower here, nontemporal stores faster).
+typedef double bq_v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void ld4(const double* __restrict__ r, int t, int T, bool vec, double (&v)[4]) {
+  if (vec && t + 4 <= T) {
+    const bq_v2d* p = reinterpret_cast<const bq_v2d*>(r + t);
+    const bq_v2d a = p[0], b = p[1];
+    v[0] = a.x;
+    v[1] = a.y;
+    v[2] = b.x;
+    v[3] = b.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = t + k < T ? r[t + k] : qnan();
+  }
+}
+
+__device__ __forceinline__ void st4(double* r, int t, int T, bool vec, const double (&v)[4]) {
+  if (vec && t + 4 <= T) {   // write-once outputs: nontemporal (streamed past L2)
+    __builtin_nontemporal_store(bq_v2d{v[0], v[1]}, reinterpret_cast<bq_v2d*>(r + t));
+    __builtin_nontemporal_store(bq_v2d{v[2], v[3]}, reinterpret_cast<bq_v2d*>(r + t + 2));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (t + k < T) __builtin_nontemporal_store(v[k], r + t + k);
+  }
+}
+
+constexpr int BW_TT = WAVE * BC_K;   // candles per tile
+constexpr int BW_R = 512;            // ring: a tile plus a halo of up to 256 candles
+constexpr int BW_Q = BW_R / BC_K;
+static_assert(BW_R >= BW_TT + BC_H && (BW_R & (BW_R - 1)) == 0 && BC_K == 4, "wave ring shape");
+// candle index (negative: before the row) -> ring slot, lane-interleaved
+__device__ __forceinline__ int wslot(int t) {
+  const unsigned p = (unsigned)t & (BW_R - 1);
+  return (int)((p & (BC_K - 1)) * BW_Q + (p >> 2));
+}
+#ifndef BQ_BW_WAVES
+#define BQ_BW_WAVES 3   // waves per SIMD the MODE 3 register budget is cut for
+#endif
+
 // MODE 0: close / btc prices, returns formed here (first return NaN, first
 // full window at t = w). MODE 2: close prices + the benchmark's returns as one
-// row shared by every symbol (formed once per launch, not once per block).
+// row shared by every symbol (formed once per launch, not once per wave).
 // MODE 1: rows of dropna'd return pairs (bq_join_returns), first full window
 // at t = w - 1.
-// MODE 3: as MODE 2, and the benchmark's window mean / variance at every t
-// are read from A.ystat (beta_btc_stats_kernel, once per launch): the block
-// scans three series (x, x*y, (x - rx)^2) instead of five.
+// MODE 3: as MODE 2, and the benchmark's window mean / variance / inverse
+// variance at every t are read from A.ystat (beta_btc_stats_kernel, once per
+// launch): the wave scans three series (x, x*y, (x - rx)^2) instead of five.
 template <int MODE>
-__global__ __launch_bounds__(BC_NT, MODE == 3 ? 3 : 2) void beta_corr_kernel(const BetaArgs A) {
+__global__ __launch_bounds__(WAVE, MODE == 3 ? BQ_BW_WAVES : 2) void beta_wave_kernel(const BetaArgs A) {
   constexpr bool PAIRS = MODE == 1, BRET = MODE >= 2, YST = MODE == 3;
-  __shared__ double sP[BC_NS][BC_R];
-  __shared__ double sWt[BC_NS][BC_NW];
-  __shared__ int sWl[3][BC_NW];
-  __shared__ int sCar[3];
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  constexpr int NS = YST ? 3 : 5;   // x, x*y, (x - rx)^2 [, y, (y - ry)^2]
+  __shared__ double sP[NS][BW_R];
+  const int lane = threadIdx.x;
   const int64_t sym = blockIdx.x;
   const double* __restrict__ rc = A.close + sym * A.ld_in;
   const double* __restrict__ rb = PAIRS ? A.btc + sym * A.ld_in : A.btc;
@@ -115,70 +179,103 @@ __global__ __launch_bounds__(BC_NT, MODE == 3 ? 3 : 2) void beta_corr_kernel(con
     if (rx != rx) rx = 0.0;
     if (ry != ry) ry = 0.0;
   }
-  if (tid < BC_H) {
+  // empty prefixes before the row (the halo of the first tile)
 #pragma unroll
-    for (int q = 0; q < BC_NS; ++q) sP[q][bslot(tid)] = 0.0;
-  }
-  if (tid < 3) sCar[tid] = -1;
-  for (int t0 = 0; t0 < T; t0 += BC_TT) {
-    const int tb = t0 + BC_K * tid, pb = BC_H + BC_K * tid;
-    double x[BC_K], y[BC_K];
-    {
-      double pc = tb >= 1 && tb <= T ? rc[tb - 1] : qnan();
-      double pbt = tb >= 1 && tb <= T ? rb[tb - 1] : qnan();
+  for (int h = 0; h < BC_H; h += WAVE)
+#pragma unroll
+    for (int s2 = 0; s2 < NS; ++s2) sP[s2][wslot(h + lane - BC_H)] = 0.0;
+  // carries of the previous tile (wave-uniform)
+  double cprev = qnan(), bprev = qnan(), xprev = qnan(), yprev = qnan(), xyprev = qnan();
+  int carx = -1, cary = -1, carxy = -1;
+  const bool vin = A.vin, vbtc = A.vbtc, vout = A.vout;
+  double cn[BC_K], bn[BC_K];
+  ld4(rc, BC_K * lane, T, vin, cn);
+  ld4(rb, BC_K * lane, T, vbtc, bn);
+  const double wd = (double)win;
+  for (int t0 = 0; t0 < T; t0 += BW_TT) {
+    const int tb = t0 + BC_K * lane;
+    // MODE 3: the benchmark's window stats of this tile (L2 hits: every symbol
+    // reads the same rows), issued before the next tile's prefetch so that
+    // waiting for them does not wait for it (loads retire in order)
+    double ym[BC_K], yv[BC_K], yi[BC_K];
+    if (YST) {
 #pragma unroll
       for (int k = 0; k < BC_K; ++k) {
         const bool ok = tb + k < T;
-        const double c = ok ? rc[tb + k] : qnan(), b = ok ? rb[tb + k] : qnan();
-        if (PAIRS) {
-          x[k] = c;
-          y[k] = b;
-        } else {
-          x[k] = log_return(c, pc);   // NaN at candle 0 (dropna)
-          y[k] = BRET ? b : log_return(b, pbt);
-        }
-        pc = c;
-        pbt = b;
+        ym[k] = ok ? A.ystat[tb + k] : 0.0;
+        yv[k] = ok ? A.ystat[T + tb + k] : 0.0;
+        yi[k] = ok ? A.ystat[2 * T + tb + k] : 0.0;
       }
     }
-    // per-candle terms (a candle without both returns adds nothing) and the
-    // lane's inclusive prefix of each
-    double q[BC_NS][BC_K];
-    int lx = -1, ly = -1, lxy = -1;   // last index where x / y / x*y changed (lane)
+    double x[BC_K], y[BC_K];
+    {
+      double c[BC_K], b[BC_K];
+#pragma unroll
+      for (int k = 0; k < BC_K; ++k) {
+        c[k] = cn[k];
+        b[k] = bn[k];
+      }
+      if (t0 + BW_TT < T) {   // next tile's inputs in flight during this one
+        ld4(rc, tb + BW_TT, T, vin, cn);
+        ld4(rb, tb + BW_TT, T, vbtc, bn);
+      }
+      double pc = dpp_f64<DPP_WAVE_SHR1>(c[BC_K - 1]), pbt = dpp_f64<DPP_WAVE_SHR1>(b[BC_K - 1]);
+      if (lane == 0) {
+        pc = cprev;
+        pbt = bprev;
+      }
+      cprev = readlane_f64(c[BC_K - 1], WAVE - 1);
+      if (!BRET) bprev = readlane_f64(b[BC_K - 1], WAVE - 1);
+#pragma unroll
+      for (int k = 0; k < BC_K; ++k) {
+        if (PAIRS) {
+          x[k] = c[k];
+          y[k] = b[k];
+        } else {
+          x[k] = log_return(c[k], pc);   // NaN at candle 0 (dropna)
+          y[k] = BRET ? b[k] : log_return(b[k], pbt);
+        }
+        pc = c[k];
+        pbt = b[k];
+      }
+    }
+    // per-candle terms (a candle without both returns adds nothing), their
+    // tile-local inclusive prefixes, and the last index where x / y / x*y
+    // changed (the same-value rule)
+    double q[NS][BC_K];
     int lcx[BC_K], lcy[BC_K], lcxy[BC_K];
     {
-      double acc[BC_NS] = {0, 0, 0, 0, 0};
-      double px = qnan(), py = qnan(), pxy = qnan();
-      if (tb >= 1 && tb <= T) {   // the previous candle's values for the run test
-        // (a neighbour lane's last candle: recomputed, cheaper than a barrier)
-        if (PAIRS) {
-          px = rc[tb - 1];
-          py = rb[tb - 1];
-        } else if (tb >= 2) {
-          px = log_return(rc[tb - 1], rc[tb - 2]);
-          py = BRET ? rb[tb - 1] : log_return(rb[tb - 1], rb[tb - 2]);
-        }
-        pxy = px * py;
+      double acc[NS];
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) acc[s2] = 0.0;
+      double px = dpp_f64<DPP_WAVE_SHR1>(x[BC_K - 1]), py = dpp_f64<DPP_WAVE_SHR1>(y[BC_K - 1]);
+      double pxy = dpp_f64<DPP_WAVE_SHR1>(x[BC_K - 1] * y[BC_K - 1]);
+      if (lane == 0) {
+        px = xprev;
+        py = yprev;
+        pxy = xyprev;
       }
+      int lx = -1, ly = -1, lxy = -1;
 #pragma unroll
       for (int k = 0; k < BC_K; ++k) {
         const int t = tb + k;
         const bool ok = x[k] == x[k] && y[k] == y[k];
         const double xy = x[k] * y[k];
         if (ok) {
-          const double u = x[k] - rx, v = y[k] - ry;
+          const double u = x[k] - rx;
           acc[0] += x[k];
-          acc[2] += xy;
-          acc[3] = fma(u, u, acc[3]);
+          acc[1] += xy;
+          acc[2] = fma(u, u, acc[2]);
           if (!YST) {
-            acc[1] += y[k];
+            const double v = y[k] - ry;
+            acc[3] += y[k];
             acc[4] = fma(v, v, acc[4]);
           }
         }
 #pragma unroll
-        for (int s2 = 0; s2 < BC_NS; ++s2) q[s2][k] = acc[s2];
+        for (int s2 = 0; s2 < NS; ++s2) q[s2][k] = acc[s2];
         if (t == 0 || !(x[k] == px)) lx = t;
-        if (t == 0 || !(y[k] == py)) ly = t;
+        if (!YST && (t == 0 || !(y[k] == py))) ly = t;   // MODE 3: the benchmark's own runs are in ystat
         if (t == 0 || !(xy == pxy)) lxy = t;
         lcx[k] = lx;
         lcy[k] = ly;
@@ -187,122 +284,97 @@ __global__ __launch_bounds__(BC_NT, MODE == 3 ? 3 : 2) void beta_corr_kernel(con
         py = y[k];
         pxy = xy;
       }
-      // wave scan of the lane totals, wave totals to LDS
+      xprev = readlane_f64(x[BC_K - 1], WAVE - 1);
+      if (!YST) yprev = readlane_f64(y[BC_K - 1], WAVE - 1);
+      xyprev = readlane_f64(x[BC_K - 1] * y[BC_K - 1], WAVE - 1);
 #pragma unroll
-      for (int s2 = 0; s2 < BC_NS; ++s2) {
-        if (YST && (s2 == 1 || s2 == 4)) continue;
-        const double inc = wave_scan_f64(acc[s2], lane);
-        if (lane == WAVE - 1) sWt[s2][w] = inc;
-        const double ex = inc - acc[s2];
+      for (int s2 = 0; s2 < NS; ++s2) {
+        const double ex = wave_scan_f64(acc[s2], lane) - acc[s2];
 #pragma unroll
         for (int k = 0; k < BC_K; ++k) q[s2][k] += ex;
       }
-      const int ix = wave_scan_max_dpp(lx + 1, lane) - 1, iy = wave_scan_max_dpp(ly + 1, lane) - 1,
+      const int ix = wave_scan_max_dpp(lx + 1, lane) - 1, iy = YST ? -1 : wave_scan_max_dpp(ly + 1, lane) - 1,
                 ixy = wave_scan_max_dpp(lxy + 1, lane) - 1;
-      if (lane == WAVE - 1) {
-        sWl[0][w] = ix;
-        sWl[1][w] = iy;
-        sWl[2][w] = ixy;
-      }
-      const int ex_x = dpp_i32<DPP_WAVE_SHR1>(ix + 1) - 1, ex_y = dpp_i32<DPP_WAVE_SHR1>(iy + 1) - 1,
-                ex_xy = dpp_i32<DPP_WAVE_SHR1>(ixy + 1) - 1;
-      __syncthreads();
-      int cx = max(sCar[0], ex_x), cy = max(sCar[1], ex_y), cxy = max(sCar[2], ex_xy);
-      double base[BC_NS] = {0, 0, 0, 0, 0};
-      for (int u = 0; u < w; ++u) {
-        cx = max(cx, sWl[0][u]);
-        cy = max(cy, sWl[1][u]);
-        cxy = max(cxy, sWl[2][u]);
-#pragma unroll
-        for (int s2 = 0; s2 < BC_NS; ++s2)
-          if (!(YST && (s2 == 1 || s2 == 4))) base[s2] += sWt[s2][u];
-      }
+      const int cx = max(carx, dpp_i32<DPP_WAVE_SHR1>(ix + 1) - 1),
+                cy = YST ? -1 : max(cary, dpp_i32<DPP_WAVE_SHR1>(iy + 1) - 1),
+                cxy = max(carxy, dpp_i32<DPP_WAVE_SHR1>(ixy + 1) - 1);
 #pragma unroll
       for (int k = 0; k < BC_K; ++k) {
         lcx[k] = max(lcx[k], cx);
         lcy[k] = max(lcy[k], cy);
         lcxy[k] = max(lcxy[k], cxy);
 #pragma unroll
-        for (int s2 = 0; s2 < BC_NS; ++s2) {
-          if (YST && (s2 == 1 || s2 == 4)) continue;
-          q[s2][k] += base[s2];
-          sP[s2][bslot(pb + k)] = q[s2][k];
-        }
+        for (int s2 = 0; s2 < NS; ++s2) sP[s2][wslot(tb + k)] = q[s2][k];
       }
     }
-    __syncthreads();
+    __syncthreads();   // one wave: orders the ring writes before the reads
     double beta[BC_K], corr[BC_K];
-    const double wd = (double)win;
 #pragma unroll
     for (int k = 0; k < BC_K; ++k) {
-      const int t = tb + k, o = bslot(pb + k - win);
-      if (t < win - (PAIRS ? 1 : 0) || t >= T) {
-        beta[k] = corr[k] = qnan();
-        continue;
-      }
-      // the lane's own prefixes are re-read from the ring (not held across the
-      // barrier: fewer live registers, more waves per SIMD)
-      const int me = bslot(pb + k);
-      const double Sx = sP[0][me] - sP[0][o], Sxy = sP[2][me] - sP[2][o];
-      const double Suu = sP[3][me] - sP[3][o];
+      const int t = tb + k;
+      // (computed for every lane, the incomplete windows masked at the end:
+      // a ring read before the row start is a zeroed slot)
+      // window sums: own prefix minus the prefix at t - win (this tile's frame)
+      const int o = wslot(t - win);
+      double S[NS];
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) S[s2] = q[s2][k] - sP[s2][o];
       // pandas: mean_xy, mean_x, mean_y = roll_mean (same-value rule)
       const bool cx = lcx[k] <= t - win + 1, cxy = lcxy[k] <= t - win + 1;
-      const double mx = cx ? x[k] : div_exact(Sx, wd, A.inv_w);
-      const double mxy = cxy ? x[k] * y[k] : div_exact(Sxy, wd, A.inv_w);
+      const double mx = cx ? x[k] : S[0] * A.inv_w;
+      const double mxy = cxy ? x[k] * y[k] : S[1] * A.inv_w;
       // variances about the row references: sum (x - rx)^2 - (sum (x - rx))^2 / w
-      const double Su = Sx - wd * rx;
-      double vx = cx ? 0.0 : (Suu - Su * Su * A.inv_w) * A.inv_w1;
-      double my, vy;
+      const double Su = S[0] - wd * rx;
+      double vx = cx ? 0.0 : (S[2] - Su * Su * A.inv_w) * A.inv_w1;
+      double my, vy, ivy;
       if (YST) {
-        my = A.ystat[t];
-        vy = A.ystat[T + t];
+        my = ym[k];
+        vy = yv[k];
+        ivy = yi[k];
       } else {
-        const double Sy = sP[1][me] - sP[1][o], Svv = sP[4][me] - sP[4][o];
         const bool cy = lcy[k] <= t - win + 1;
-        my = cy ? y[k] : div_exact(Sy, wd, A.inv_w);
-        const double Sv = Sy - wd * ry;
-        vy = cy ? 0.0 : (Svv - Sv * Sv * A.inv_w) * A.inv_w1;
+        my = cy ? y[k] : S[3] * A.inv_w;
+        const double Sv = S[3] - wd * ry;
+        vy = cy ? 0.0 : (S[4] - Sv * Sv * A.inv_w) * A.inv_w1;
+        vy = vy < 0.0 ? 0.0 : vy;
+        ivy = vy == 0.0 ? qnan() : rcp_nr(vy);
       }
       const double cov = (mxy - mx * my) * A.bias;
       vx = vx < 0.0 ? 0.0 : vx;
-      vy = vy < 0.0 ? 0.0 : vy;
       // reciprocal / reciprocal square root with Newton refinement (a few ulps,
       // well inside the 1e-9 bar) instead of IEEE divides: cov / vy, and
       // cov / sqrt(vx vy) (+-inf / NaN when vx vy == 0, as pandas' division)
-      beta[k] = vy == 0.0 ? qnan() : cov * rcp_nr(vy);
-      corr[k] = cov * rsq_nr(vx * vy);
+      const bool full = t >= win - (PAIRS ? 1 : 0);
+      beta[k] = full ? cov * ivy : qnan();
+      corr[k] = full ? cov * rsq_nr(vx * vy) : qnan();
     }
     const int64_t orow = sym * A.ld_out;
+    if (A.beta) st4(A.beta + orow, tb, T, vout, beta);
+    if (A.corr) st4(A.corr + orow, tb, T, vout, corr);
+    carx = __builtin_amdgcn_readlane(lcx[BC_K - 1], WAVE - 1);
+    cary = __builtin_amdgcn_readlane(lcy[BC_K - 1], WAVE - 1);
+    carxy = __builtin_amdgcn_readlane(lcxy[BC_K - 1], WAVE - 1);
+    if (t0 + BW_TT >= T) break;
+    // the halo of the next tile: this tile's last 128 prefixes in the next
+    // tile's frame (held in registers by lanes 32..63)
+    double tot[NS];
 #pragma unroll
-    for (int k = 0; k < BC_K; ++k) {
-      if (tb + k < T) {
-        if (A.beta) A.beta[orow + tb + k] = beta[k];
-        if (A.corr) A.corr[orow + tb + k] = corr[k];
-      }
-    }
-    if (t0 + BC_TT >= T) break;
-    // halo for the next tile: the last 128 prefixes, re-based to end at 0
-    double last[BC_NS];
-#pragma unroll
-    for (int s2 = 0; s2 < BC_NS; ++s2) last[s2] = sP[s2][bslot(BC_R - 1)];
-    __syncthreads();   // every read of this tile's ring is done
-    if (pb >= BC_TT) {
+    for (int s2 = 0; s2 < NS; ++s2) tot[s2] = readlane_f64(q[s2][BC_K - 1], WAVE - 1);
+    __syncthreads();   // this tile's ring reads are done
+    if (BC_K * lane >= BW_TT - BC_H) {
 #pragma unroll
       for (int k = 0; k < BC_K; ++k)
 #pragma unroll
-        for (int s2 = 0; s2 < BC_NS; ++s2) sP[s2][bslot(pb + k - BC_TT)] = q[s2][k] - last[s2];
-    }
-    if (tid == BC_NT - 1) {
-      sCar[0] = lcx[BC_K - 1];
-      sCar[1] = lcy[BC_K - 1];
-      sCar[2] = lcxy[BC_K - 1];
+        for (int s2 = 0; s2 < NS; ++s2) sP[s2][wslot(tb + k)] = q[s2][k] - tot[s2];
     }
   }
 }
 
 // The benchmark's rolling(w) mean and variance (ddof 1) of its log returns
 // at every t (NaN while t < w; pandas' same-value rule: a constant window has
-// the value itself as mean and 0 variance): ystat[0][t], ystat[1][t]. One
+// the value itself as mean and 0 variance): ystat[0][t], ystat[1][t], and
+// 1 / variance (NaN where the variance is 0: beta's var.replace(0, nan))
+// in ystat[2][t]. One
 // 256-thread workgroup walks the row with the prefix scheme of the main
 // kernel. y = returns row (y[0] NaN).
 __global__ __launch_bounds__(BC_NT) void beta_btc_stats_kernel(const double* __restrict__ y, int T, int win,
@@ -383,6 +455,7 @@ __global__ __launch_bounds__(BC_NT) void beta_btc_stats_kernel(const double* __r
       }
       ystat[t] = m;
       ystat[T + t] = var;
+      ystat[2 * T + t] = var == 0.0 ? qnan() : 1.0 / var;
     }
     if (t0 + BC_TT >= T) break;
     double last[2] = {sP[0][bslot(BC_R - 1)], sP[1][bslot(BC_R - 1)]};
@@ -422,13 +495,17 @@ int launch_beta(int mode, const double* close, const double* btc_close, int64_t 
   A.inv_w1 = 1.0 / (double)(window - 1);
   A.bias = (double)window / (double)(window - 1);
   A.ystat = ystat;
+  const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  A.vin = a16(close) && (ld_in & 1) == 0;
+  A.vbtc = a16(btc_close) && (mode != 1 || (ld_in & 1) == 0);
+  A.vout = (!beta || a16(beta)) && (!corr || a16(corr)) && (ld_out & 1) == 0;
   if (mode == 3) {
     hipLaunchKernelGGL(beta_btc_stats_kernel, dim3(1), dim3(BC_NT), 0, (hipStream_t)stream, btc_close, A.T, window,
                        A.inv_w, A.inv_w1, ystat);
-    hipLaunchKernelGGL(beta_corr_kernel<3>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
-  } else if (mode == 1) hipLaunchKernelGGL(beta_corr_kernel<1>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
-  else if (mode == 2) hipLaunchKernelGGL(beta_corr_kernel<2>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
-  else hipLaunchKernelGGL(beta_corr_kernel<0>, dim3((unsigned)S), dim3(BC_NT), 0, (hipStream_t)stream, A);
+    hipLaunchKernelGGL(beta_wave_kernel<3>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
+  } else if (mode == 1) hipLaunchKernelGGL(beta_wave_kernel<1>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
+  else if (mode == 2) hipLaunchKernelGGL(beta_wave_kernel<2>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
+  else hipLaunchKernelGGL(beta_wave_kernel<0>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 }  // namespace

@@ -405,7 +405,7 @@ def beta_corr(
     bret = torch.full((T,), float("nan"), dtype=torch.float64, device=close.device)
     if T > 1:
         torch.log(btc[0, 1:] / btc[0, :-1], out=bret[1:])
-    scratch = torch.empty(2 * T, dtype=torch.float64, device=close.device)   # benchmark window stats
+    scratch = torch.empty(3 * T, dtype=torch.float64, device=close.device)   # benchmark window stats
     st = _lib.load().bq_beta_corr_bret(
         ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(bret.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
         S, T, _row_stride(close),

@@ -350,9 +350,9 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
 /* bq_beta_corr with the benchmark given as its log returns (btc_returns[T],
  * btc_returns[t] = log(btc[t] / btc[t-1]), NaN at t = 0): the returns are
  * formed once per call instead of once per symbol row (engine.beta_corr).
- * scratch: NULL, or 2*T doubles of device memory in which the benchmark's
- * window mean / variance are computed once (a one-workgroup pre-pass) instead
- * of in every symbol's workgroup. */
+ * scratch: NULL, or 3*T doubles of device memory in which the benchmark's
+ * window mean / variance / inverse variance are computed once (a
+ * one-workgroup pre-pass) instead of in every symbol's wave. */
 int bq_beta_corr_bret(const double* close, const double* btc_returns, double* scratch, int64_t S, int64_t T,
                       int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
 int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in, int32_t window,

@@ -76,3 +76,32 @@ def test_dropin_scalar(cuda):
         assert corr == pytest.approx(z[f"{case}__corr_last"][-1], rel=1e-9, abs=1e-12)
         assert btc_price_change(pd.DataFrame({"close": b})) == pytest.approx(
             z[f"{case}__btc_change_96"][-1], nan_ok=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [5, 50, 126])
+@pytest.mark.parametrize("odd_stride", [False, True])
+def test_kernel_jumps_partial_tiles_and_strides(cuda, window, odd_stride):
+    """Moves beyond the kernel's short-ratio log path (|c/p - 1| > 1/8: the
+    library log), ragged last tiles, the largest window, and rows whose
+    stride rules out the 16-byte accesses (odd leading dimension). (Window 2
+    is left out: on the self pair its covariance cancels to ~1e-7 relative in
+    pandas itself, below any fixed tolerance.)"""
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(window + 7 * odd_stride)
+    S, T = 6, 1337
+    r = rng.normal(0.0, 0.01, size=(S, T))
+    jumps = rng.random((S, T)) < 0.02
+    r[jumps] = rng.choice([-0.4, -0.15, 0.14, 0.5], size=int(jumps.sum()))
+    close = 50.0 * np.exp(np.cumsum(r, axis=1))
+    close[2, 400:480] = close[2, 399]   # a halted stretch: zero returns
+    btc = close[0].copy()
+    ld = T + 1 if odd_stride else T
+    buf = torch.zeros((S, ld), dtype=torch.float64, device="cuda")
+    buf[:, :T] = torch.from_numpy(close).cuda()
+    out = engine.beta_corr(buf[:, :T], torch.from_numpy(btc).cuda(), window=window)
+    for s in range(S):
+        wb, wc = ref.beta_corr_series(close[s], btc, window)
+        assert_close(out["beta"][s].cpu().numpy(), wb, f"beta[{s}]", rtol=1e-8, scale=1.0)
+        assert_close(out["corr"][s].cpu().numpy(), wc, f"corr[{s}]", rtol=1e-8, scale=1.0)

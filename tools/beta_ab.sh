@@ -1,6 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for lib in binquant_amd/lib/libbinquant_amd.so; do
+for lib in ${LIBS:-binquant_amd/lib/libbinquant_amd.so}; do
 BQ_LIB_PATH=$PWD/$lib timeout -k 10 300 python -c "
 import sys, json; sys.path.insert(0,'.'); import torch
 from binquant_amd import engine
