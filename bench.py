@@ -318,7 +318,6 @@ def bench_rows(args, dev):
     qv = v * c
     btc = c[0].clone()
     ts = (1_700_000_000_000 + 900_000 * torch.arange(T, device=dev, dtype=torch.int64)).expand(S, T).contiguous()
-    atr = engine.enrich(o, h, l, c, v, columns=("ATR",))["ATR"]
     agg = {"open": "first", "high": "max", "low": "min", "close": "last", "volume": "sum"}
     # name -> (device call, algorithmic bytes per candle, row reference)
     rows = {
@@ -334,7 +333,7 @@ def bench_rows(args, dev):
         "a20_wilder_rsi": (lambda: signals.wilder_rsi(c), 16, "strategies/mean_reversion_fade.py:88-109"),
         "a20_adx": (lambda: signals.adx(h, l, c), 32, "strategies/range_bb_rsi_mean_reversion.py:101-122"),
         "a20_zscore": (lambda: signals.zscore(c), 16, "strategies/range_bb_rsi_mean_reversion.py:124-138"),
-        "supertrend": (lambda: engine.supertrend(h, l, c, atr=atr), 4 * 8 + 1 + 16, "strategies/coinrule/coinrule.py:143"),
+        "supertrend": (lambda: engine.supertrend(h, l, c), 3 * 8 + 1 + 16, "strategies/coinrule/coinrule.py:143"),
         "a9_resample_1h": (lambda: engine.resample(ts, {"open": o, "high": h, "low": l, "close": c, "volume": v},
                                                    agg, 3_600_000), 48 + 48 / 4, "producers/context_evaluator.py:403-407"),
         "f4_btc_join_returns": (lambda: engine.join_returns(ts, c, ts[0], btc), 16 + 16,

@@ -11,72 +11,168 @@
 //       otherwise keep the trend, and hold the band on the trend's side
 //       (up: lower[t] = max(lower[t], lower[t-1]); down: upper[t] =
 //       min(upper[t], upper[t-1])).
-//   ATR (TR.rolling(period).mean(), the `atr` restatement) comes in as an
-//   input column so the kernel only runs the comparisons; NaN bands in the
+//   ATR = TR.rolling(period).mean(): bq_supertrend takes it as an input column;
+//   bq_supertrend_hlc forms it in the same walk, replaying pandas' roll_mean
+//   (pandas/_libs/window/aggregations.pyx add_mean / remove_mean / calc_mean,
+//   pandas 2.3.3: Kahan sums with separate add / remove compensations, the
+//   same-value and sign rules, min_periods = period) on the lane's own TR
+//   sequence, so its ATR and bands are pandas' bit for bit. NaN bands in the
 //   warm-up compare false, so the trend holds its initial `up` state.
 //
 // Mapping: one wave = 64 symbols; chunks of ST_CT candles are read coalesced
 // and transposed through LDS (bq_device.h stage_*); the next chunk's loads are
-// in flight while the current chunk's recurrence runs.
+// in flight while the current chunk's recurrence runs, and the chunk's steps
+// are unrolled so the state-independent work (LDS reads, TR, hl2) of later
+// steps overlaps the dependent chain of earlier ones. The TR values still in
+// the window sit in an LDS ring (period + 16 slots, lane-contiguous).
 #include "bq_device.h"
 #include "binquant_amd.h"
 
 namespace bq {
 
-constexpr int ST_CT = 16;   // candles per staged chunk
+#ifndef BQ_ST_CT
+#define BQ_ST_CT 16
+#endif
+constexpr int ST_CT = BQ_ST_CT;   // candles per staged chunk (the global loads in flight per wave)
+#ifndef BQ_ST_SUB
+#define BQ_ST_SUB 8
+#endif
+constexpr int ST_SUB = BQ_ST_SUB;   // candles per register sub-chunk of the sequential part
 
 struct StArgs {
   const double *h, *l, *c, *atr;
   uint8_t* up;
   double *upper, *lower;
   int64_t S, ld_in, ld_out;
-  int T;
+  int T, period, ring;   // ring: TR slots per lane (period + ST_SUB)
   double mult;
 };
 
+// pandas roll_mean state for a fixed window with min_periods = window. The
+// NaN skips and the result rules are selects, not branches: the walk runs
+// one wave per SIMD, where every exec-mask branch is paid in full each step.
+struct AtrMean {
+  double sum, comp_add, comp_rem, prev;
+  int nobs, neg, same;
+  __device__ __forceinline__ void add(double v) {
+    const bool ok = v == v;
+    const double y = v - comp_add;
+    const double t = sum + y;
+    const double c = t - sum - y;
+    sum = ok ? t : sum;
+    comp_add = ok ? c : comp_add;
+    nobs += ok;
+    neg += ok & (bool)signbit(v);
+    same = ok ? ((v == prev) ? same + 1 : 1) : same;
+    prev = ok ? v : prev;
+  }
+  __device__ __forceinline__ void remove(double v) {
+    const bool ok = v == v;
+    const double y = -v - comp_rem;
+    const double t = sum + y;
+    const double c = t - sum - y;
+    sum = ok ? t : sum;
+    comp_rem = ok ? c : comp_rem;
+    nobs -= ok;
+    neg -= ok & (bool)signbit(v);
+  }
+  __device__ __forceinline__ double value(int minp) const {
+    const double r = sum / (double)nobs;
+    double o = same >= nobs ? prev : r;
+    o = ((same < nobs) & (((neg == 0) & (r < 0.0)) | ((neg == nobs) & (r > 0.0)))) ? 0.0 : o;
+    return ((nobs < minp) | (nobs <= 0)) ? qnan() : o;
+  }
+};
+
+// FATR: the ATR is formed here from high / low / close (bq_supertrend_hlc);
+// otherwise it is the fourth input column. Per chunk the lane first pulls its
+// symbol's candles out of the staging buffer into registers 16 at a time,
+// forms their 16 TRs, appends them to the ring and reads back the 16 leaving
+// the window (ring of period + 16 slots, so the appends never overwrite one
+// still to leave): the sequential part then runs on registers only, and the Kahan
+// chain of step j + 1 overlaps the division and band logic of step j.
+template <bool FATR>
 __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
+  extern __shared__ double sTR[];               // FATR: TR ring [ring][WAVE]
   __shared__ double sX[4][ST_CT * STG_PITCH];   // h, l, c, atr; then upper, lower, trend
+  constexpr int NIN = FATR ? 3 : 4;
   const int lane = threadIdx.x;
   const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
   const int T = A.T;
-  double rh[ST_CT], rl[ST_CT], rc[ST_CT], ra[ST_CT];
-  stage_load<ST_CT>(A.h, A.ld_in, sym0, A.S, 0, T, lane, rh);
-  stage_load<ST_CT>(A.l, A.ld_in, sym0, A.S, 0, T, lane, rl);
-  stage_load<ST_CT>(A.c, A.ld_in, sym0, A.S, 0, T, lane, rc);
-  stage_load<ST_CT>(A.atr, A.ld_in, sym0, A.S, 0, T, lane, ra);
+  const int P = A.period, R = A.ring;
+  const double* const in[4] = {A.h, A.l, A.c, A.atr};
+  double r[4][ST_CT];
+#pragma unroll
+  for (int f = 0; f < NIN; ++f) stage_load<ST_CT>(in[f], A.ld_in, sym0, A.S, 0, T, lane, r[f]);
   bool up = true;
-  double up_p = qnan(), lo_p = qnan();
+  double up_p = qnan(), lo_p = qnan(), pc = qnan();   // NaN bands before candle 0
+  AtrMean m{0.0, 0.0, 0.0, 0.0, 0, 0, 0};
+  int wslot = 0, rslot = FATR ? R - P : 0;   // ring slots of candle t0 and of candle t0 - P
   for (int t0 = 0; t0 < T; t0 += ST_CT) {
-    stage_put<ST_CT>(sX[0], lane, rh);
-    stage_put<ST_CT>(sX[1], lane, rl);
-    stage_put<ST_CT>(sX[2], lane, rc);
-    stage_put<ST_CT>(sX[3], lane, ra);
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) stage_put<ST_CT>(sX[f], lane, r[f]);
     __syncthreads();
     // prefetch the next chunk (unconditional: past T the clamped loads give
     // NaN that is never used; no branch keeps the loop's waits counted)
-    stage_load<ST_CT>(A.h, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rh);
-    stage_load<ST_CT>(A.l, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rl);
-    stage_load<ST_CT>(A.c, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, rc);
-    stage_load<ST_CT>(A.atr, A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, ra);
-    const int n = min(ST_CT, T - t0);
-    for (int j = 0; j < n; ++j) {
-      const int i = j * STG_PITCH + lane;
-      const double hl2 = (sX[0][i] + sX[1][i]) / 2.0;
-      const double c = sX[2][i], m_atr = A.mult * sX[3][i];
-      double bu = hl2 + m_atr, bl = hl2 - m_atr;
-      if (t0 + j > 0) {
-        if (c > up_p) up = true;
-        else if (c < lo_p) up = false;
-        else {
-          if (up && bl < lo_p) bl = lo_p;
-          if (!up && bu > up_p) bu = up_p;
+#pragma unroll
+    for (int f = 0; f < NIN; ++f) stage_load<ST_CT>(in[f], A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, r[f]);
+#pragma unroll
+    for (int j0 = 0; j0 < ST_CT; j0 += ST_SUB) {
+      const int u0 = t0 + j0;
+      double h[ST_SUB], l[ST_SUB], c[ST_SUB], atr[ST_SUB];
+#pragma unroll
+      for (int j = 0; j < ST_SUB; ++j) {
+        const int i = (j0 + j) * STG_PITCH + lane;
+        h[j] = sX[0][i];
+        l[j] = sX[1][i];
+        c[j] = sX[2][i];
+        if (!FATR) atr[j] = sX[3][i];
+      }
+      if (FATR) {
+        double tr[ST_SUB], old[ST_SUB];
+#pragma unroll
+        for (int j = 0; j < ST_SUB; ++j) {
+          tr[j] = true_range(h[j], l[j], j == 0 ? pc : c[j - 1]);
+          const int ws = wslot + j >= R ? wslot + j - R : wslot + j;
+          sTR[ws * WAVE + lane] = tr[j];
+        }
+        // (one wave: its LDS reads see its own earlier writes)
+#pragma unroll
+        for (int j = 0; j < ST_SUB; ++j) {
+          const int rs = rslot + j >= R ? rslot + j - R : rslot + j;
+          old[j] = u0 + j >= P ? sTR[rs * WAVE + lane] : qnan();   // NaN: nothing leaves
+        }
+        pc = c[ST_SUB - 1];
+        wslot = wslot + ST_SUB >= R ? wslot + ST_SUB - R : wslot + ST_SUB;
+        rslot = rslot + ST_SUB >= R ? rslot + ST_SUB - R : rslot + ST_SUB;
+#pragma unroll
+        for (int j = 0; j < ST_SUB; ++j) {
+          if (u0 + j < T) {   // pandas: the removal, then the add, then calc_mean
+            m.remove(old[j]);
+            m.add(tr[j]);
+            atr[j] = m.value(P);
+          }
         }
       }
-      up_p = bu;
-      lo_p = bl;
-      sX[0][i] = bu;
-      sX[1][i] = bl;
-      sX[2][i] = up ? 1.0 : 0.0;
+#pragma unroll
+      for (int j = 0; j < ST_SUB; ++j) {
+        if (u0 + j < T) {   // wave-uniform: the last chunk may be partial
+          const double hl2 = (h[j] + l[j]) / 2.0;
+          const double m_atr = A.mult * atr[j];
+          double bu = hl2 + m_atr, bl = hl2 - m_atr;
+          // (t == 0: the NaN previous bands compare false and hold `up`)
+          const bool flip_up = c[j] > up_p, flip_dn = !flip_up & (c[j] < lo_p), hold = !flip_up & !flip_dn;
+          up = flip_up | (!flip_dn & up);
+          bl = (hold & up & (bl < lo_p)) ? lo_p : bl;
+          bu = (hold & !up & (bu > up_p)) ? up_p : bu;
+          up_p = bu;
+          lo_p = bl;
+          const int i = (j0 + j) * STG_PITCH + lane;
+          sX[0][i] = bu;
+          sX[1][i] = bl;
+          sX[2][i] = up ? 1.0 : 0.0;
+        }
+      }
     }
     __syncthreads();
     stage_store<ST_CT>(sX[0], A.upper, A.ld_out, sym0, A.S, t0, T, lane);   // null: dropped
@@ -88,20 +184,22 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
 
 }  // namespace bq
 
-extern "C" int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, int64_t ld_in, double multiplier,
-                             uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream) {
+namespace {
+int launch_supertrend(bool fatr, const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t period,
+                      double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream) {
   using namespace bq;
-  if (!hlca || !up || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff || !(multiplier == multiplier))
+  if (!in || !up || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff || !(multiplier == multiplier))
     return BQ_EINVAL;
   if (ld_out > BQ_MAX_ROLL_LD) return BQ_EINVAL;   // 32-bit buffer offsets over a wave's 64 rows
-  for (int i = 0; i < 4; ++i)
-    if (!hlca[i]) return BQ_EINVAL;
+  if (fatr && (period < 1 || period > BQ_MAX_WINDOW)) return BQ_EINVAL;
+  for (int i = 0; i < (fatr ? 3 : 4); ++i)
+    if (!in[i]) return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;
   StArgs A;
-  A.h = hlca[0];
-  A.l = hlca[1];
-  A.c = hlca[2];
-  A.atr = hlca[3];
+  A.h = in[0];
+  A.l = in[1];
+  A.c = in[2];
+  A.atr = fatr ? nullptr : in[3];
   A.up = up;
   A.upper = upper;
   A.lower = lower;
@@ -110,7 +208,26 @@ extern "C" int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, in
   A.ld_out = ld_out;
   A.T = (int)T;
   A.mult = multiplier;
+  const int ring = fatr ? period + ST_SUB : 0;
+  A.period = fatr ? period : 0;
+  A.ring = ring;
   const unsigned blocks = (unsigned)((S + WAVE - 1) / WAVE);
-  hipLaunchKernelGGL(supertrend_kernel, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, A);
+  if (fatr)
+    hipLaunchKernelGGL(supertrend_kernel<true>, dim3(blocks), dim3(WAVE), (size_t)ring * WAVE * sizeof(double),
+                       (hipStream_t)stream, A);
+  else
+    hipLaunchKernelGGL(supertrend_kernel<false>, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+}  // namespace
+
+extern "C" int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, int64_t ld_in, double multiplier,
+                             uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream) {
+  return launch_supertrend(false, hlca, S, T, ld_in, 0, multiplier, up, upper, lower, ld_out, stream);
+}
+
+extern "C" int bq_supertrend_hlc(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t period,
+                                 double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out,
+                                 void* stream) {
+  return launch_supertrend(true, hlc, S, T, ld_in, period, multiplier, up, upper, lower, ld_out, stream);
 }

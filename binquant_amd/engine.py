@@ -642,26 +642,31 @@ def supertrend(
 ) -> dict[str, torch.Tensor]:
     """pybinbot Indicators.set_supertrend (strategies/coinrule/coinrule.py:143-160)
     on a [S, T] panel: {"supertrend": bool (uptrend), "supertrend_upper",
-    "supertrend_lower": final bands}. ATR = TR.rolling(period).mean() from the
-    enrich kernel unless given."""
+    "supertrend_lower": final bands}. ATR = TR.rolling(period).mean(), formed in
+    the same walk as pandas' roll_mean (bq_supertrend_hlc) unless given."""
     high = _check_panel(high, "high")
     S, T = high.shape
     low = _check_panel(low, "low", (S, T))
     close = _check_panel(close, "close", (S, T))
-    if atr is None:
-        zero = torch.zeros_like(close)
-        atr = enrich(close, high, low, close, zero, params=IndicatorParams(atr_window=int(period)),
-                     columns=("ATR",), stream=stream)["ATR"]
-    atr = _check_panel(atr, "atr", (S, T))
-    ins = [t.contiguous() for t in (high, low, close, atr)]
     up = torch.empty((S, T), dtype=torch.bool, device=close.device)
     upper = torch.empty((S, T), dtype=torch.float64, device=close.device)
     lower = torch.empty_like(upper)
-    st = _lib.load().bq_supertrend(
-        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, float(multiplier), ctypes.c_void_p(up.data_ptr()),
-        ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()), T, _stream_handle(stream),
-    )
-    _lib.check(st, "bq_supertrend")
+    if atr is None:
+        ins = [t.contiguous() for t in (high, low, close)]
+        st = _lib.load().bq_supertrend_hlc(
+            _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, int(period), float(multiplier),
+            ctypes.c_void_p(up.data_ptr()), ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()), T,
+            _stream_handle(stream),
+        )
+        _lib.check(st, "bq_supertrend_hlc")
+    else:
+        atr = _check_panel(atr, "atr", (S, T))
+        ins = [t.contiguous() for t in (high, low, close, atr)]
+        st = _lib.load().bq_supertrend(
+            _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, float(multiplier), ctypes.c_void_p(up.data_ptr()),
+            ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()), T, _stream_handle(stream),
+        )
+        _lib.check(st, "bq_supertrend")
     return {"supertrend": up, "supertrend_upper": upper, "supertrend_lower": lower}
 
 

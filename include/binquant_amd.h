@@ -304,6 +304,14 @@ int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32
  */
 int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, int64_t ld_in, double multiplier,
                   uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream);
+/*
+ * bq_supertrend with the ATR formed in the same walk: hlc = {high, low, close}
+ * [S][ld_in] fp64, ATR = TR.rolling(period).mean() replayed as pandas'
+ * roll_mean (1 <= period <= BQ_MAX_WINDOW), so flags and bands are pandas'
+ * bit for bit; one launch, no ATR column in HBM (engine.supertrend).
+ */
+int bq_supertrend_hlc(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t period,
+                      double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream);
 
 /* ---- frame plumbing: resample and timestamp joins (ragged rows) ------------ */
 /* Timestamps are int64 ms, ascending within a row; lens[s] = valid candles of

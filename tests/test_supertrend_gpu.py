@@ -2,10 +2,14 @@
 coinrule.py:143-160) vs the oracle's band recursion (oracle/indicators_ref.py:
 supertrend; pybinbot absent -> parity unpinned against pybinbot itself).
 
-The trend flag is a state machine over comparisons, so it is compared exactly
-up to the first candle whose decision lies within the 1e-9 tolerance band of
-its threshold (a near-tie may legitimately flip and then propagate); the
-bands are compared with the fp64 tolerance of tests/util.py over the same span.
+engine.supertrend forms the ATR in the kernel's own walk as a replay of
+pandas' roll_mean (bq_supertrend_hlc), so flags and bands must equal the
+oracle's bit for bit over every candle. With an ATR column from elsewhere
+(bq_supertrend, here the enrich kernel's windowed ATR) the trend flag is a
+state machine over comparisons, so it is compared exactly up to the first
+candle whose decision lies within the 1e-9 tolerance band of its threshold (a
+near-tie may legitimately flip and then propagate); the bands are compared
+with the fp64 tolerance of tests/util.py over the same span.
 """
 
 import numpy as np
@@ -41,18 +45,38 @@ def oracle_panel(panel, period, mult):
     return out, tie_free
 
 
-def run(panel, period=10, mult=3.0):
+def run(panel, period=10, mult=3.0, atr_input=False):
     t = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in panel.items()}
-    r = engine.supertrend(t["high"], t["low"], t["close"], period=period, multiplier=mult)
+    atr = None
+    if atr_input:
+        zero = torch.zeros_like(t["close"])
+        atr = engine.enrich(t["close"], t["high"], t["low"], t["close"], zero,
+                            params=engine.IndicatorParams(atr_window=period), columns=("ATR",))["ATR"]
+    r = engine.supertrend(t["high"], t["low"], t["close"], period=period, multiplier=mult, atr=atr)
     torch.cuda.synchronize()
     return {k: v.cpu().numpy() for k, v in r.items()}
 
 
-@pytest.mark.parametrize("S,T,period,mult", [(70, 700, 10, 3.0), (3, 1, 10, 3.0), (5, 9, 10, 3.0),
-                                             (64, 257, 7, 2.0), (130, 33, 14, 1.5), (1, 2000, 10, 3.0)])
-def test_supertrend_matches_oracle(cuda, S, T, period, mult):
-    panel = numpy_panel(S, T, seed0=S + T + period, edges=False)
+CASES = [(70, 700, 10, 3.0), (3, 1, 10, 3.0), (5, 9, 10, 3.0), (64, 257, 7, 2.0), (130, 33, 14, 1.5),
+         (1, 2000, 10, 3.0), (65, 300, 1, 3.0), (9, 500, 16, 3.0), (9, 500, 126, 2.5)]
+
+
+@pytest.mark.parametrize("S,T,period,mult", CASES)
+@pytest.mark.parametrize("edges", [False, True])
+def test_supertrend_bit_exact(cuda, S, T, period, mult, edges):
+    """Fused ATR: every flag and band equals the oracle's (NaN candles, halts
+    and gaps included with edges=True)."""
+    panel = numpy_panel(S, T, seed0=S + T + period, edges=edges)
     got = run(panel, period, mult)
+    want, _ = oracle_panel(panel, period, mult)
+    for k in want:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+
+
+@pytest.mark.parametrize("S,T,period,mult", CASES[:6])
+def test_supertrend_atr_input_matches_oracle(cuda, S, T, period, mult):
+    panel = numpy_panel(S, T, seed0=S + T + period, edges=False)
+    got = run(panel, period, mult, atr_input=True)
     want, n_ok = oracle_panel(panel, period, mult)
     price = np.abs(panel["close"]).mean(axis=1, keepdims=True)
     for s in range(S):
