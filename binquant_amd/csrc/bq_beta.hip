@@ -60,13 +60,6 @@ struct BetaArgs {
   int vin, vbtc, vout;   // 16-byte aligned rows: close / btc loads, beta / corr stores
 };
 
-// 1 / v with the hardware reciprocal and two Newton steps (v > 0)
-__device__ __forceinline__ double rcp_nr(double v) {
-  double r = __builtin_amdgcn_rcp(v);
-  r = fma(r, fma(-v, r, 1.0), r);
-  return fma(r, fma(-v, r, 1.0), r);
-}
-
 // 1 / sqrt(v) for v >= 0 (+inf at 0) with two Newton steps
 __device__ __forceinline__ double rsq_nr(double v) {
   const double r0 = __builtin_amdgcn_rsq(v);
@@ -74,27 +67,6 @@ __device__ __forceinline__ double rsq_nr(double v) {
   double r = r0 * fma(-h * r0, r0, 1.5);
   r = r * fma(-h * r, r, 1.5);
   return v > 0.0 ? r : r0;   // select, not a branch
-}
-
-// log(c / p) as pandas forms it (the IEEE quotient, then its log). A 15-minute
-// ratio is almost always within 1/8 of 1: there log(m) = 2 atanh(s),
-// s = (m - 1) / (m + 1), m - 1 exact, seven odd terms to below half an ulp of
-// the sum (|s| <= 1/15, s^16 / 17 < 2^-66): ~20 double ops against ~76 for
-// the library log, within 2 ulp of it. Larger moves, zero / negative / NaN
-// prices take the library log (a branch, skipped when no lane needs it).
-__device__ __forceinline__ double log_return(double c, double p) {
-  const double m = c / p;
-  const double d = m - 1.0;
-  if (__builtin_expect(!(fabs(d) <= 0.125), 0)) return log(m);
-  const double s = d * rcp_nr(2.0 + d), z = s * s;
-  double r = 1.0 / 15.0;
-  r = fma(r, z, 1.0 / 13.0);
-  r = fma(r, z, 1.0 / 11.0);
-  r = fma(r, z, 1.0 / 9.0);
-  r = fma(r, z, 1.0 / 7.0);
-  r = fma(r, z, 1.0 / 5.0);
-  r = fma(r, z, 1.0 / 3.0);
-  return (2.0 * s) * fma(r, z, 1.0);
 }
 
 // inclusive wave prefix sum of a double (DPP row scans + readlane row carries)

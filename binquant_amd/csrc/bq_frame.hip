@@ -155,6 +155,14 @@ __device__ __forceinline__ int match_last(const int64_t* __restrict__ bts, int n
   return (j >= 0 && bts[j] == key) ? j : -1;
 }
 
+// match_last with a guess: index-aligned frames (the common case: the symbol
+// and the benchmark share the 15-minute grid from the same start) hit at the
+// guess with two loads instead of a dependent binary search.
+__device__ __forceinline__ int match_last_near(const int64_t* __restrict__ bts, int nb, int64_t key, int guess) {
+  if (guess >= 0 && guess < nb && bts[guess] == key && (guess + 1 == nb || bts[guess + 1] != key)) return guess;
+  return match_last(bts, nb, key);
+}
+
 __global__ __launch_bounds__(256) void align_kernel(const int64_t* __restrict__ ts, const int64_t* __restrict__ lens,
                                                     int64_t S, int T, int64_t ld_in, const int64_t* __restrict__ bts,
                                                     const double* __restrict__ bval, int nb, double* __restrict__ out,
@@ -189,15 +197,18 @@ __global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __re
   const int64_t* __restrict__ rts = ts + s * ld_in;
   const double* __restrict__ rc = close + s * ld_in;
   const int n = row_len(lens, s, T);
+  // the row's offset into the benchmark's index, from its first candle
+  const int j0 = n > 0 ? match_last(bts, nb, rts[0]) : -1;
+  const int guess_off = j0 >= 0 ? j0 : 0;
   if (tid == 0) sBase = 0;
   __syncthreads();
   for (int t0 = 0; t0 < n; t0 += JR_NT) {
     const int t = t0 + tid;
     double xa = qnan(), yb = qnan();
     if (t < n && t > 0) {
-      xa = log(rc[t] / rc[t - 1]);   // the frame's own previous row
-      const int j = match_last(bts, nb, rts[t]);
-      if (j > 0) yb = log(bclose[j] / bclose[j - 1]);
+      xa = log_return(rc[t], rc[t - 1]);   // the frame's own previous row
+      const int j = match_last_near(bts, nb, rts[t], t + guess_off);
+      if (j > 0) yb = log_return(bclose[j], bclose[j - 1]);
     }
     const bool keep = xa == xa && yb == yb;
     const uint64_t m = __ballot(keep);

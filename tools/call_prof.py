@@ -11,7 +11,9 @@ name = sys.argv[1]
 S, T = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (12500, 2000)
 p = device_panel(S, T, seed=99)
 h, l, c = p["high"], p["low"], p["close"]
+ts = (1_700_000_000_000 + 900_000 * torch.arange(T, device=c.device, dtype=torch.int64)).expand(S, T).contiguous()
 calls = {
+    "join_returns": lambda: engine.join_returns(ts, c, ts[0], c[0].clone()),
     "supertrend": lambda: engine.supertrend(h, l, c, period=10, multiplier=3.0),
     "beta_corr": lambda: engine.beta_corr(c, c[0].clone(), 50),
     "market_features": lambda: engine.market_features(h, l, c, max_bars=400),
