@@ -246,6 +246,12 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   const int T = A.T;
   const bool vin = vec_in != 0, vout = vec_out != 0;
 
+  // the first tile's loads go out before anything else: their HBM latency
+  // overlaps the serial constant set-up below (a workgroup's fixed start-up
+  // cost otherwise adds ~5% to a 10k-candle row)
+  Tile nx;
+  load_tile(A, irow, EN_K * tid, vin, nx);
+
   // ---- per-workgroup constants (pandas: comass = (span-1)/2, alpha = 1/(1+comass))
   if (tid == 0) {
     for (int e = 0; e < NE; ++e) {
@@ -303,8 +309,6 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   }
   __syncthreads();
 
-  Tile nx;
-  load_tile(A, irow, EN_K * tid, vin, nx);
   // EMA carry into candle 0 = (x0, x0, 0, x0, x0): pandas starts every EMA at
   // its first value (output[0] = x0, macd signal[0] = macd[0] = 0), and the
   // generic step from y == x leaves y unchanged, so no first-candle branch.
