@@ -345,7 +345,7 @@ def bench_rows(args, dev):
         gbs = S * T * bpc / (ms * 1e-3) / 1e9
         out[name] = {"ms": ms, "value": S * T / (ms * 1e-3), "unit": "symbol-candles/s", "GBps": gbs,
                      "frac": gbs / HBM_PEAK_GBS, "bytes_per_candle": bpc, "reference": ref}
-    del p, o, h, l, c, v, qv, ts, atr
+    del p, o, h, l, c, v, qv, ts
     torch.cuda.empty_cache()
     if args.no_cpu_baseline:
         return out
