@@ -205,6 +205,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),
     "bq_join_returns": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
     "bq_beta_corr_bret": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
+    "bq_beta_corr_ws": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_beta_corr_pairs": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_store_update": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _P, _PP, _P, _I64, _P]),
     "bq_store_features": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _PP, _P, _P]),

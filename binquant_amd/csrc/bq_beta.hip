@@ -349,14 +349,23 @@ __global__ __launch_bounds__(WAVE, MODE == 3 ? BQ_BW_WAVES : 2) void beta_wave_k
 // in ystat[2][t]. One
 // 256-thread workgroup walks the row with the prefix scheme of the main
 // kernel. y = returns row (y[0] NaN).
-__global__ __launch_bounds__(BC_NT) void beta_btc_stats_kernel(const double* __restrict__ y, int T, int win,
+// bp != NULL: y is formed here from the benchmark's prices
+// (log_return(bp[t], bp[t-1]), NaN at t = 0) and written to ystat[3][t] for
+// the symbol walk, so a call needs no separate returns pass.
+__global__ __launch_bounds__(BC_NT) void beta_btc_stats_kernel(const double* __restrict__ y,
+                                                               const double* __restrict__ bp, int T, int win,
                                                                double inv_w, double inv_w1, double* ystat) {
   __shared__ double sP[2][BC_R];
   __shared__ double sWt[2][BC_NW];
   __shared__ int sWl[BC_NW];
   __shared__ int sCar;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  double ry = T > 1 ? y[1] : 0.0;
+  const auto yv = [&](int t) -> double {
+    if (t < 0 || t >= T) return qnan();
+    if (bp) return t == 0 ? qnan() : log_return(bp[t], bp[t - 1]);
+    return y[t];
+  };
+  double ry = T > 1 ? yv(1) : 0.0;
   if (ry != ry) ry = 0.0;
   if (tid < BC_H) sP[0][bslot(tid)] = sP[1][bslot(tid)] = 0.0;
   if (tid == 0) sCar = -1;
@@ -364,11 +373,12 @@ __global__ __launch_bounds__(BC_NT) void beta_btc_stats_kernel(const double* __r
     const int tb = t0 + BC_K * tid, pb = BC_H + BC_K * tid;
     double v[BC_K], q[2][BC_K], acc[2] = {0.0, 0.0};
     int lc[BC_K], l = -1;
-    double pv = tb >= 1 && tb <= T ? y[tb - 1] : qnan();
+    double pv = tb >= 1 && tb <= T ? yv(tb - 1) : qnan();
 #pragma unroll
     for (int k = 0; k < BC_K; ++k) {
       const int t = tb + k;
-      v[k] = t < T ? y[t] : qnan();
+      v[k] = yv(t);
+      if (bp && t < T) ystat[3 * T + t] = v[k];
       if (v[k] == v[k]) {
         const double d = v[k] - ry;
         acc[0] += v[k];
@@ -469,11 +479,13 @@ int launch_beta(int mode, const double* close, const double* btc_close, int64_t 
   A.ystat = ystat;
   const auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
   A.vin = a16(close) && (ld_in & 1) == 0;
-  A.vbtc = a16(btc_close) && (mode != 1 || (ld_in & 1) == 0);
+  A.vbtc = (mode == 4 ? a16(ystat + 3 * T) : a16(btc_close)) && (mode != 1 || (ld_in & 1) == 0);
   A.vout = (!beta || a16(beta)) && (!corr || a16(corr)) && (ld_out & 1) == 0;
-  if (mode == 3) {
-    hipLaunchKernelGGL(beta_btc_stats_kernel, dim3(1), dim3(BC_NT), 0, (hipStream_t)stream, btc_close, A.T, window,
-                       A.inv_w, A.inv_w1, ystat);
+  if (mode == 3 || mode == 4) {   // 4: benchmark prices, its returns formed by the pre-pass into ystat[3]
+    hipLaunchKernelGGL(beta_btc_stats_kernel, dim3(1), dim3(BC_NT), 0, (hipStream_t)stream,
+                       mode == 3 ? btc_close : nullptr, mode == 4 ? btc_close : nullptr, A.T, window, A.inv_w,
+                       A.inv_w1, ystat);
+    if (mode == 4) A.btc = ystat + 3 * T;
     hipLaunchKernelGGL(beta_wave_kernel<3>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
   } else if (mode == 1) hipLaunchKernelGGL(beta_wave_kernel<1>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
   else if (mode == 2) hipLaunchKernelGGL(beta_wave_kernel<2>, dim3((unsigned)S), dim3(WAVE), 0, (hipStream_t)stream, A);
@@ -491,6 +503,13 @@ extern "C" int bq_beta_corr_bret(const double* close, const double* btc_returns,
                                  int64_t T, int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out,
                                  void* stream) {
   return launch_beta(scratch ? 3 : 2, close, btc_returns, S, T, ld_in, window, beta, corr, ld_out, stream, scratch);
+}
+
+extern "C" int bq_beta_corr_ws(const double* close, const double* btc_close, double* scratch, int64_t S, int64_t T,
+                               int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out,
+                               void* stream) {
+  if (!scratch) return BQ_EINVAL;
+  return launch_beta(4, close, btc_close, S, T, ld_in, window, beta, corr, ld_out, stream, scratch);
 }
 
 extern "C" int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in,

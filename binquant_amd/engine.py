@@ -400,18 +400,15 @@ def beta_corr(
     btc = _check_panel(btc_close.reshape(1, -1), "btc_close", (1, T)).contiguous()
     beta = torch.empty((S, T), dtype=torch.float64, device=close.device)
     corr = torch.empty_like(beta)
-    # the benchmark's log returns once per call (log(c / c.shift(1)), :166-169),
-    # shared by every symbol row of the kernel (bq_beta_corr_bret)
-    bret = torch.full((T,), float("nan"), dtype=torch.float64, device=close.device)
-    if T > 1:
-        torch.log(btc[0, 1:] / btc[0, :-1], out=bret[1:])
-    scratch = torch.empty(3 * T, dtype=torch.float64, device=close.device)   # benchmark window stats
-    st = _lib.load().bq_beta_corr_bret(
-        ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(bret.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+    # the benchmark's log returns (log(c / c.shift(1)), :166-169) and window
+    # stats once per call, in the kernel's one-workgroup pre-pass (scratch)
+    scratch = torch.empty(4 * T, dtype=torch.float64, device=close.device)
+    st = _lib.load().bq_beta_corr_ws(
+        ctypes.c_void_p(close.data_ptr()), ctypes.c_void_p(btc.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
         S, T, _row_stride(close),
         int(window), ctypes.c_void_p(beta.data_ptr()), ctypes.c_void_p(corr.data_ptr()), T, _stream_handle(stream),
     )
-    _lib.check(st, "bq_beta_corr_bret")
+    _lib.check(st, "bq_beta_corr_ws")
     return {"beta": beta, "corr": corr}
 
 

@@ -363,6 +363,12 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
  * one-workgroup pre-pass) instead of in every symbol's wave. */
 int bq_beta_corr_bret(const double* close, const double* btc_returns, double* scratch, int64_t S, int64_t T,
                       int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
+/* bq_beta_corr with a device scratch of 4*T doubles: a one-workgroup
+ * pre-pass forms the benchmark's log returns and their window mean /
+ * variance / inverse variance once per call, then one wave per symbol row
+ * (engine.beta_corr: two launches per call, no host-side returns pass). */
+int bq_beta_corr_ws(const double* close, const double* btc_close, double* scratch, int64_t S, int64_t T,
+                    int64_t ld_in, int32_t window, double* beta, double* corr, int64_t ld_out, void* stream);
 int bq_beta_corr_pairs(const double* x, const double* y, int64_t S, int64_t T, int64_t ld_in, int32_t window,
                        double* beta, double* corr, int64_t ld_out, void* stream);
 

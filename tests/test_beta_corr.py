@@ -105,3 +105,35 @@ def test_kernel_jumps_partial_tiles_and_strides(cuda, window, odd_stride):
         wb, wc = ref.beta_corr_series(close[s], btc, window)
         assert_close(out["beta"][s].cpu().numpy(), wb, f"beta[{s}]", rtol=1e-8, scale=1.0)
         assert_close(out["corr"][s].cpu().numpy(), wc, f"corr[{s}]", rtol=1e-8, scale=1.0)
+
+
+@pytest.mark.gpu
+def test_entry_points_agree(cuda):
+    """bq_beta_corr_ws (engine), bq_beta_corr_bret (benchmark returns given)
+    and bq_beta_corr (both price rows, returns formed per wave) compute the
+    same sums: equal to 1e-12 on a panel with halts and jumps."""
+    import ctypes
+
+    from binquant_amd import _lib, engine
+    from binquant_amd.synth import numpy_panel
+
+    S, T, w = 20, 1500, 50
+    p = numpy_panel(S, T, seed0=5, edges=True)
+    c = torch.from_numpy(np.ascontiguousarray(p["close"])).cuda()
+    b = c[3].clone()
+    ref_out = engine.beta_corr(c, b, w)
+    lib = _lib.load()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    beta0, corr0 = torch.empty_like(c), torch.empty_like(c)
+    _lib.check(lib.bq_beta_corr(vp(c), vp(b), S, T, T, w, vp(beta0), vp(corr0), T, None), "bq_beta_corr")
+    bret = torch.full((T,), float("nan"), dtype=torch.float64, device="cuda")
+    torch.log(b[1:] / b[:-1], out=bret[1:])
+    scratch = torch.empty(3 * T, dtype=torch.float64, device="cuda")
+    beta3, corr3 = torch.empty_like(c), torch.empty_like(c)
+    _lib.check(lib.bq_beta_corr_bret(vp(c), vp(bret), vp(scratch), S, T, T, w, vp(beta3), vp(corr3), T, None),
+               "bq_beta_corr_bret")
+    torch.cuda.synchronize()
+    for got in (beta0, beta3):
+        assert_close(got.cpu().numpy(), ref_out["beta"].cpu().numpy(), "beta", rtol=1e-12, scale=1.0)
+    for got in (corr0, corr3):
+        assert_close(got.cpu().numpy(), ref_out["corr"].cpu().numpy(), "corr", rtol=1e-12, scale=1.0)
