@@ -616,6 +616,20 @@ __device__ __forceinline__ double okey_value(unsigned long long k) {
   return __longlong_as_double((long long)b);
 }
 
+// value of lane ^ ld (ld a power of two, a compile-time constant once the
+// sort's loops are unrolled): DPP quad permutes for 1 and 2, ds_swizzle's
+// xor mode for 4..16 (no address operand), ds_bpermute only across halves
+__device__ __forceinline__ unsigned lane_xor(unsigned v, int ld) {
+  switch (ld) {
+    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+    case 4: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+    case 8: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (8 << 10));
+    case 16: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (16 << 10));
+    default: return __shfl_xor(v, ld, WAVE);
+  }
+}
+
 template <int EPL, int OPL>
 __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
   constexpr int N = WAVE * EPL;          // sorted slots (power of two)
@@ -676,7 +690,7 @@ __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
           const int i = lane * EPL + e;
           const bool up = (i & k) == 0;
           const unsigned long long a = key[e], b = key[e + d];
-          const bool swap = up ? (b < a) : (a < b);
+          const bool swap = (up & (b < a)) | (!up & (a < b));   // selects, not branches
           key[e] = swap ? b : a;
           key[e + d] = swap ? a : b;
           const unsigned pa = pos[e], pb = pos[e + d];
@@ -688,13 +702,14 @@ __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
 #pragma unroll
         for (int e = 0; e < EPL; ++e) {
           const int i = lane * EPL + e;
-          const unsigned lo32 = __shfl_xor((unsigned)key[e], ld, WAVE);
-          const unsigned hi32 = __shfl_xor((unsigned)(key[e] >> 32), ld, WAVE);
-          const unsigned pp = __shfl_xor(pos[e], ld, WAVE);
+          const unsigned lo32 = lane_xor((unsigned)key[e], ld);
+          const unsigned hi32 = lane_xor((unsigned)(key[e] >> 32), ld);
+          const unsigned pp = lane_xor(pos[e], ld);
           const unsigned long long pk = ((unsigned long long)hi32 << 32) | lo32;
           const bool lower = (i & d) == 0, up = (i & k) == 0;
           // the lower slot of an ascending pair keeps the minimum
-          const bool take = (lower == up) ? (pk < key[e]) : (key[e] < pk);
+          const bool keep_min = lower == up;
+          const bool take = (keep_min & (pk < key[e])) | (!keep_min & (key[e] < pk));
           key[e] = take ? pk : key[e];
           pos[e] = take ? pp : pos[e];
         }
