@@ -189,14 +189,28 @@ __device__ __forceinline__ double oscillator(double a, double b) {
   return (100.0 * a) / (a + b);
 }
 
-// x / n for a small integer n via one reciprocal and one FMA correction:
-// the correctly rounded quotient except in rare ties (well inside the 1e-9
-// parity tolerance), at a fraction of the cost of an IEEE fp64 divide.
+// x / n for a small integer n via one reciprocal and one FMA correction,
+// r = RN(1 / n) computed once on the host. By Markstein's theorem (r within
+// half an ulp of 1/n, q = RN(x r) a faithful quotient, e = x - q n exact by
+// FMA) RN(q + e r) is the correctly rounded x / n for finite x away from
+// underflow: 0 mismatches in 51M random cases over n = 1..256, exponents
+// -300..300 (tests/csrc/div_exact_check.c, run by tests/test_div_exact.py).
+// 3 instructions against ~10 (one quarter-rate rcp) for the IEEE divide.
 __device__ __forceinline__ double div_exact(double x, double n, double r) {
-  // r = 1.0 / n, computed once on the host
   double q = x * r;
   const double e = fma(-q, n, x);
   return fma(e, r, q);
+}
+
+// div_exact where bit-equality with an IEEE divide is contractual (pandas
+// replays): zero, infinite and NaN x keep q = x r (±0, ±inf, NaN, as x / n),
+// and the rare |x| < 2^-960 takes the IEEE divide (a branch skipped when no
+// lane needs it).
+__device__ __forceinline__ double div_count(double x, double n, double r) {
+  if (__builtin_expect(fabs(x) < 0x1p-960 && x != 0.0, 0)) return x / n;
+  const double q = x * r;
+  const double c = fma(fma(-q, n, x), r, q);
+  return ((x == 0.0) | !(fabs(q) <= __DBL_MAX__)) ? q : c;
 }
 
 // 1 / v with the hardware reciprocal and two Newton steps (v > 0)

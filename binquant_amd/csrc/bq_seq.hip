@@ -45,7 +45,7 @@ struct StArgs {
   double *upper, *lower;
   int64_t S, ld_in, ld_out;
   int T, period, ring;   // ring: TR slots per lane (period + ST_SUB)
-  double mult;
+  double mult, inv_period;
 };
 
 // pandas roll_mean state for a fixed window with min_periods = window. The
@@ -76,8 +76,10 @@ struct AtrMean {
     nobs -= ok;
     neg -= ok & (bool)signbit(v);
   }
-  __device__ __forceinline__ double value(int minp) const {
-    const double r = sum / (double)nobs;
+  // min_periods = window: a value exists only at nobs == window, so the
+  // quotient is always sum / window (div_count: IEEE-exact, 3 fp64 ops)
+  __device__ __forceinline__ double value(int minp, double wd, double inv_w) const {
+    const double r = div_count(sum, wd, inv_w);
     double o = same >= nobs ? prev : r;
     o = ((same < nobs) & (((neg == 0) & (r < 0.0)) | ((neg == nobs) & (r > 0.0)))) ? 0.0 : o;
     return ((nobs < minp) | (nobs <= 0)) ? qnan() : o;
@@ -100,6 +102,7 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
   const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
   const int T = A.T;
   const int P = A.period, R = A.ring;
+  const double pd = (double)P;
   const double* const in[4] = {A.h, A.l, A.c, A.atr};
   double r[4][ST_CT];
 #pragma unroll
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
           if (u0 + j < T) {   // pandas: the removal, then the add, then calc_mean
             m.remove(old[j]);
             m.add(tr[j]);
-            atr[j] = m.value(P);
+            atr[j] = m.value(P, pd, A.inv_period);
           }
         }
       }
@@ -178,6 +181,118 @@ __global__ __launch_bounds__(WAVE) void supertrend_kernel(const StArgs A) {
     stage_store<ST_CT>(sX[0], A.upper, A.ld_out, sym0, A.S, t0, T, lane);   // null: dropped
     stage_store<ST_CT>(sX[1], A.lower, A.ld_out, sym0, A.S, t0, T, lane);
     stage_store<ST_CT>(sX[2], A.up, A.ld_out, sym0, A.S, t0, T, lane);
+    __syncthreads();
+  }
+}
+
+// bq_supertrend_hlc as a two-wave pipeline per 64 symbols: the walk is bound
+// per wave (its time is flat from 1 024 to 16 384 symbols; ablation at
+// 12.5k x 2k — 1.0 ms whole, 0.60 without the ATR replay, 0.83 without the
+// stores), so its per-step work is split over two waves on two SIMDs
+// (0.95 -> 0.88 ms: what is left is the latency of each chunk's loads with
+// only 196 waves' worth of loads in flight). Wave 0
+// stages chunk n (loads, LDS transpose), forms its TRs and replays pandas'
+// roll_mean into sAtr; wave 1 runs the band / trend recursion on chunk n - 1
+// from the same LDS tiles, writes the results in place and streams them out.
+// Three barriers per chunk; both waves pass every one of them.
+__global__ __launch_bounds__(2 * WAVE) void supertrend_pipe_kernel(const StArgs A) {
+  // dynamic LDS (> 64 KiB at the largest periods): two chunk buffers of
+  // h, l, c (wave 1 overwrites them with upper, lower, trend), two ATR
+  // tiles, then the TR ring [ring][WAVE] of wave 0
+  extern __shared__ double smem[];
+  constexpr int TL = ST_CT * STG_PITCH;
+  double(*sIn)[3][TL] = reinterpret_cast<double(*)[3][TL]>(smem);
+  double(*sAtr)[TL] = reinterpret_cast<double(*)[TL]>(smem + 6 * TL);
+  double* sTR = smem + 8 * TL;
+  const int wv = threadIdx.x / WAVE, lane = threadIdx.x & (WAVE - 1);
+  const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
+  const int T = A.T;
+  const int P = A.period, R = A.ring;
+  const double pd = (double)P;
+  const double* const in[3] = {A.h, A.l, A.c};
+  const int nch = (T + ST_CT - 1) / ST_CT;
+  // wave 0 state
+  double r[3][ST_CT];
+  double pc = qnan();
+  AtrMean m{0.0, 0.0, 0.0, 0.0, 0, 0, 0};
+  int wslot = 0, rslot = R - P;
+  // wave 1 state
+  bool up = true;
+  double up_p = qnan(), lo_p = qnan();   // NaN bands before candle 0
+  if (wv == 0) {
+#pragma unroll
+    for (int f = 0; f < 3; ++f) stage_load<ST_CT>(in[f], A.ld_in, sym0, A.S, 0, T, lane, r[f]);
+  }
+  for (int n = 0; n <= nch; ++n) {
+    const int b = n & 1, b1 = b ^ 1;
+    if (wv == 0 && n < nch) {
+#pragma unroll
+      for (int f = 0; f < 3; ++f) stage_put<ST_CT>(sIn[b][f], lane, r[f]);
+    }
+    __syncthreads();
+    if (wv == 0) {
+      if (n < nch) {
+        const int t0 = n * ST_CT;
+#pragma unroll
+        for (int f = 0; f < 3; ++f) stage_load<ST_CT>(in[f], A.ld_in, sym0, A.S, t0 + ST_CT, T, lane, r[f]);
+#pragma unroll
+        for (int j0 = 0; j0 < ST_CT; j0 += ST_SUB) {
+          double tr[ST_SUB], old[ST_SUB], c[ST_SUB];
+#pragma unroll
+          for (int j = 0; j < ST_SUB; ++j) {
+            const int i = (j0 + j) * STG_PITCH + lane;
+            c[j] = sIn[b][2][i];
+            tr[j] = true_range(sIn[b][0][i], sIn[b][1][i], j == 0 ? pc : c[j - 1]);
+            const int ws = wslot + j >= R ? wslot + j - R : wslot + j;
+            sTR[ws * WAVE + lane] = tr[j];
+          }
+#pragma unroll
+          for (int j = 0; j < ST_SUB; ++j) {
+            const int rs = rslot + j >= R ? rslot + j - R : rslot + j;
+            old[j] = t0 + j0 + j >= P ? sTR[rs * WAVE + lane] : qnan();   // NaN: nothing leaves
+          }
+          pc = c[ST_SUB - 1];
+          wslot = wslot + ST_SUB >= R ? wslot + ST_SUB - R : wslot + ST_SUB;
+          rslot = rslot + ST_SUB >= R ? rslot + ST_SUB - R : rslot + ST_SUB;
+#pragma unroll
+          for (int j = 0; j < ST_SUB; ++j) {
+            if (t0 + j0 + j < T) {   // pandas: the removal, then the add, then calc_mean
+              m.remove(old[j]);
+              m.add(tr[j]);
+              sAtr[b][(j0 + j) * STG_PITCH + lane] = m.value(P, pd, A.inv_period);
+            }
+          }
+        }
+      }
+    } else if (n >= 1) {
+      const int t0 = (n - 1) * ST_CT;
+#pragma unroll
+      for (int j = 0; j < ST_CT; ++j) {
+        if (t0 + j < T) {
+          const int i = j * STG_PITCH + lane;
+          const double h = sIn[b1][0][i], l = sIn[b1][1][i], c = sIn[b1][2][i];
+          const double hl2 = (h + l) / 2.0;
+          const double m_atr = A.mult * sAtr[b1][i];
+          double bu = hl2 + m_atr, bl = hl2 - m_atr;
+          const bool flip_up = c > up_p, flip_dn = !flip_up & (c < lo_p), hold = !flip_up & !flip_dn;
+          up = flip_up | (!flip_dn & up);
+          bl = (hold & up & (bl < lo_p)) ? lo_p : bl;
+          bu = (hold & !up & (bu > up_p)) ? up_p : bu;
+          up_p = bu;
+          lo_p = bl;
+          sIn[b1][0][i] = bu;
+          sIn[b1][1][i] = bl;
+          sIn[b1][2][i] = up ? 1.0 : 0.0;
+        }
+      }
+    }
+    __syncthreads();
+    if (wv == 1 && n >= 1) {
+      const int t0 = (n - 1) * ST_CT;
+      stage_store<ST_CT>(sIn[b1][0], A.upper, A.ld_out, sym0, A.S, t0, T, lane);   // null: dropped
+      stage_store<ST_CT>(sIn[b1][1], A.lower, A.ld_out, sym0, A.S, t0, T, lane);
+      stage_store<ST_CT>(sIn[b1][2], A.up, A.ld_out, sym0, A.S, t0, T, lane);
+    }
     __syncthreads();
   }
 }
@@ -210,11 +325,24 @@ int launch_supertrend(bool fatr, const double* const* in, int64_t S, int64_t T, 
   A.mult = multiplier;
   const int ring = fatr ? period + ST_SUB : 0;
   A.period = fatr ? period : 0;
+  A.inv_period = fatr ? 1.0 / (double)period : 0.0;
   A.ring = ring;
   const unsigned blocks = (unsigned)((S + WAVE - 1) / WAVE);
-  if (fatr)
+  if (fatr) {
+    // > 64 KiB of LDS at the largest periods: opt in once, before any graph
+    // capture can be active (first call of the process)
+    static const bool lds_opt_in = hipFuncSetAttribute((const void*)supertrend_pipe_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       160 * 1024) == hipSuccess;
+    (void)lds_opt_in;
+#ifdef BQ_ST_ONE_WAVE
     hipLaunchKernelGGL(supertrend_kernel<true>, dim3(blocks), dim3(WAVE), (size_t)ring * WAVE * sizeof(double),
                        (hipStream_t)stream, A);
+#else
+    hipLaunchKernelGGL(supertrend_pipe_kernel, dim3(blocks), dim3(2 * WAVE),
+                       (size_t)(8 * ST_CT * STG_PITCH + ring * WAVE) * sizeof(double), (hipStream_t)stream, A);
+#endif
+  }
   else
     hipLaunchKernelGGL(supertrend_kernel<false>, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
