@@ -137,3 +137,22 @@ def test_entry_points_agree(cuda):
         assert_close(got.cpu().numpy(), ref_out["beta"].cpu().numpy(), "beta", rtol=1e-12, scale=1.0)
     for got in (corr0, corr3):
         assert_close(got.cpu().numpy(), ref_out["corr"].cpu().numpy(), "corr", rtol=1e-12, scale=1.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 2, 50, 51, 255, 256, 257, 384, 512, 513])
+def test_kernel_tile_edges(cuda, T):
+    """Row lengths around the wave walker's 256-candle tiles and the window
+    (first full window at t = w; the halo re-based at every tile end)."""
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    S, w = 5, 50
+    p = numpy_panel(S, max(T, 2), seed0=T, edges=True)
+    close = np.ascontiguousarray(p["close"][:, :T])
+    btc = close[1].copy()
+    out = engine.beta_corr(torch.from_numpy(close).cuda(), torch.from_numpy(btc).cuda(), window=w)
+    for s in range(S):
+        wb, wc = ref.beta_corr_series(close[s], btc, w)
+        assert_close(out["beta"][s].cpu().numpy(), wb, f"beta[{s}]", rtol=1e-8, scale=1.0)
+        assert_close(out["corr"][s].cpu().numpy(), wc, f"corr[{s}]", rtol=1e-8, scale=1.0)
