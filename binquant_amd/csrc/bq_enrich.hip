@@ -178,8 +178,61 @@ __device__ __forceinline__ void load4(const double* __restrict__ row, int tb, in
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) dbl2 gdbl2;
 
-__device__ __forceinline__ void store4(double* __restrict__ row_, int tb, int T, bool vec, const double (&x)[EN_K]) {
+#ifndef BQ_EN_SWAPST
+#define BQ_EN_SWAPST 1   // whole-line output stores through v_permlane32_swap
+#endif
+
+__device__ __forceinline__ void put2(gdouble* row, int t, int T, bool full, dbl2 v) {
+  if (full || t + 2 <= T) {
+#if BQ_EN_NTSTORE
+    __builtin_nontemporal_store(v, reinterpret_cast<gdbl2*>(row + t));
+#else
+    *reinterpret_cast<gdbl2*>(row + t) = v;
+#endif
+  } else if (t < T) {
+    row[t] = v.x;
+  }
+}
+
+// Output stores. A lane holds 4 consecutive candles, so its natural pair of
+// 16-byte stores covers every other 16 bytes of the wave's 2 KiB per
+// instruction — half of each 128-byte line, the other half a separate
+// instruction. At the headline shape that pattern caps the 5-in / 14-out
+// stream at ~5.3 TB/s, whole-line coverage per instruction reaches ~6.4
+// (tools/coalesce_ceiling.hip, 100k x 10k). v_permlane32_swap exchanges the
+// upper half-wave's first pair with the lower half-wave's second pair: then
+// register A holds candles [0, 128) of the wave's slice (lane a < 32 its own
+// 4a, 4a+1; lane 32 + a lane a's 4a+2, 4a+3) and register B candles
+// [128, 256), so each store instruction writes one contiguous KiB (lanes
+// permuted within it). `vec` is wave-uniform (a kernel argument), so every
+// lane takes part in the swap; `full` (every candle of the tile in range)
+// drops the range checks.
+__device__ __forceinline__ void store4(double* __restrict__ row_, int tb, int T, bool vec, const double (&x)[EN_K],
+                                       bool full = false) {
   gdouble* row = (gdouble*)row_;
+#if BQ_EN_SWAPST
+  if constexpr (EN_K == 4) {
+    if (vec) {
+      union {
+        dbl2 d;
+        unsigned u[4];
+      } a, b;
+      a.d = dbl2{x[0], x[1]};
+      b.d = dbl2{x[2], x[3]};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane32_swap(a.u[i], b.u[i], false, false);
+        a.u[i] = r[0];
+        b.u[i] = r[1];
+      }
+      const int lane = __lane_id();
+      const int ta = lane < 32 ? tb : tb - 126;   // lane 32 + a: wave base + 4a + 2
+      put2(row, ta, T, full, a.d);
+      put2(row, ta + 128, T, full, b.d);
+      return;
+    }
+  }
+#endif
   if (vec && tb + EN_K <= T) {
     gdbl2* p = reinterpret_cast<gdbl2*>(row + tb);
 #pragma unroll
@@ -218,8 +271,10 @@ __device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int 
   }
 }
 
-template <bool DIV>
-__global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichArgs A, int vec_in, int vec_out) {
+// VOUT: every output row 16-byte aligned (a template argument, so the
+// unaligned element-wise store path is not compiled into the common kernel)
+template <bool DIV, bool VOUT>
+__global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichArgs A, int vec_in) {
   // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
   __shared__ double sP[EN_R];    // close prefix: halo re-based, tile wave-local
   __shared__ double sC[EN_R];    // close
@@ -244,7 +299,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   const int64_t irow = sym * A.ld_in;
   const int64_t orow = sym * A.ld_out;
   const int T = A.T;
-  const bool vin = vec_in != 0, vout = vec_out != 0;
+  const bool vin = vec_in != 0, vout = VOUT;
 
   // the first tile's loads go out before anything else: their HBM latency
   // overlaps the serial constant set-up below (a workgroup's fixed start-up
@@ -478,10 +533,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         e0[k] = y[E_0];
         e1[k] = y[E_1];
       }
-      if (P.out[BQ_MACD]) store4(P.out[BQ_MACD] + orow, tb, T, vout, mfast);
-      if (P.out[BQ_MACD_SIGNAL]) store4(P.out[BQ_MACD_SIGNAL] + orow, tb, T, vout, msig);
-      if (P.out[BQ_EMA_FAST]) store4(P.out[BQ_EMA_FAST] + orow, tb, T, vout, e0);
-      if (P.out[BQ_EMA_SLOW]) store4(P.out[BQ_EMA_SLOW] + orow, tb, T, vout, e1);
+      const bool whole = t0 + EN_TT <= T;
+      if (P.out[BQ_MACD]) store4(P.out[BQ_MACD] + orow, tb, T, vout, mfast, whole);
+      if (P.out[BQ_MACD_SIGNAL]) store4(P.out[BQ_MACD_SIGNAL] + orow, tb, T, vout, msig, whole);
+      if (P.out[BQ_EMA_FAST]) store4(P.out[BQ_EMA_FAST] + orow, tb, T, vout, e0, whole);
+      if (P.out[BQ_EMA_SLOW]) store4(P.out[BQ_EMA_SLOW] + orow, tb, T, vout, e1, whole);
     }
 
     // ---- rolling windows -------------------------------------------------------
@@ -508,7 +564,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
       (void)lb;
       auto warm = [&](int t, int win) { return !FULL && t < win - 1; };
       auto put = [&](double* col, const double (&x)[EN_K]) {
-        if (FULL) store4(col + orow, tb, T, true, x);
+        if (FULL) store4(col + orow, tb, T, true, x, true);
         else store4(col + orow, tb, T, vout, x);
       };
       // close.rolling(win).mean(): prefix difference / win, or the value
@@ -832,10 +888,12 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
     const double al = 1.0 / (1.0 + com);
     div |= ((1.0 - al) + al) != 1.0;
   }
-  if (div)
-    hipLaunchKernelGGL(enrich_kernel<true>, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
-  else
-    hipLaunchKernelGGL(enrich_kernel<false>, dim3((unsigned)S), dim3(EN_NT), 0, (hipStream_t)stream, A, vin, vout);
+  const dim3 grid((unsigned)S), block(EN_NT);
+  hipStream_t st = (hipStream_t)stream;
+  if (div && vout) hipLaunchKernelGGL((enrich_kernel<true, true>), grid, block, 0, st, A, vin);
+  else if (div) hipLaunchKernelGGL((enrich_kernel<true, false>), grid, block, 0, st, A, vin);
+  else if (vout) hipLaunchKernelGGL((enrich_kernel<false, true>), grid, block, 0, st, A, vin);
+  else hipLaunchKernelGGL((enrich_kernel<false, false>), grid, block, 0, st, A, vin);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
