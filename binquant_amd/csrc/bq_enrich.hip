@@ -273,7 +273,16 @@ __device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int 
 
 // VOUT: every output row 16-byte aligned (a template argument, so the
 // unaligned element-wise store path is not compiled into the common kernel)
-template <bool DIV, bool VOUT>
+// DEF: the windows are the reference's (ma 7/25/100, rsi 14, bb 20, atr 14,
+// twap 12, mfi 14): compile-time window lengths let every window walk unroll
+// completely (all ring reads issued before the dependent sums, immediate LDS
+// offsets) — the same operations in the same order as the generic kernel.
+template <bool DEF>
+__device__ __forceinline__ int win_of(int def, int v) {
+  return DEF ? def : __builtin_amdgcn_readfirstlane(v);
+}
+
+template <bool DIV, bool VOUT, bool DEF>
 __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichArgs A, int vec_in) {
   // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
   __shared__ double sP[EN_R];    // close prefix: halo re-based, tile wave-local
@@ -581,7 +590,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         if (P.out[BQ_MA_FAST + i]) {
-          const int win = __builtin_amdgcn_readfirstlane(P.ma[i]);
+          const int win = win_of<DEF>(i == 0 ? 7 : (i == 1 ? 25 : 100), P.ma[i]);
           const double inv = P.inv_ma[i];
 #pragma unroll
           for (int k = 0; k < EN_K; ++k) res[k] = cmean(win, inv, k);
@@ -592,11 +601,12 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         // mean from the prefix; variance from sliding sums of (c - r), (c - r)^2
         // with the lane-local reference r = close at the lane's first candle.
         double up[EN_K], mid[EN_K], lo[EN_K];
-        const int win = __builtin_amdgcn_readfirstlane(P.bb_w);
+        const int win = win_of<DEF>(20, P.bb_w);
         const double bk = P.bb_k, invw = P.inv_bb, invdv = P.inv_bb_dv;
         const bool okdv = win > P.bb_ddof;
         const double r = cu.c[0];
         double s1 = 0.0, s2 = 0.0;
+#pragma unroll
         for (int x = FULL ? 1 - win : max(1 - win, gstart - pb); x <= 0; ++x) {
           const double d = sC[RS(x)] - r;
           s1 += d;
@@ -633,9 +643,10 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         // c_t - c_{t-w} (telescoping): RSI = 50 (1 + D / A). Counts of up
         // and down moves make the all-gain (100), all-loss (0) and flat (NaN)
         // windows exact. d of candle 0 is NaN -> contributes nothing.
-        const int win = __builtin_amdgcn_readfirstlane(P.rsi_w);
+        const int win = win_of<DEF>(14, P.rsi_w);
         double A = 0.0, prev = sC[RS(-win)];
         int nup = 0, ndn = 0;
+#pragma unroll
         for (int x = 1 - win; x <= 0; ++x) {
           const double c = sC[RS(x)], d = c - prev;
           A += fmax(fabs(d), 0.0);   // fmax drops the NaN of candle 0
@@ -668,11 +679,12 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         put(P.out[BQ_RSI], res);
       }
       // sliding mean of a per-candle ring array with the same-value rule
-      auto smean = [&](const double* Q, int win_, double inv, bool nonneg) {
-        const int win = __builtin_amdgcn_readfirstlane(win_);
+      auto smean = [&](const double* Q, int defw, int win_, double inv, bool nonneg) {
+        const int win = win_of<DEF>(defw, win_);
         const double wd = (double)win;
         double sum = 0.0, pq = qnan();
         int run = 0;
+#pragma unroll
         for (int x = 1 - win; x <= 0; ++x) {
           const double q = Q[RS(x)];
           sum += q;
@@ -694,20 +706,21 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         }
       };
       if (P.out[BQ_ATR]) {
-        smean(sTR, P.atr_w, P.inv_atr, true);
+        smean(sTR, 14, P.atr_w, P.inv_atr, true);
         put(P.out[BQ_ATR], res);
       }
       if (P.out[BQ_TWAP]) {
-        smean(sO4, P.twap_w, P.inv_twap, false);
+        smean(sO4, 12, P.twap_w, P.inv_twap, false);
         put(P.out[BQ_TWAP], res);
       }
       if (P.out[BQ_MFI]) {
         // MFI = 100 pos / (pos + neg) with pos + neg = B = sum|f| and
         // pos - neg = F = sum f (f = signed flow): MFI = 50 (1 + F / B);
         // counts of up/down flows make the one-sided and empty windows exact.
-        const int win = __builtin_amdgcn_readfirstlane(P.mfi_w);
+        const int win = win_of<DEF>(14, P.mfi_w);
         double B = 0.0, F = 0.0;
         int nup = 0, ndn = 0;
+#pragma unroll
         for (int x = 1 - win; x <= 0; ++x) {
           const double f = sMF[RS(x)];
           B += fabs(f);
@@ -890,10 +903,21 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   }
   const dim3 grid((unsigned)S), block(EN_NT);
   hipStream_t st = (hipStream_t)stream;
-  if (div && vout) hipLaunchKernelGGL((enrich_kernel<true, true>), grid, block, 0, st, A, vin);
-  else if (div) hipLaunchKernelGGL((enrich_kernel<true, false>), grid, block, 0, st, A, vin);
-  else if (vout) hipLaunchKernelGGL((enrich_kernel<false, true>), grid, block, 0, st, A, vin);
-  else hipLaunchKernelGGL((enrich_kernel<false, false>), grid, block, 0, st, A, vin);
+  const bool def = P.ma_periods[0] == 7 && P.ma_periods[1] == 25 && P.ma_periods[2] == 100 && P.rsi_window == 14 &&
+                   P.bb_window == 20 && P.atr_window == 14 && P.twap_window == 12 && P.mfi_window == 14;
+#define BQ_EN_LAUNCH(D, V, F) hipLaunchKernelGGL((enrich_kernel<D, V, F>), grid, block, 0, st, A, vin)
+  if (def) {
+    if (div && vout) BQ_EN_LAUNCH(true, true, true);
+    else if (div) BQ_EN_LAUNCH(true, false, true);
+    else if (vout) BQ_EN_LAUNCH(false, true, true);
+    else BQ_EN_LAUNCH(false, false, true);
+  } else {
+    if (div && vout) BQ_EN_LAUNCH(true, true, false);
+    else if (div) BQ_EN_LAUNCH(true, false, false);
+    else if (vout) BQ_EN_LAUNCH(false, true, false);
+    else BQ_EN_LAUNCH(false, false, false);
+  }
+#undef BQ_EN_LAUNCH
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
