@@ -99,15 +99,10 @@ __device__ __forceinline__ void ld4(const double* __restrict__ r, int t, int T, 
   }
 }
 
+// write-once outputs: whole-line nontemporal stores (bq_device.h store_lines);
+// the wave's lanes all call it (one wave per symbol)
 __device__ __forceinline__ void st4(double* r, int t, int T, bool vec, const double (&v)[4]) {
-  if (vec && t + 4 <= T) {   // write-once outputs: nontemporal (streamed past L2)
-    __builtin_nontemporal_store(bq_v2d{v[0], v[1]}, reinterpret_cast<bq_v2d*>(r + t));
-    __builtin_nontemporal_store(bq_v2d{v[2], v[3]}, reinterpret_cast<bq_v2d*>(r + t + 2));
-  } else {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (t + k < T) __builtin_nontemporal_store(v[k], r + t + k);
-  }
+  store_lines<4>(r, t, T, vec, v);
 }
 
 constexpr int BW_TT = WAVE * BC_K;   // candles per tile

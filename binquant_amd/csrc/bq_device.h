@@ -325,4 +325,117 @@ __device__ __forceinline__ double safe_pct(double cur, double prev) {
   return (cur - prev) / fabs(prev);
 }
 
+
+// ---- line-covering stores ---------------------------------------------------
+// A lane holding K consecutive fp64 candles (K/2 16-byte pieces) stores them
+// with K/2 instructions, each covering 16 bytes of every 8K bytes: 1/2 (K = 4)
+// or 1/4 (K = 8) of each 128-byte line per instruction. At full-chip write
+// rates that pattern streams ~20 % below whole-line coverage
+// (tools/coalesce_ceiling.hip). line_exchange moves the pieces between lanes
+// with v_permlane32_swap / v_permlane16_swap (no LDS) so that register m holds
+// candles [128 m, 128 m + 128) of the wave's slice, lane L at candle offset
+// line_offset<K>(L) + 128 m: each store instruction writes one contiguous KiB
+// (lanes permuted within it). Every lane of the wave must execute it.
+// Checked on the GPU by tools/permlane_check.hip.
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+union DwordsOf2 {
+  dbl2 d;
+  unsigned u[4];
+};
+
+// lanes 32-63 of a <-> lanes 0-31 of b
+__device__ __forceinline__ void swap_halves(dbl2& a, dbl2& b) {
+  DwordsOf2 x, y;
+  x.d = a;
+  y.d = b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x.u[i], y.u[i], false, false);
+    x.u[i] = r[0];
+    y.u[i] = r[1];
+  }
+  a = x.d;
+  b = y.d;
+}
+
+// rows 1 and 3 of a <-> rows 0 and 2 of b (rows of 16 lanes)
+__device__ __forceinline__ void swap_rows(dbl2& a, dbl2& b) {
+  DwordsOf2 x, y;
+  x.d = a;
+  y.d = b;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x.u[i], y.u[i], false, false);
+    x.u[i] = r[0];
+    y.u[i] = r[1];
+  }
+  a = x.d;
+  b = y.d;
+}
+
+template <int K>
+__device__ __forceinline__ void line_exchange(dbl2 (&p)[K / 2]) {
+  static_assert(K == 4 || K == 8, "line_exchange: 4 or 8 candles per lane");
+  if constexpr (K == 4) {
+    swap_halves(p[0], p[1]);
+  } else {   // 4 x 4 transpose of (row, piece): two butterfly stages
+    swap_halves(p[0], p[2]);
+    swap_halves(p[1], p[3]);
+    swap_rows(p[0], p[1]);
+    swap_rows(p[2], p[3]);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ int line_offset(int lane) {
+  if constexpr (K == 4) return lane < 32 ? 4 * lane : 4 * (lane - 32) + 2;
+  else return 8 * (lane & 15) + 2 * (lane >> 4);
+}
+
+
+// Row stores of a lane's K consecutive candles starting at candle tb of `row`
+// through line_exchange. vec (16-byte aligned row, wave-uniform) selects the
+// exchanged vector path, executed by every lane; full = every candle of the
+// wave's slice is < T (drops the range checks). Non-temporal: the outputs
+// are streamed, not re-read by the kernel.
+template <int K>
+__device__ __forceinline__ void store_lines(double* __restrict__ row_, int tb, int T, bool vec, const double (&x)[K],
+                                            bool full = false) {
+  typedef __attribute__((address_space(1))) double gd;
+  typedef __attribute__((address_space(1))) dbl2 gd2;
+  gd* row = (gd*)row_;
+  if (vec) {
+    dbl2 p[K / 2];
+#pragma unroll
+    for (int j = 0; j < K / 2; ++j) p[j] = dbl2{x[2 * j], x[2 * j + 1]};
+    line_exchange<K>(p);
+    const int lane = __lane_id();
+    const int t = tb - K * lane + line_offset<K>(lane);
+#pragma unroll
+    for (int m = 0; m < K / 2; ++m) {
+      const int u = t + 128 * m;
+      if (full || u + 2 <= T) __builtin_nontemporal_store(p[m], reinterpret_cast<gd2*>(row + u));
+      else if (u < T) row[u] = p[m].x;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (tb + k < T) row[tb + k] = x[k];
+  }
+}
+
+
+// x = lo .. 0 through f; UNROLL (lo a compile-time constant after inlining)
+// unrolls the walk completely, otherwise the compiler's default applies.
+template <bool UNROLL, typename F>
+__device__ __forceinline__ void walk_window(int lo, F&& f) {
+  if constexpr (UNROLL) {
+#pragma unroll
+    for (int x = lo; x <= 0; ++x) f(x);
+  } else {
+    for (int x = lo; x <= 0; ++x) f(x);
+  }
+}
+
 }  // namespace bq

@@ -606,12 +606,11 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const bool okdv = win > P.bb_ddof;
         const double r = cu.c[0];
         double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-        for (int x = FULL ? 1 - win : max(1 - win, gstart - pb); x <= 0; ++x) {
+        walk_window<DEF && FULL>(FULL ? 1 - win : max(1 - win, gstart - pb), [&](int x) {
           const double d = sC[RS(x)] - r;
           s1 += d;
           s2 = fma(d, d, s2);
-        }
+        });
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k, p = pb + k;
@@ -646,14 +645,13 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const int win = win_of<DEF>(14, P.rsi_w);
         double A = 0.0, prev = sC[RS(-win)];
         int nup = 0, ndn = 0;
-#pragma unroll
-        for (int x = 1 - win; x <= 0; ++x) {
+        walk_window<DEF>(1 - win, [&](int x) {
           const double c = sC[RS(x)], d = c - prev;
           A += fmax(fabs(d), 0.0);   // fmax drops the NaN of candle 0
           nup += d > 0.0;
           ndn += d < 0.0;
           prev = c;
-        }
+        });
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k, p = pb + k;
@@ -684,13 +682,12 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const double wd = (double)win;
         double sum = 0.0, pq = qnan();
         int run = 0;
-#pragma unroll
-        for (int x = 1 - win; x <= 0; ++x) {
+        walk_window<DEF>(1 - win, [&](int x) {
           const double q = Q[RS(x)];
           sum += q;
           run = q == pq ? run + 1 : 1;
           pq = q;
-        }
+        });
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k;
@@ -720,14 +717,13 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const int win = win_of<DEF>(14, P.mfi_w);
         double B = 0.0, F = 0.0;
         int nup = 0, ndn = 0;
-#pragma unroll
-        for (int x = 1 - win; x <= 0; ++x) {
+        walk_window<DEF>(1 - win, [&](int x) {
           const double f = sMF[RS(x)];
           B += fabs(f);
           F += f;
           nup += f > 0.0;
           ndn += f < 0.0;
-        }
+        });
 #pragma unroll
         for (int k = 0; k < EN_K; ++k) {
           const int t = tb + k;

@@ -65,18 +65,10 @@ __device__ __forceinline__ void mf_load(const double* __restrict__ row, int tb, 
 
 typedef double mdbl2 __attribute__((ext_vector_type(2)));
 
+// whole-line stores (bq_device.h store_lines); called by every thread of the block
 __device__ __forceinline__ void mf_store(double* __restrict__ row, int tb, int T, bool vec,
                                          const double (&x)[MF_K]) {
-  if (vec && tb + MF_K <= T) {
-    mdbl2* p = reinterpret_cast<mdbl2*>(row + tb);
-    mdbl2 a = {x[0], x[1]}, b = {x[2], x[3]};
-    __builtin_nontemporal_store(a, p);
-    __builtin_nontemporal_store(b, p + 1);
-  } else {
-#pragma unroll
-    for (int k = 0; k < MF_K; ++k)
-      if (tb + k < T) row[tb + k] = x[k];
-  }
+  store_lines<MF_K>(row, tb, T, vec, x);
 }
 
 __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int vec_in, int vec_out) {
@@ -284,9 +276,18 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       } else {
         mid = (sPc[q] - sPc[q - mb]) / (double)mb;
         double acc = 0.0;
-        for (int i = q - mb + 1; i <= q; ++i) {
-          const double d = sC[i] - mid;
-          acc = fma(d, d, acc);
+        if (mb == BB_W) {   // every candle past the warm-up: a compile-time walk,
+                            // all 20 ring reads issued ahead of the sum (same order)
+#pragma unroll
+          for (int j = 1 - BB_W; j <= 0; ++j) {
+            const double d = sC[q + j] - mid;
+            acc = fma(d, d, acc);
+          }
+        } else {
+          for (int i = q - mb + 1; i <= q; ++i) {
+            const double d = sC[i] - mid;
+            acc = fma(d, d, acc);
+          }
         }
         sd = sqrt(acc / (double)mb);
       }

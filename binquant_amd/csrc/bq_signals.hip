@@ -62,16 +62,9 @@ __device__ __forceinline__ void sg_load(const double* __restrict__ row, int tb, 
   }
 }
 
+// whole-line stores (bq_device.h store_lines); every thread of the block calls it
 __device__ __forceinline__ void sg_store(double* __restrict__ row, int tb, int T, bool vec, const double (&x)[SG_K]) {
-  if (vec && tb + SG_K <= T) {
-    sg_dbl2* p = reinterpret_cast<sg_dbl2*>(row + tb);
-#pragma unroll
-    for (int j = 0; j < SG_K / 2; ++j) __builtin_nontemporal_store(sg_dbl2{x[2 * j], x[2 * j + 1]}, p + j);
-  } else {
-#pragma unroll
-    for (int k = 0; k < SG_K; ++k)
-      if (tb + k < T) row[tb + k] = x[k];
-  }
+  store_lines<SG_K>(row, tb, T, vec, x);
 }
 
 // Block-wide inclusive max of a per-lane int (>= -1): wave DPP scan, wave
@@ -100,6 +93,9 @@ struct SigArgs {
 // ---- zscore ----------------------------------------------------------------------
 // mean = close.rolling(w, min_periods=w).mean(), std = .std(ddof=0);
 // z = 0 where std == 0 or NaN (incl. the warm-up), else (c - mean) / std.
+// W > 0: the window is the reference's (20), known at compile time, so the
+// window walks unroll completely (same operations, same order); W = 0: any.
+template <int W>
 __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
   __shared__ double sC[SG_R];
   __shared__ int sW[SG_NW];
@@ -109,7 +105,7 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
   const double* __restrict__ rc = A.in[0] + sym * A.ld_in;
   double* __restrict__ ro = A.out + sym * A.ld_out;
   const int T = A.T;
-  const int win = __builtin_amdgcn_readfirstlane(A.win);
+  const int win = W ? W : __builtin_amdgcn_readfirstlane(A.win);
   if (tid < SG_H) sC[sg_slot(tid)] = qnan();
   if (tid == 0) sCar = -1;
   double nx[SG_K];
@@ -146,11 +142,17 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
       const int gs = SG_H - t0;   // ring position of candle 0
       const double r = c[0];
       double s1 = 0.0, s2 = 0.0;
-      for (int x = max(1 - win, gs - pb); x <= 0; ++x) {
-        const double v = sC[sg_slot(pb + x)];
+      auto walk = [&](int x0) {
+        const double v = sC[sg_slot(pb + x0)];
         const double d = v - r;
         s1 += d;
         s2 = fma(d, d, s2);
+      };
+      if (W && gs - pb <= 1 - W) {
+#pragma unroll
+        for (int x = 1 - W; x <= 0; ++x) walk(x);
+      } else {
+        for (int x = max(1 - win, gs - pb); x <= 0; ++x) walk(x);
       }
 #pragma unroll
       for (int k = 0; k < SG_K; ++k) {
@@ -186,6 +188,7 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
 // tr = max(h - l, |h - pc|, |l - pc|) (skip NaN), +DM / -DM, rolling(w) sums,
 // DI = 100 * sum / atr_sum, dx = 100 |DI+ - DI-| / (DI+ + DI-) (0 for a zero
 // or NaN denominator, fillna(0)), adx = dx.rolling(w).mean(), 100 where NaN.
+template <int W>   // as zscore_kernel (the reference's window: 14)
 __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
   __shared__ double sTR[SG_R], sPD[SG_R], sMD[SG_R], sDX[SG_R];
   __shared__ int sW[SG_NW], sW2[SG_NW];
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
   const double* __restrict__ rc = A.in[2] + sym * A.ld_in;
   double* __restrict__ ro = A.out + sym * A.ld_out;
   const int T = A.T;
-  const int win = __builtin_amdgcn_readfirstlane(A.win);
+  const int win = W ? W : __builtin_amdgcn_readfirstlane(A.win);
   if (tid < SG_H) {
     sTR[sg_slot(tid)] = sPD[sg_slot(tid)] = sMD[sg_slot(tid)] = sDX[sg_slot(tid)] = 0.0;
   }
@@ -262,11 +265,11 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
     double dx[SG_K];
     {
       double st = 0.0, sp = 0.0, sm = 0.0;
-      for (int x = 1 - win; x <= 0; ++x) {
+      walk_window<(W > 0)>(1 - win, [&](int x) {
         st += sTR[sg_slot(pb + x)];
         sp += sPD[sg_slot(pb + x)];
         sm += sMD[sg_slot(pb + x)];
-      }
+      });
 #pragma unroll
       for (int k = 0; k < SG_K; ++k) {
         const int t = tb + k;
@@ -311,7 +314,7 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
     double adx[SG_K];
     {
       double s = 0.0;
-      for (int x = 1 - win; x <= 0; ++x) s += sDX[sg_slot(pb + x)];
+      walk_window<(W > 0)>(1 - win, [&](int x) { s += sDX[sg_slot(pb + x)]; });
 #pragma unroll
       for (int k = 0; k < SG_K; ++k) {
         const int t = tb + k;
@@ -500,7 +503,8 @@ int bq_zscore(const double* close, int64_t S, int64_t T, int64_t ld_in, int32_t 
   A.win = window;
   A.inv_w = 1.0 / (double)window;
   set_vec(A, ld_in, ld_out, 1);
-  hipLaunchKernelGGL(zscore_kernel, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
+  if (window == 20) hipLaunchKernelGGL(zscore_kernel<20>, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
+  else hipLaunchKernelGGL(zscore_kernel<0>, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
@@ -522,7 +526,8 @@ int bq_adx(const double* high, const double* low, const double* close, int64_t S
   A.win = window;
   A.inv_w = 1.0 / (double)window;
   set_vec(A, ld_in, ld_out, 3);
-  hipLaunchKernelGGL(adx_kernel, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
+  if (window == 14) hipLaunchKernelGGL(adx_kernel<14>, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
+  else hipLaunchKernelGGL(adx_kernel<0>, dim3((unsigned)S), dim3(SG_NT), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
