@@ -438,4 +438,59 @@ __device__ __forceinline__ void walk_window(int lo, F&& f) {
   }
 }
 
+
+// Inverse of line_exchange (each stage is an involution: apply them in
+// reverse order).
+template <int K>
+__device__ __forceinline__ void line_unexchange(dbl2 (&p)[K / 2]) {
+  static_assert(K == 4 || K == 8, "line_unexchange: 4 or 8 candles per lane");
+  if constexpr (K == 4) {
+    swap_halves(p[0], p[1]);
+  } else {
+    swap_rows(p[0], p[1]);
+    swap_rows(p[2], p[3]);
+    swap_halves(p[0], p[2]);
+    swap_halves(p[1], p[3]);
+  }
+}
+
+// Row loads in the line-covering order: issues the lane's K/2 pieces of the
+// wave's slice (lane L: candles line_offset<K>(L) + 128 m), each load
+// instruction reading one contiguous KiB; candles >= T read as `fill`. The
+// pieces land in x (x[2m], x[2m+1]) in exchanged order: line_unexchange_x
+// turns them into the lane's K consecutive candles once they have arrived (a
+// prefetch issues the loads a tile ahead and exchanges at use). vec
+// (16-byte aligned row) is wave-uniform; every lane executes both steps.
+template <int K>
+__device__ __forceinline__ void load_pieces(const double* __restrict__ row, int tb, int T, double (&x)[K],
+                                            double fill) {
+  const int lane = __lane_id();
+  const int t = tb - K * lane + line_offset<K>(lane);
+#pragma unroll
+  for (int m = 0; m < K / 2; ++m) {
+    const int u = t + 128 * m;
+    if (u + 2 <= T) {
+      const dbl2 v = *reinterpret_cast<const dbl2*>(row + u);
+      x[2 * m] = v.x;
+      x[2 * m + 1] = v.y;
+    } else {
+      x[2 * m] = u < T ? row[u] : fill;
+      x[2 * m + 1] = fill;
+    }
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void line_unexchange_x(double (&x)[K]) {
+  dbl2 p[K / 2];
+#pragma unroll
+  for (int m = 0; m < K / 2; ++m) p[m] = dbl2{x[2 * m], x[2 * m + 1]};
+  line_unexchange<K>(p);
+#pragma unroll
+  for (int m = 0; m < K / 2; ++m) {
+    x[2 * m] = p[m].x;
+    x[2 * m + 1] = p[m].y;
+  }
+}
+
 }  // namespace bq

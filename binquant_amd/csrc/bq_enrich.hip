@@ -255,19 +255,42 @@ struct Tile {
   double ph, pl, pc;   // candle tb-1 (NaN before the series start)
 };
 
+#ifndef BQ_EN_LINELOAD
+#define BQ_EN_LINELOAD 0   // line-covering input loads (bq_device.h load_pieces): measured 0.5-1.6% slower here
+#endif
+
 __device__ __forceinline__ void load_tile(const EnrichArgs& A, int64_t row, int tb, bool vin, Tile& t) {
   const int T = A.T;
-  load4(A.in[BQ_OPEN] + row, tb, T, vin, t.o);
-  load4(A.in[BQ_HIGH] + row, tb, T, vin, t.h);
-  load4(A.in[BQ_LOW] + row, tb, T, vin, t.l);
-  load4(A.in[BQ_CLOSE] + row, tb, T, vin, t.c);
-  load4(A.in[BQ_VOLUME] + row, tb, T, vin, t.v);
+  if (BQ_EN_LINELOAD && vin) {   // wave-uniform; exchanged into place at use (tile_arrived)
+    load_pieces<EN_K>(A.in[BQ_OPEN] + row, tb, T, t.o, 0.0);
+    load_pieces<EN_K>(A.in[BQ_HIGH] + row, tb, T, t.h, 0.0);
+    load_pieces<EN_K>(A.in[BQ_LOW] + row, tb, T, t.l, 0.0);
+    load_pieces<EN_K>(A.in[BQ_CLOSE] + row, tb, T, t.c, 0.0);
+    load_pieces<EN_K>(A.in[BQ_VOLUME] + row, tb, T, t.v, 0.0);
+  } else {
+    load4(A.in[BQ_OPEN] + row, tb, T, vin, t.o);
+    load4(A.in[BQ_HIGH] + row, tb, T, vin, t.h);
+    load4(A.in[BQ_LOW] + row, tb, T, vin, t.l);
+    load4(A.in[BQ_CLOSE] + row, tb, T, vin, t.c);
+    load4(A.in[BQ_VOLUME] + row, tb, T, vin, t.v);
+  }
   if (tb >= 1 && tb <= T) {
     t.ph = A.in[BQ_HIGH][row + tb - 1];
     t.pl = A.in[BQ_LOW][row + tb - 1];
     t.pc = A.in[BQ_CLOSE][row + tb - 1];
   } else {
     t.ph = t.pl = t.pc = qnan();
+  }
+}
+
+// the prefetched tile's pieces -> each lane's EN_K consecutive candles
+__device__ __forceinline__ void tile_arrived(bool vin, Tile& t) {
+  if (BQ_EN_LINELOAD && vin) {
+    line_unexchange_x<EN_K>(t.o);
+    line_unexchange_x<EN_K>(t.h);
+    line_unexchange_x<EN_K>(t.l);
+    line_unexchange_x<EN_K>(t.c);
+    line_unexchange_x<EN_K>(t.v);
   }
 }
 
@@ -377,7 +400,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   // its first value (output[0] = x0, macd signal[0] = macd[0] = 0), and the
   // generic step from y == x leaves y unchanged, so no first-candle branch.
   if (tid == 0) {
-    const double x0 = nx.c[0];
+    const double x0 = nx.c[0];   // candle 0 in either load order (line_offset(0) == 0)
     sEcar[E_FAST] = sEcar[E_SLOW] = sEcar[E_0] = sEcar[E_1] = x0;
     sEcar[E_SIG] = 0.0;
   }
@@ -386,7 +409,8 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
     const int tb = t0 + EN_K * tid;
     const int pb = EN_H + EN_K * tid;
     const EnrichArgs& P = sA;
-    const Tile cu = nx;
+    Tile cu = nx;
+    tile_arrived(vin, cu);
     if (t0 + EN_TT < T) load_tile(A, irow, tb + EN_TT, vin, nx);   // prefetch tile n+1
 
     // ---- phase 1: per-candle quantities into the LDS ring --------------------
