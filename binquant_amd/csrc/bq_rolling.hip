@@ -630,13 +630,76 @@ __device__ __forceinline__ unsigned lane_xor(unsigned v, int ld) {
   }
 }
 
-template <int EPL, int OPL>
+// Inclusive XOR prefix of a u32 over the wave (DPP rows + readlane row
+// totals; bound_ctrl's 0 is XOR's identity).
+__device__ __forceinline__ unsigned wave_scan_xor(unsigned x, int lane) {
+  x ^= (unsigned)dpp_i32<DPP_ROW_SHR1>((int)x);
+  x ^= (unsigned)dpp_i32<DPP_ROW_SHR2>((int)x);
+  x ^= (unsigned)dpp_i32<DPP_ROW_SHR4>((int)x);
+  x ^= (unsigned)dpp_i32<DPP_ROW_SHR8>((int)x);
+  const unsigned r0 = (unsigned)__builtin_amdgcn_readlane((int)x, 15);
+  const unsigned r1 = r0 ^ (unsigned)__builtin_amdgcn_readlane((int)x, 31);
+  const unsigned r2 = r1 ^ (unsigned)__builtin_amdgcn_readlane((int)x, 47);
+  const int row = lane >> 4;
+  return x ^ (row == 0 ? 0u : (row == 1 ? r0 : (row == 2 ? r1 : r2)));
+}
+
+// index of the r-th (0-based) set bit of the NW-word mask M (r < popcount(M)):
+// the word by running popcounts, then a 16/8/4/2/1 popcount bisection in it;
+// selects only (no divergent branches)
+template <int NW>
+__device__ __forceinline__ int select_bit(const unsigned (&M)[NW], int r) {
+  unsigned word = 0;
+  int base = 0;
+  bool found = false;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const int c = __popc(M[q]);
+    const bool here = !found && r < c;
+    word = here ? M[q] : word;
+    base = here ? 32 * q : base;
+    r = (!found && !here) ? r - c : r;
+    found = found || here;
+  }
+  int p = 0;
+#pragma unroll
+  for (int h = 16; h >= 1; h >>= 1) {
+    const int c = __popc(word & ((1u << h) - 1u));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    p = up ? p + h : p;
+    word = up ? word >> h : word;
+  }
+  return base + p;
+}
+
+// SEL: instead of walking the sorted union, each lane picks its
+// ranks by bit selection. Union slot u gets the one-hot mask of its sorted
+// index; the wave's XOR prefix over u gives X(u), and the members of window
+// [m, m + w) in sorted order are the bits of X(m + w - 1) ^ X(m - 1) (slots
+// hold distinct sorted indices). NaNs sort last, so the r-th member for
+// r < n (the window's non-NaN count) is a number. Cost per wave: one scan of
+// N/32-word masks and two selections per output, instead of a walk of up to
+// N broadcast reads that every lane of the wave waits out. Measured at
+// 12.5k x 2k (tools/rank_ab.py, identical digests): 64-output tiles 0.74-0.92
+// -> 0.57-0.61 ms for every q; 128-output tiles (256 slots, 8-word masks,
+// 43 KB of LDS per block) win for central ranks (median 96: 1.30 -> 0.92 ms)
+// and lose where the walk from the nearer end is short (q = 0.92, w = 80:
+// 0.73 -> 0.95), so the host picks per job (sel_tile).
+#ifndef BQ_RANK_SEL
+#define BQ_RANK_SEL 1   // 0: never select (measurement)
+#endif
+
+template <int EPL, int OPL, bool SEL>
 __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
   constexpr int N = WAVE * EPL;          // sorted slots (power of two)
   constexpr int TILE = WAVE * OPL;       // outputs per wave
+  constexpr int NWORD = N / 32;          // words of a union-slot mask
   __shared__ unsigned long long s_key[4][N];
   __shared__ unsigned short s_pos[4][N];
   __shared__ unsigned short s_cnt[4][N + 1];   // non-NaN values before union slot u
+  __shared__ unsigned char s_idx[4][SEL ? N : 1];              // union slot -> sorted index
+  __shared__ unsigned s_X[4][SEL ? N : 1][SEL ? NWORD : 1];    // XOR prefix of the one-hot masks
   const RollJob& A = B.j[blockIdx.y];
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
   const int T = B.T, w = A.win;
@@ -720,8 +783,67 @@ __global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
   for (int e = 0; e < EPL; ++e) {
     s_key[wv][lane * EPL + e] = key[e];
     s_pos[wv][lane * EPL + e] = (unsigned short)pos[e];
+    if constexpr (SEL) s_idx[wv][pos[e]] = (unsigned char)(lane * EPL + e);
   }
   __syncthreads();
+  if constexpr (SEL) {
+    // one-hot masks of this lane's union slots, their XOR prefix in slot order
+    unsigned P[EPL][NWORD];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) {
+      const int j = s_idx[wv][lane * EPL + e];
+#pragma unroll
+      for (int q = 0; q < NWORD; ++q) {
+        const unsigned oh = (j >> 5) == q ? (1u << (j & 31)) : 0u;
+        P[e][q] = e == 0 ? oh : (P[e - 1][q] ^ oh);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NWORD; ++q) {
+      const unsigned tot = P[EPL - 1][q];
+      const unsigned excl = wave_scan_xor(tot, lane) ^ tot;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) s_X[wv][lane * EPL + e][q] = excl ^ P[e][q];
+    }
+    __syncthreads();
+    double* __restrict__ out = A.out + sym * A.ld_out;
+#pragma unroll
+    for (int o = 0; o < OPL; ++o) {
+      const int mo = o * WAVE + lane;
+      const int t = t0 + mo;
+      const int n = (int)s_cnt[wv][mo + w] - (int)s_cnt[wv][mo];
+      if (!live || t >= T) continue;
+      double r = qnan();
+      if (n >= A.minp && n > 0) {
+        unsigned M[NWORD];
+#pragma unroll
+        for (int q = 0; q < NWORD; ++q)
+          M[q] = s_X[wv][mo + w - 1][q] ^ (mo > 0 ? s_X[wv][mo - 1][q] : 0u);
+        int a;
+        bool two;
+        double frac = 0.0;
+        if (A.mode == BQ_ROLL_MEDIAN) {
+          const int h = n >> 1;
+          a = (n & 1) ? h : h - 1;
+          two = !(n & 1);
+        } else {
+          const double idxf = A.q * (double)(n - 1);
+          a = (int)idxf;
+          two = n > 1 && (double)a != idxf;
+          frac = idxf - (double)a;
+        }
+        const double lo = okey_value(s_key[wv][select_bit<NWORD>(M, a)]);
+        if (!two) r = lo;
+        else {
+          const double hi = okey_value(s_key[wv][select_bit<NWORD>(M, a + 1)]);
+          if (A.mode == BQ_ROLL_MEDIAN) r = (lo + hi) / 2.0;
+          else r = lo + (hi - lo) * frac;
+        }
+      }
+      out[t] = r;
+    }
+    return;
+  }
 
   // per output: window count n, the ranks needed, the walk targets
   const int n_num = s_cnt[wv][N];   // non-NaN values in the union (sorted first)
@@ -937,11 +1059,20 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
   hipLaunchKernelGGL(bq::rank_kernel<W>, dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
-template <int EPL, int OPL>
+template <int EPL, int OPL, bool SEL>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   const int64_t nt = (B.T + bq::WAVE * OPL - 1) / (bq::WAVE * OPL);
   const unsigned blocks = (unsigned)((B.S * nt + 3) / 4);
-  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL, SEL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+}
+
+// tile group of a job: 0 = 64-output tiles (w <= 65: union fits 128 slots),
+// bit selection; 1 / 2 = 128-output tiles with selection for central ranks /
+// the walk where the rank is near an end of the window (tile_rank_kernel)
+int tile_group(int w, int mode, double q) {
+  if (w <= 65) return 0;
+  const bool central = mode == BQ_ROLL_MEDIAN || (q >= 0.25 && q <= 0.75);
+  return BQ_RANK_SEL && central ? 1 : 2;
 }
 
 int stencil_bucket(int w) { return w <= 4 ? 0 : w <= 8 ? 1 : w <= 16 ? 2 : w <= 24 ? 3 : 4; }
@@ -1119,17 +1250,18 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     nrank[b] = 0;
     rank_items[b] = 0;
   };
-  RollBatch tile[2];
-  int ntile[2] = {0, 0};
-  for (int g = 0; g < 2; ++g) {
+  RollBatch tile[3];
+  int ntile[3] = {0, 0, 0};
+  for (int g = 0; g < 3; ++g) {
     memset(&tile[g], 0, sizeof(RollBatch));
     tile[g].S = S;
     tile[g].T = (int)T;
   }
   auto flush_tile = [&](int g) {
     if (!ntile[g]) return;
-    if (g == 0) launch_tile_rank<2, 1>(tile[g], ntile[g], st);
-    else launch_tile_rank<4, 2>(tile[g], ntile[g], st);
+    if (g == 0) launch_tile_rank<2, 1, BQ_RANK_SEL != 0>(tile[g], ntile[g], st);
+    else if (g == 1) launch_tile_rank<4, 2, true>(tile[g], ntile[g], st);
+    else launch_tile_rank<4, 2, false>(tile[g], ntile[g], st);
     ntile[g] = 0;
   };
   RollBatch sten[5];
@@ -1174,7 +1306,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       sten[b].j[nsten[b]++] = J;
       if (nsten[b] == RW_MAXJOBS) flush_sten(b);
     } else if (rank_impl(in.window, S, T) >= 1) {
-      const int g = in.window <= 65 ? 0 : 1;   // union of a 64- / 128-output tile fits 128 / 256 slots
+      const int g = tile_group(in.window, in.mode, in.q);
       tile[g].j[ntile[g]++] = J;
       if (ntile[g] == RW_MAXJOBS) flush_tile(g);
     } else {
@@ -1203,7 +1335,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   }
   flush_rep();
   for (int b = 0; b < 6; ++b) flush_rank(b);
-  for (int g = 0; g < 2; ++g) flush_tile(g);
+  for (int g = 0; g < 3; ++g) flush_tile(g);
   for (int b = 0; b < 5; ++b) flush_sten(b);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
