@@ -36,6 +36,9 @@ constexpr int MF_H = BQ_MAX_HISTORY;   // halo of the window-seeded EMA terms
 constexpr int MF_R = MF_H + MF_TT;
 constexpr int MF_HS = 32;              // halo of the short windows (ATR 14, BB 20)
 constexpr int MF_RS = MF_HS + MF_TT;
+#ifndef BQ_MF_PREFETCH
+#define BQ_MF_PREFETCH 0   // register prefetch of the next tile's inputs
+#endif
 constexpr int ATR_W = 14;   // live_market_context_accumulator.py:268
 constexpr int BB_W = 20;    // :269-270
 
@@ -71,7 +74,14 @@ __device__ __forceinline__ void mf_store(double* __restrict__ row, int tb, int T
   store_lines<MF_K>(row, tb, T, vec, x);
 }
 
-__global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int vec_in, int vec_out) {
+#ifndef BQ_MF_WPS
+#define BQ_MF_WPS 1   // __launch_bounds__ min waves per SIMD
+#endif
+// DIV: the EMAs need pandas' `/ (old_wt + new_wt)` (a non-unit sum; for the
+// reference's spans 20 / 50 the sum is exactly 1.0 and the divide is the
+// identity — checked on the host with the same IEEE arithmetic)
+template <bool DIV>
+__global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatArgs A, int vec_in, int vec_out) {
   __shared__ double sPc[MF_RS], sPt[MF_RS], sC[MF_RS];
   __shared__ double sD[2][MF_R];   // Y_e - close (EMA window identity)
   __shared__ double sX[4][MF_NW + 1];   // c, c[-2], h, l of each wave's last candle
@@ -104,14 +114,34 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
   }
   __syncthreads();
 
+#if BQ_MF_PREFETCH
+  double nh[MF_K], nl[MF_K], nc[MF_K];   // the next tile's inputs, in flight during this one
+  mf_load(rH, MF_K * tid, T, vin, nh);
+  mf_load(rL, MF_K * tid, T, vin, nl);
+  mf_load(rC, MF_K * tid, T, vin, nc);
+#endif
   for (int t0 = 0; t0 < T; t0 += MF_TT) {
     const int tb = t0 + MF_K * tid;
     const int pb = MF_H + MF_K * tid;     // position in the long-halo arrays
     const int qb = MF_HS + MF_K * tid;    // position in the short-halo arrays
     double h[MF_K], l[MF_K], c[MF_K];
+#if BQ_MF_PREFETCH
+#pragma unroll
+    for (int k = 0; k < MF_K; ++k) {
+      h[k] = nh[k];
+      l[k] = nl[k];
+      c[k] = nc[k];
+    }
+    if (t0 + MF_TT < T) {
+      mf_load(rH, tb + MF_TT, T, vin, nh);
+      mf_load(rL, tb + MF_TT, T, vin, nl);
+      mf_load(rC, tb + MF_TT, T, vin, nc);
+    }
+#else
     mf_load(rH, tb, T, vin, h);
     mf_load(rL, tb, T, vin, l);
     mf_load(rC, tb, T, vin, c);
+#endif
 
     double pc1 = __shfl_up(c[MF_K - 1], 1, WAVE);
     double pc2 = __shfl_up(c[MF_K - 2], 1, WAVE);
@@ -234,7 +264,7 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       for (int k = 0; k < MF_K; ++k) {
         const double x = c[k];
         if (tb + k == 0) y = x;
-        else if (y != x) y = (om * y + al * x) / dn;
+        else if (y != x) y = DIV ? (om * y + al * x) / dn : om * y + al * x;
         Y[e][k] = y;
         sD[e][pb + k] = y - x;
       }
@@ -243,6 +273,32 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
 
     // ---- features ----------------------------------------------------------
     double fr[MF_K], fe20[MF_K], fe50[MF_K], ftr[MF_K], fap[MF_K], fbw[MF_K];
+    // Steady state (the lane's first candle has a full 20-candle window under
+    // the history cap, so all four do): the four Bollinger windows share one pass over the 23
+    // ring values they cover — each value read once and folded into every
+    // window holding it, each window's squares still summed in ascending
+    // order — and the divisions by the window lengths are div_count (IEEE-
+    // exact): the same results as the per-candle path below.
+    const bool steady = M >= BB_W && tb >= BB_W - 1;   // (history cap >= both windows)
+    double bmid[MF_K], bacc[MF_K];
+    if (steady) {
+#pragma unroll
+      for (int k = 0; k < MF_K; ++k) {
+        bmid[k] = div_count(sPc[qb + k] - sPc[qb + k - BB_W], (double)BB_W, 1.0 / BB_W);
+        bacc[k] = 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < BB_W + MF_K - 1; ++m) {
+        const double v = sC[qb - (BB_W - 1) + m];
+#pragma unroll
+        for (int k = 0; k < MF_K; ++k) {
+          if (m - k >= 0 && m - k < BB_W) {
+            const double d = v - bmid[k];
+            bacc[k] = fma(d, d, bacc[k]);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < MF_K; ++k) {
       const int t = tb + k, p = pb + k, q = qb + k;
@@ -265,7 +321,8 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       if (lct[k] <= t - ma + 1) atr = tr[k];
       else {
         double S = sPt[q] - sPt[q - ma];
-        atr = (S < 0.0 ? 0.0 : S) / (double)ma;
+        S = S < 0.0 ? 0.0 : S;
+        atr = steady ? div_count(S, (double)ATR_W, 1.0 / ATR_W) : S / (double)ma;
       }
       // BB: rolling(20, min_periods=1) mean / std(ddof=0).fillna(0) (:269-272)
       const int mb = min(BB_W, n);
@@ -273,6 +330,9 @@ __global__ __launch_bounds__(MF_NT) void features_kernel(const FeatArgs A, int v
       if (lcc[k] <= t - mb + 1) {
         mid = cl;
         sd = 0.0;
+      } else if (steady) {
+        mid = bmid[k];
+        sd = sqrt(div_count(bacc[k], (double)BB_W, 1.0 / BB_W));
       } else {
         mid = (sPc[q] - sPc[q - mb]) / (double)mb;
         double acc = 0.0;
@@ -487,7 +547,10 @@ int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t l
   int vout = (ld_out % 2) == 0;
   for (int i = 0; i < BQ_NUM_FEATURES; ++i)
     if (feat[i]) vout &= aligned(feat[i]);
-  hipLaunchKernelGGL(features_kernel, dim3((unsigned)S), dim3(MF_NT), 0, (hipStream_t)stream, A, vin, vout);
+  if (A.den[0] != 1.0 || A.den[1] != 1.0)
+    hipLaunchKernelGGL(features_kernel<true>, dim3((unsigned)S), dim3(MF_NT), 0, (hipStream_t)stream, A, vin, vout);
+  else
+    hipLaunchKernelGGL(features_kernel<false>, dim3((unsigned)S), dim3(MF_NT), 0, (hipStream_t)stream, A, vin, vout);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
