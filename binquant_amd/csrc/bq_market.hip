@@ -143,10 +143,11 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
     mf_load(rC, tb, T, vin, c);
 #endif
 
-    double pc1 = __shfl_up(c[MF_K - 1], 1, WAVE);
-    double pc2 = __shfl_up(c[MF_K - 2], 1, WAVE);
-    double ph = __shfl_up(h[MF_K - 1], 1, WAVE);
-    double pl = __shfl_up(l[MF_K - 1], 1, WAVE);
+    // neighbour values and scans on DPP (VALU) moves; lane 0's are replaced below
+    double pc1 = dpp_f64<DPP_WAVE_SHR1>(c[MF_K - 1]);
+    double pc2 = dpp_f64<DPP_WAVE_SHR1>(c[MF_K - 2]);
+    double ph = dpp_f64<DPP_WAVE_SHR1>(h[MF_K - 1]);
+    double pl = dpp_f64<DPP_WAVE_SHR1>(l[MF_K - 1]);
     if (lane == WAVE - 1) {
       sX[0][w + 1] = c[MF_K - 1];
       sX[1][w + 1] = c[MF_K - 2];
@@ -191,13 +192,13 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
         tc = dd_add1(tc, c[k]);
         tt = dd_add1(tt, tr[k]);
       }
-      dd ic = wave_incl_scan_dd(tc, lane), it = wave_incl_scan_dd(tt, lane);
+      dd ic = wave_scan_dd_dpp(tc, lane), it = wave_scan_dd_dpp(tt, lane);
       if (lane == WAVE - 1) {
         sWh[0][w] = ic.hi; sWl[0][w] = ic.lo;
         sWh[1][w] = it.hi; sWl[1][w] = it.lo;
       }
-      double a0 = __shfl_up(ic.hi, 1, WAVE), a1 = __shfl_up(ic.lo, 1, WAVE);
-      double b0 = __shfl_up(it.hi, 1, WAVE), b1 = __shfl_up(it.lo, 1, WAVE);
+      double a0 = dpp_f64<DPP_WAVE_SHR1>(ic.hi), a1 = dpp_f64<DPP_WAVE_SHR1>(ic.lo);
+      double b0 = dpp_f64<DPP_WAVE_SHR1>(it.hi), b1 = dpp_f64<DPP_WAVE_SHR1>(it.lo);
       preC = lane == 0 ? dd{0.0, 0.0} : dd{a0, a1};
       preT = lane == 0 ? dd{0.0, 0.0} : dd{b0, b1};
     }
@@ -207,19 +208,20 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
       double y = 0.0;
 #pragma unroll
       for (int k = 0; k < MF_K; ++k) y = (tb + k == 0) ? c[k] : fma(A.lin_a[e], y, A.lin_b[e] * c[k]);
-      double inc = wave_incl_scan_affine(y, A.apow[e], lane);
+      double inc = wave_scan_affine_dpp(y, A.apow[e], lane);
       if (lane == WAVE - 1) sWe[e][w] = inc;
-      double ex = __shfl_up(inc, 1, WAVE);
+      double ex = dpp_f64<DPP_WAVE_SHR1>(inc);
       epre[e] = lane == 0 ? 0.0 : ex;
     }
     int lpc, lpt;
     {
-      int ic = wave_incl_scan_max(lcc[MF_K - 1], lane), it = wave_incl_scan_max(lct[MF_K - 1], lane);
+      // indices >= -1: scanned as index + 1 so DPP's zero fill is the identity
+      int ic = wave_scan_max_dpp(lcc[MF_K - 1] + 1, lane) - 1, it = wave_scan_max_dpp(lct[MF_K - 1] + 1, lane) - 1;
       if (lane == WAVE - 1) {
         sWlc[0][w] = ic;
         sWlc[1][w] = it;
       }
-      int a = __shfl_up(ic, 1, WAVE), b = __shfl_up(it, 1, WAVE);
+      int a = dpp_i32<DPP_WAVE_SHR1>(ic + 1) - 1, b = dpp_i32<DPP_WAVE_SHR1>(it + 1) - 1;
       lpc = lane == 0 ? -1 : a;
       lpt = lane == 0 ? -1 : b;
     }
