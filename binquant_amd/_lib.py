@@ -154,6 +154,7 @@ class BqRollJob(ctypes.Structure):
         ("mode", ctypes.c_int32),
         ("q", ctypes.c_double),
         ("alpha", ctypes.c_double),
+        ("rows", ctypes.c_int64),
     ]
 
 

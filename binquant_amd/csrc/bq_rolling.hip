@@ -68,6 +68,7 @@ struct RollJob {
   int64_t ld_in, ld_out;
   int win, minp, shift, mode, seg, nseg;
   double q, alpha;
+  int64_t rows;   // this job's rows (<= the batch's S; a benchmark row beside a panel)
 };
 
 struct RollBatch {
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
   const int RL = ring * RP_CT;
   const int lane = threadIdx.x;
   const int64_t sym0 = (int64_t)blockIdx.x * WAVE;
-  const int64_t S = B.S;
+  const int64_t S = A.rows;
+  if (sym0 >= S) return;   // the block is one wave: a uniform exit
   const int T = B.T, w = A.win, sh = A.shift;
   const bool welford = A.mode >= BQ_ROLL_VAR;
   const bool live = sym0 + lane < S;
@@ -369,7 +371,8 @@ __device__ __forceinline__ void replay_restage_body(const RollJob& A, const Roll
   constexpr bool welford = CLS == 2;
   const int lane = threadIdx.x;
   const int64_t sym0 = (int64_t)blockIdx.x * SPW;
-  const int64_t S = B.S;
+  const int64_t S = A.rows;
+  if (sym0 >= S) return;   // the block is one wave: a uniform exit
   const int T = B.T, w = A.win, sh = A.shift;
   const int64_t rows = S - sym0 < SPW ? S - sym0 : SPW;
   const int nbytes = (int)(rows * A.ld_out * (int64_t)sizeof(double));
@@ -492,6 +495,57 @@ __global__ __launch_bounds__(WAVE, BQ_RS_WPS_MIXED) void replay_mixed_kernel(con
     case 1: replay_restage_body<1, SPW, V>(A, B, s_in, s_out); break;
     case 2: replay_restage_body<2, SPW, V>(A, B, s_in, s_out); break;
     default: replay_restage_body<3, SPW, V>(A, B, s_in, s_out);
+  }
+}
+
+// ---- forward fill as a scan (x.ffill(): exact copies, any order) -------------------
+// One 256-thread block per (row, job) walks tiles of 1024 candles (4 per
+// lane): the last valid index before each lane comes from a block max-scan
+// (DPP within the wave, wave totals through LDS), its value from the tile in
+// LDS or the carry of the previous tiles; each lane then fills its 4 candles.
+// A fill only copies values, so the result equals the sequential replay bit
+// for bit — at 16 B per candle instead of a 2000-step walk per lane (the
+// replay's cost for T = 2000 is ~0.5 ms whatever the row count).
+constexpr int FF_NT = 256, FF_K = 4, FF_TT = FF_NT * FF_K;
+
+__global__ __launch_bounds__(FF_NT) void ffill_kernel(const RollBatch B, int vec) {
+  __shared__ double sv[FF_TT];
+  __shared__ int sW[FF_NT / WAVE];
+  __shared__ double sCar;
+  const RollJob& A = B.j[blockIdx.y];
+  const int64_t sym = blockIdx.x;
+  if (sym >= A.rows) return;   // the whole block: no barrier is left waiting
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const double* __restrict__ x = A.x + sym * A.ld_in;
+  double* __restrict__ out = A.out + sym * A.ld_out;
+  const int T = B.T;
+  if (tid == 0) sCar = qnan();   // leading NaNs stay
+  for (int t0 = 0; t0 < T; t0 += FF_TT) {
+    const int tb = t0 + FF_K * tid;
+    double v[FF_K];
+#pragma unroll
+    for (int k = 0; k < FF_K; ++k) v[k] = tb + k < T ? x[tb + k] : qnan();
+    int li = -1;
+#pragma unroll
+    for (int k = 0; k < FF_K; ++k) {
+      if (v[k] == v[k]) li = tb + k;
+      sv[FF_K * tid + k] = v[k];
+    }
+    const int inc = wave_scan_max_dpp(li + 1, lane) - 1;   // indices >= -1
+    if (lane == WAVE - 1) sW[w] = inc;
+    int p = dpp_i32<DPP_WAVE_SHR1>(inc + 1) - 1;           // lane 0 -> -1
+    __syncthreads();   // the tile, the wave totals and the carry are visible
+    for (int u = 0; u < w; ++u) p = max(p, sW[u]);
+    double cur = p >= t0 ? sv[p - t0] : sCar;
+    double o[FF_K];
+#pragma unroll
+    for (int k = 0; k < FF_K; ++k) {
+      cur = v[k] == v[k] ? v[k] : cur;
+      o[k] = cur;
+    }
+    store_lines<FF_K>(out, tb, T, vec != 0, o);
+    __syncthreads();   // every read of sv / sW / sCar of this tile is done
+    if (tid == FF_NT - 1) sCar = cur;
   }
 }
 
@@ -1038,10 +1092,18 @@ __global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) 
 
 namespace {
 
-bool job_ok(const bq_roll_job& j, int64_t T) {
+bool job_ok(const bq_roll_job& j, int64_t S, int64_t T) {
   if (!j.x || !j.out || j.ld_in < T || j.ld_out < T || j.min_periods < 0) return false;
   // replay results leave through 32-bit buffer offsets over 64 rows
   if (j.ld_out > BQ_MAX_ROLL_LD) return false;
+  // a job's own row count (a benchmark row beside the panel): the lane-per-row
+  // kernels (moments, ewm) and the fill honour it; order statistics and the
+  // integer sums walk the batch's S rows
+  if (j.rows < 0 || j.rows > S) return false;
+  const bool own_rows = j.rows != 0 && j.rows != S;
+  if (own_rows && j.mode != BQ_ROLL_EWM && j.mode != BQ_ROLL_FFILL &&
+      !(j.mode >= BQ_ROLL_MEAN && j.mode <= BQ_ROLL_STD0))
+    return false;
   if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
   if (j.mode == BQ_ROLL_FFILL) return j.shift == 0;
   return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
@@ -1179,7 +1241,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   using namespace bq;
   if (!jobs || n_jobs < 0 || S < 0 || T < 0 || T > 0x7fffffff) return BQ_EINVAL;
   for (int i = 0; i < n_jobs; ++i)
-    if (!job_ok(jobs[i], T)) return BQ_EINVAL;
+    if (!job_ok(jobs[i], S, T)) return BQ_EINVAL;
   if (S == 0 || T == 0 || n_jobs == 0) return BQ_OK;
   hipStream_t st = (hipStream_t)stream;
   // replay jobs (moments, ewm): lane = symbol; rank jobs grouped by window size
@@ -1264,6 +1326,19 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     else launch_tile_rank<4, 2, false>(tile[g], ntile[g], st);
     ntile[g] = 0;
   };
+  RollBatch ff;
+  memset(&ff, 0, sizeof(ff));
+  ff.S = S;
+  ff.T = (int)T;
+  int nff = 0;
+  auto flush_ff = [&]() {
+    if (!nff) return;
+    int vec = 1;   // 16-byte output rows: whole-line stores
+    for (int i = 0; i < nff; ++i)
+      vec &= (ff.j[i].ld_out % 2) == 0 && (((uintptr_t)ff.j[i].out) & 15u) == 0;
+    hipLaunchKernelGGL(ffill_kernel, dim3((unsigned)S, (unsigned)nff), dim3(FF_NT), 0, st, ff, vec);
+    nff = 0;
+  };
   RollBatch sten[5];
   int nsten[5] = {0, 0, 0, 0, 0};
   for (int b = 0; b < 5; ++b) {
@@ -1290,6 +1365,12 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     J.mode = in.mode;
     J.q = in.q;
     J.alpha = in.alpha;
+    J.rows = in.rows > 0 ? in.rows : S;
+    if (J.mode == BQ_ROLL_FFILL) {   // a scan, not a replay (ffill_kernel)
+      ff.j[nff++] = J;
+      if (nff == RW_MAXJOBS) flush_ff();
+      continue;
+    }
     if (in.mode == BQ_ROLL_ISUM && (in.window > 32 || S * ((T + SR_NT - 1) / SR_NT) > 0x7fffffff))
       J.mode = BQ_ROLL_SUM;   // long window: the replay (identical values for integer series)
     if (J.mode == BQ_ROLL_ISUM) {   // integer-valued sum: a direct window sum, stencil launch
@@ -1334,6 +1415,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     }
   }
   flush_rep();
+  flush_ff();
   for (int b = 0; b < 6; ++b) flush_rank(b);
   for (int g = 0; g < 3; ++g) flush_tile(g);
   for (int b = 0; b < 5; ++b) flush_sten(b);

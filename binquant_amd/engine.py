@@ -547,21 +547,31 @@ class Ffill:
 
 @device_entry
 def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
-    """Independent Roll / Ewm series over one [S, T] shape in as few launches
-    as the kernel families allow (bq_rolling_batch): the lane-per-symbol
-    replays of different series run side by side instead of one launch each."""
+    """Independent Roll / Ewm / Ffill series over one [S, T] shape in as few
+    launches as the kernel families allow (bq_rolling_batch): the
+    lane-per-symbol replays of different series run side by side instead of
+    one launch each. A moment / ewm / ffill series may have fewer rows than
+    the panel (e.g. the [1, T] benchmark beside an [S, T] panel): it joins
+    the same launch (bq_roll_job.rows) instead of paying a replay walk of
+    its own."""
     if not specs:
         return []
-    x0 = _check_panel(specs[0].x, "x")
-    S, T = x0.shape
+    xs = [_check_panel(sp.x, "x") for sp in specs]
+    S = max(int(x.shape[0]) for x in xs)
+    T = int(xs[0].shape[1])
     outs: list[torch.Tensor] = []
     jobs = []
     keep = []
-    for sp in specs:
-        x = _check_panel(sp.x, "x", (S, T))
-        out = torch.empty((S, T), dtype=torch.float64, device=x.device)
+    for sp, x in zip(specs, xs):
+        rows = int(x.shape[0])
+        if x.shape[1] != T:
+            raise ValueError(f"x: shape {tuple(x.shape)}: every series of a batch needs T = {T}")
+        if rows != S and isinstance(sp, Roll) and sp.stat not in ("mean", "sum", "var", "std", "var0", "std0"):
+            raise ValueError(f"x: shape {tuple(x.shape)} != {(S, T)} (only moments, ewm and ffill may have fewer rows)")
+        out = torch.empty((rows, T), dtype=torch.float64, device=x.device)
         j = _lib.BqRollJob()
         j.x, j.out, j.ld_in, j.ld_out = x.data_ptr(), out.data_ptr(), _row_stride(x), T
+        j.rows = rows if rows != S else 0
         if isinstance(sp, Ffill):
             j.mode = _lib.ROLL_FFILL
         elif isinstance(sp, Ewm):

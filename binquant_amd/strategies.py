@@ -155,12 +155,12 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -
     prev = F.shift(C, 1)
     tr = F.run({"tr": F.fmax(F.fmax(H - L, (H - prev).abs()), (L - prev).abs())})["tr"]   # max(axis=1) skips NaN
     bench = btc_close.reshape(1, -1).contiguous()
-    atr, vmean, hmax, lmin, e20, e50, cf = engine.rolling_many(
+    # the benchmark's [1, T] series ride in the panel's batch (one launch)
+    atr, vmean, hmax, lmin, e20, e50, cf, bf, be20, be50 = engine.rolling_many(
         E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
         R(h, p.compression_bars, "max", shift=1), R(l, p.compression_bars, "min", shift=1),
-        E(c, span=20), E(c, span=50), FF(c),
+        E(c, span=20), E(c, span=50), FF(c), FF(bench), E(bench, span=20), E(bench, span=50),
     )
-    bf, be20, be50 = engine.rolling_many(FF(bench), E(bench, span=20), E(bench, span=50))
     e: dict[str, object] = {}
     e["candidate_atr"] = atr
     m3 = pct_change_filled(cf, p.momentum_bars)

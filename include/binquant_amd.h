@@ -262,6 +262,10 @@ typedef struct bq_roll_job {
   int32_t window, min_periods, shift, mode;   /* mode: bq_roll_mode            */
   double q;                /* quantile                                         */
   double alpha;            /* BQ_ROLL_EWM                                      */
+  int64_t rows;            /* rows of this job's x / out, 1 <= rows <= S (a    */
+                           /* benchmark series beside the panel); 0 = all S.  */
+                           /* Moments / ewm / ffill only: order statistics    */
+                           /* need 0 or S.                                     */
 } bq_roll_job;
 int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream);
 
