@@ -307,6 +307,9 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
 #ifndef BQ_RS_WPS
 #define BQ_RS_WPS 2   // min waves per SIMD (register cap) of the re-staging replays
 #endif
+#ifndef BQ_RS_LPT
+#define BQ_RS_LPT 1   // mixed replay batches ordered longest class first
+#endif
 #ifndef BQ_RS_WPS_MIXED
 #define BQ_RS_WPS_MIXED 2   // the all-classes kernel
 #endif
@@ -1291,6 +1294,17 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       for (int c = 0; c < 4; ++c)
         if (ncls[c]) launch_restage_any(c, cls[c], ncls[c], st);
     } else if (impl == 2) {
+      // longest first: blocks start in blockIdx order (x, then the job), so
+      // the costliest replays (Welford, ~3x a Kahan step) go to the front of
+      // the grid instead of starting in its tail (outputs are per job)
+      if (BQ_RS_LPT) {
+        RollJob sorted[RW_MAXJOBS];
+        int n = 0;
+        for (int c : {2, 1, 0, 3})
+          for (int i = 0; i < nrep; ++i)
+            if (replay_class(rep.j[i].mode) == c) sorted[n++] = rep.j[i];
+        for (int i = 0; i < nrep; ++i) rep.j[i] = sorted[i];
+      }
       launch_restage_any(4, rep, nrep, st);
     } else {
       hipLaunchKernelGGL(replay_kernel, dim3((unsigned)((S + WAVE - 1) / WAVE), (unsigned)nrep), dim3(WAVE), lds, st,
