@@ -44,6 +44,22 @@ __device__ __forceinline__ int lower_bound_i64(const int64_t* __restrict__ ts, i
   return lo;
 }
 
+// lower_bound with a guess first: on a regular grid (the kline rows) the
+// index of key is (key - ts[0]) / step with step = (ts[n-1] - ts[0]) / (n - 1);
+// the guess is taken only when ts[g-1] < key <= ts[g] holds, so the result is
+// lower_bound's for any row (a gap or an irregular row falls back to the
+// binary search): two loads instead of ~11 dependent ones per search.
+__device__ __forceinline__ int lower_bound_guess(const int64_t* __restrict__ ts, int n, int64_t key, int64_t t0v,
+                                                 int64_t step) {
+  if (step > 0) {
+    int64_t g = key <= t0v ? 0 : (key - t0v + step - 1) / step;
+    g = g > n ? n : g;
+    const bool ok = (g == 0 || ts[g - 1] < key) && (g == n || ts[g] >= key);
+    if (ok) return (int)g;
+  }
+  return lower_bound_i64(ts, n, key);
+}
+
 __device__ __forceinline__ int row_len(const int64_t* lens, int64_t s, int T) {
   if (!lens) return T;
   const int64_t n = lens[s];
@@ -95,8 +111,10 @@ __global__ __launch_bounds__(256) void resample_kernel(const ResampleArgs A) {
   row_bins(ts, n, A.I, origin, b0, nb);
   if (b >= nb) return;
   const int64_t key = origin + (b0 + b) * A.I;
-  const int lo = lower_bound_i64(ts, n, key);
-  const int hi = lower_bound_i64(ts, n, key + A.I);
+  const int64_t t0v = ts[0], span = ts[n - 1] - t0v;   // n >= 1 here (nb > b >= 0)
+  const int64_t step = n > 1 && span > 0 && span % (n - 1) == 0 ? span / (n - 1) : 0;
+  const int lo = lower_bound_guess(ts, n, key, t0v, step);
+  const int hi = lower_bound_guess(ts, n, key + A.I, t0v, step);
   if (A.out_ts) A.out_ts[s * A.ld_out + b] = key;
   for (int f = 0; f < A.nf; ++f) {
     const double* __restrict__ x = A.in[f] + s * A.ld_in;
