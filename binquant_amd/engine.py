@@ -593,6 +593,13 @@ def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.
         outs.append(out)
         keep.append(x)
     L = _lib.load()
+    # a batch call takes MAX_ROLL_JOBS jobs: the sequential replays (moments,
+    # ewm — one latency-bound launch per call, whatever its job count) go
+    # into the calls first, so 14 replays + 4 order statistics make one replay
+    # launch instead of a second one for the replays that spilled into the
+    # next call (outputs stay in spec order: each job carries its own pointer)
+    _REPLAY = (_lib.ROLL_EWM,) + tuple(_lib.ROLL_MODES[k] for k in ("mean", "sum", "var", "std", "var0", "std0"))
+    jobs = sorted(jobs, key=lambda j: 0 if j.mode in _REPLAY else 1)
     for i in range(0, len(jobs), _lib.MAX_ROLL_JOBS):
         chunk = jobs[i : i + _lib.MAX_ROLL_JOBS]
         arr = (_lib.BqRollJob * len(chunk))(*chunk)
