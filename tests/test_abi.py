@@ -62,6 +62,36 @@ def test_invalid_arguments_rejected_without_device():
     assert lib.bq_state_create(ctypes.byref(h), 0, None) == _lib.BQ_EINVAL
 
 
+def test_roll_job_rows_validated_without_device():
+    """bq_roll_job.rows: a job's own row count must lie in [0, S], and only the
+    lane-per-row kernels (moments, ewm, ffill) take one below S — the
+    validation runs before any HIP call (fake, never dereferenced pointers)."""
+    from binquant_amd import _lib
+
+    lib = _lib.load()
+    null = ctypes.c_void_p()
+    assert ctypes.sizeof(_lib.BqRollJob) == 72   # the header's bq_roll_job
+
+    def job(mode, rows, **kw):
+        j = _lib.BqRollJob()
+        j.x, j.out, j.ld_in, j.ld_out = 0x1000, 0x2000, 100, 100
+        j.window, j.min_periods, j.mode, j.rows = 5, 5, mode, rows
+        for k, v in kw.items():
+            setattr(j, k, v)
+        return j
+
+    def call(*jobs, S=8):
+        arr = (_lib.BqRollJob * len(jobs))(*jobs)
+        return lib.bq_rolling_batch(arr, len(jobs), S, 100, null)
+
+    median = _lib.ROLL_MODES["median"]
+    assert call(job(median, 3)) == _lib.BQ_EINVAL                     # order statistics: all S rows
+    assert call(job(_lib.ROLL_MODES["isum"], 3)) == _lib.BQ_EINVAL
+    assert call(job(_lib.ROLL_MODES["mean"], 9)) == _lib.BQ_EINVAL     # rows > S
+    assert call(job(_lib.ROLL_MODES["mean"], -1)) == _lib.BQ_EINVAL
+    assert call(job(_lib.ROLL_EWM, 1, alpha=0.0)) == _lib.BQ_EINVAL    # alpha still checked
+
+
 def test_missing_library_fails_loudly(tmp_path):
     from binquant_amd import _lib
 
