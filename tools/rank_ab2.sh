@@ -6,8 +6,8 @@ mkdir -p gpurun_out/rk2
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_rolling_impls_gpu.py tests/test_strategies_gpu.py -m gpu > gpurun_out/rk2/tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/rk2/tests.log; exit 1; }
 tail -1 gpurun_out/rk2/tests.log
 for rep in 1 2; do
-  BQ_RANK_IMPL=tile timeout -k 10 300 python3 tools/rank_ab.py > gpurun_out/rk2/new_$rep.jsonl || exit 1
-  BQ_LIB_PATH=$PWD/$BQ_AB_LIB BQ_RANK_IMPL=tile timeout -k 10 300 python3 tools/rank_ab.py > gpurun_out/rk2/old_$rep.jsonl || exit 1
+  BQ_RANK_IMPL=${IMPL:-tile} timeout -k 10 300 python3 tools/rank_ab.py > gpurun_out/rk2/new_$rep.jsonl || exit 1
+  BQ_LIB_PATH=$PWD/$BQ_AB_LIB BQ_RANK_IMPL=${IMPL:-tile} timeout -k 10 300 python3 tools/rank_ab.py > gpurun_out/rk2/old_$rep.jsonl || exit 1
 done
 python3 - <<'PY'
 import json
