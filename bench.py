@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--no-rows", action="store_true")
     ap.add_argument("--row-symbols", type=int, default=12_500)
     ap.add_argument("--row-candles", type=int, default=2_000)
-    ap.add_argument("--store-ticks", type=int, default=50)
+    ap.add_argument("--store-ticks", type=int, default=300)
     ap.add_argument("--live-symbols", type=int, default=1000)
     return ap.parse_args()
 
@@ -420,7 +420,7 @@ def bench_store(args, dev):
     del hist, slots, tsh
     lat = []
     vol = np.ones(S)
-    for k in range(args.store_ticks + 5):
+    for k in range(args.store_ticks + 20):   # 20 untimed warm-up ticks
         ts = t0 + 900_000 * (M + k)
         price *= np.exp(rng.normal(0, 0.002, S))
         c = price
@@ -428,7 +428,7 @@ def bench_store(args, dev):
         a = time.perf_counter()
         ctx = acc.on_closed_candles(syms, np.full(S, ts), c, c * 1.001, c * 0.999, c, vol, at=ts)
         torch.cuda.synchronize()
-        if k >= 5:
+        if k >= 20:
             lat.append(time.perf_counter() - a)
     sl = store.fresh_slots(ts)
     fms = _time_call(lambda: store.features(sl), reps=5)
