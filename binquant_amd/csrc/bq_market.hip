@@ -36,6 +36,19 @@ constexpr int MF_H = BQ_MAX_HISTORY;   // halo of the window-seeded EMA terms
 constexpr int MF_R = MF_H + MF_TT;
 constexpr int MF_HS = 32;              // halo of the short windows (ATR 14, BB 20)
 constexpr int MF_RS = MF_HS + MF_TT;
+#ifndef BQ_MF_LDSPERM
+#define BQ_MF_LDSPERM 1   // lane-interleaved short-halo arrays (as bq_enrich's LX)
+#endif
+// slot of short-halo ring position i: lanes own 4 consecutive positions, so
+// in the natural layout the 64 lanes of a wave touch slots 4 doubles apart (a
+// 4-way bank conflict on every access); position i at (i % 4) * (RS / 4) +
+// i / 4 puts the lanes' k-th candles side by side. qb is a multiple of 4, so
+// for a constant offset x the slot of qb + x is (qb / 4) + a constant.
+#if BQ_MF_LDSPERM
+#define FX(i) (((((i) & 3)) * (MF_RS / 4)) + ((i) >> 2))
+#else
+#define FX(i) (i)
+#endif
 #ifndef BQ_MF_PREFETCH
 #define BQ_MF_PREFETCH 0   // register prefetch of the next tile's inputs
 #endif
@@ -108,9 +121,9 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
     sD[1][i] = qnan();
   }
   if (tid < MF_HS) {
-    sPc[tid] = 0.0;
-    sPt[tid] = 0.0;
-    sC[tid] = qnan();
+    sPc[FX(tid)] = 0.0;
+    sPt[FX(tid)] = 0.0;
+    sC[FX(tid)] = qnan();
   }
   __syncthreads();
 
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
       sX[3][w + 1] = l[MF_K - 1];
     }
 #pragma unroll
-    for (int k = 0; k < MF_K; ++k) sC[qb + k] = c[k];
+    for (int k = 0; k < MF_K; ++k) sC[FX(qb + k)] = c[k];
     __syncthreads();   // B1
     if (lane == 0) {
       pc1 = sX[0][w];
@@ -239,8 +252,8 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
       for (int k = 0; k < MF_K; ++k) {
         bc = dd_add1(bc, c[k]);
         bt = dd_add1(bt, tr[k]);
-        sPc[qb + k] = dd_round(bc);
-        sPt[qb + k] = dd_round(bt);
+        sPc[FX(qb + k)] = dd_round(bc);
+        sPt[FX(qb + k)] = dd_round(bt);
       }
       int cc = sLcar[0], ct = sLcar[1];
       for (int u = 0; u < w; ++u) {
@@ -286,12 +299,12 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
     if (steady) {
 #pragma unroll
       for (int k = 0; k < MF_K; ++k) {
-        bmid[k] = div_count(sPc[qb + k] - sPc[qb + k - BB_W], (double)BB_W, 1.0 / BB_W);
+        bmid[k] = div_count(sPc[FX(qb + k)] - sPc[FX(qb + k - BB_W)], (double)BB_W, 1.0 / BB_W);
         bacc[k] = 0.0;
       }
 #pragma unroll
       for (int m = 0; m < BB_W + MF_K - 1; ++m) {
-        const double v = sC[qb - (BB_W - 1) + m];
+        const double v = sC[FX(qb - (BB_W - 1) + m)];
 #pragma unroll
         for (int k = 0; k < MF_K; ++k) {
           if (m - k >= 0 && m - k < BB_W) {
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
       double atr;
       if (lct[k] <= t - ma + 1) atr = tr[k];
       else {
-        double S = sPt[q] - sPt[q - ma];
+        double S = sPt[FX(q)] - sPt[FX(q - ma)];
         S = S < 0.0 ? 0.0 : S;
         atr = steady ? div_count(S, (double)ATR_W, 1.0 / ATR_W) : S / (double)ma;
       }
@@ -336,18 +349,18 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
         mid = bmid[k];
         sd = sqrt(div_count(bacc[k], (double)BB_W, 1.0 / BB_W));
       } else {
-        mid = (sPc[q] - sPc[q - mb]) / (double)mb;
+        mid = (sPc[FX(q)] - sPc[FX(q - mb)]) / (double)mb;
         double acc = 0.0;
         if (mb == BB_W) {   // every candle past the warm-up: a compile-time walk,
                             // all 20 ring reads issued ahead of the sum (same order)
 #pragma unroll
           for (int j = 1 - BB_W; j <= 0; ++j) {
-            const double d = sC[q + j] - mid;
+            const double d = sC[FX(q + j)] - mid;
             acc = fma(d, d, acc);
           }
         } else {
           for (int i = q - mb + 1; i <= q; ++i) {
-            const double d = sC[i] - mid;
+            const double d = sC[FX(i)] - mid;
             acc = fma(d, d, acc);
           }
         }
@@ -377,9 +390,9 @@ __global__ __launch_bounds__(MF_NT, BQ_MF_WPS) void features_kernel(const FeatAr
     }
     if (tid < MF_HS) {   // short halos; prefixes re-based to the tile end
       const int src = MF_TT + tid;
-      sPc[tid] = sPc[src] - sPc[MF_RS - 1];
-      sPt[tid] = sPt[src] - sPt[MF_RS - 1];
-      sC[tid] = sC[src];
+      sPc[FX(tid)] = sPc[FX(src)] - sPc[FX(MF_RS - 1)];
+      sPt[FX(tid)] = sPt[FX(src)] - sPt[FX(MF_RS - 1)];
+      sC[FX(tid)] = sC[FX(src)];
     }
     if (tid < 4) sX[tid][0] = sX[tid][MF_NW];
     if (tid == MF_NT - 1) {
