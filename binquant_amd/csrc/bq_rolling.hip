@@ -1061,6 +1061,24 @@ __global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) 
     A.out[sym * A.ld_out + t] = r;
     return;
   }
+  if (A.mode == BQ_ROLL_QUANTILE && (A.q == 1.0 || A.q == 0.0)) {
+    // rolling max / min (q = 1 / 0: rank n - 1 / 0): the extreme of the
+    // window's numbers, which is what the network leaves in that slot (its
+    // fmin / fmax order -0 below +0 the same way) — w - 1 comparisons
+    // instead of the sort
+    const bool hi = A.q == 1.0;
+    double e = hi ? -__builtin_inf() : __builtin_inf();
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double a = s[threadIdx.x + j];
+      const bool num = j < w && a == a;
+      n += num ? 1 : 0;
+      e = num ? (hi ? fmax(e, a) : fmin(e, a)) : e;
+    }
+    A.out[sym * A.ld_out + t] = (n >= A.minp && n > 0) ? e : qnan();
+    return;
+  }
   double v[N];
   int n = 0;
 #pragma unroll
