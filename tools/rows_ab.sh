@@ -3,7 +3,7 @@
 # Usage: bash tools/rows_ab.sh lib.so ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-for lib in "$@"; do
+for lib in binquant_amd/lib/libbinquant_amd.so "$@"; do
   BQ_LIB_PATH=$PWD/$lib timeout -k 10 300 python -m pytest -x -q tests/test_rolling_impls_gpu.py tests/test_strategies_gpu.py tests/test_panel_fixtures_gpu.py -m gpu > gpurun_out/ab_test.log 2>&1 || { echo "TESTFAIL $lib"; tail -20 gpurun_out/ab_test.log; exit 1; }
   echo "parity ok $lib"
 done
