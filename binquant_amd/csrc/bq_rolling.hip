@@ -747,21 +747,26 @@ __device__ __forceinline__ int select_bit(const unsigned (&M)[NW], int r) {
 #define BQ_RANK_SEL 1   // 0: never select (measurement)
 #endif
 
+#ifndef BQ_TR_WPB
+#define BQ_TR_WPB 1   // waves per block of the tile rank kernel
+#endif
 template <int EPL, int OPL, bool SEL>
-__global__ __launch_bounds__(256) void tile_rank_kernel(const RollBatch B) {
+__global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBatch B) {
   constexpr int N = WAVE * EPL;          // sorted slots (power of two)
   constexpr int TILE = WAVE * OPL;       // outputs per wave
   constexpr int NWORD = N / 32;          // words of a union-slot mask
-  __shared__ unsigned long long s_key[4][N];
-  __shared__ unsigned short s_pos[4][N];
-  __shared__ unsigned short s_cnt[4][N + 1];   // non-NaN values before union slot u
-  __shared__ unsigned char s_idx[4][SEL ? N : 1];              // union slot -> sorted index
-  __shared__ unsigned s_X[4][SEL ? N : 1][SEL ? NWORD : 1];    // XOR prefix of the one-hot masks
+  // one wave per block (BQ_TR_WPB = 1): the waves share no LDS, so a block
+  // barrier would only make independent tiles wait for each other
+  __shared__ unsigned long long s_key[BQ_TR_WPB][N];
+  __shared__ unsigned short s_pos[BQ_TR_WPB][N];
+  __shared__ unsigned short s_cnt[BQ_TR_WPB][N + 1];   // non-NaN values before union slot u
+  __shared__ unsigned char s_idx[BQ_TR_WPB][SEL ? N : 1];              // union slot -> sorted index
+  __shared__ unsigned s_X[BQ_TR_WPB][SEL ? N : 1][SEL ? NWORD : 1];    // XOR prefix of the one-hot masks
   const RollJob& A = B.j[blockIdx.y];
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
   const int T = B.T, w = A.win;
   const int64_t nt = (T + TILE - 1) / TILE;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t tile = (int64_t)blockIdx.x * BQ_TR_WPB + wv;
   const bool live = tile < B.S * nt;   // every wave reaches the barriers
   const int64_t sym = live ? tile / nt : 0;
   const int t0 = live ? (int)(tile % nt) * TILE : 0;
@@ -1145,8 +1150,9 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
 template <int EPL, int OPL, bool SEL>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   const int64_t nt = (B.T + bq::WAVE * OPL - 1) / (bq::WAVE * OPL);
-  const unsigned blocks = (unsigned)((B.S * nt + 3) / 4);
-  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL, SEL>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+  const unsigned blocks = (unsigned)((B.S * nt + BQ_TR_WPB - 1) / BQ_TR_WPB);
+  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL, SEL>), dim3(blocks, (unsigned)n), dim3(64 * BQ_TR_WPB), 0, st,
+                     B);
 }
 
 // tile group of a job: 0 = 64-output tiles (w <= 65: union fits 128 slots),
