@@ -110,3 +110,22 @@ def test_time_parallel_helpers_match_exact_replay(cuda, T):
         for c in cuts:
             far = np.abs(w - c) > 1e-9 * np.maximum(np.abs(w), 1.0)
             np.testing.assert_array_equal((g > c)[far], (w > c)[far], err_msg=f"{name} cut {c}")
+
+
+@pytest.mark.parametrize("T", [700, 2049])
+def test_time_parallel_helpers_other_windows(cuda, T):
+    """The kernels are instantiated for the reference's windows (z-score 20,
+    ADX 14: the window walks unrolled at compile time); any other window takes
+    the generic instantiation — checked here against the exact replay."""
+    from binquant_amd import signals
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(70, T, seed0=T + 1)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    for w in (10, 33):
+        g = signals.adx(d["high"], d["low"], d["close"], window=w).cpu().numpy()
+        e = signals.adx(d["high"], d["low"], d["close"], window=w, exact=True).cpu().numpy()
+        assert_close(g, e, f"adx{w}", rtol=1e-9, scale=100.0)
+        g = signals.zscore(d["close"], window=w).cpu().numpy()
+        e = signals.zscore(d["close"], window=w, exact=True).cpu().numpy()
+        assert_close_or_exact(g, e, p["close"], w, indicators_ref.exact_zscore, f"zscore{w}", scale=1.0)
