@@ -24,8 +24,11 @@
 // pandas' rules are kept: constant windows (rolling mean returns the value,
 // var returns 0), min_periods warm-up NaN, the helpers' fillna / where.
 //
-// Input contract: finite prices (the diff's NaN at candle 0 is handled); a
-// row with missing candles goes through the exact path (signals.*(exact=True)).
+// Missing candles (NaN) follow pandas' rules: z-score / ADX lanes whose
+// sliding sums a NaN entered re-sum their windows directly (finite again once
+// the gap leaves the window); the Wilder RSI row is replayed serially with
+// pandas' ewm update from the first tile holding a non-finite close (gap
+// decay, observation count, a late first observation).
 #include "bq_device.h"
 #include "binquant_amd.h"
 
@@ -172,6 +175,32 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
         }
         z[k] = v;
       }
+      // A missing candle (NaN) that entered the sliding sums poisons the
+      // lane's later outputs, although pandas' windows that no longer hold it
+      // are finite again (rolling(w, min_periods=w) is NaN only while the
+      // window holds the gap: z = 0 there). Such lanes re-sum every window
+      // directly, about a reference inside it.
+      if (s1 != s1 || s2 != s2) {
+#pragma unroll
+        for (int k = 0; k < SG_K; ++k) {
+          const int t = tb + k;
+          double v = 0.0;
+          const double rk = c[k];
+          if (t >= win - 1 && lcl[k] > t - win + 1 && rk == rk) {
+            double a1 = 0.0, a2 = 0.0;
+            for (int x = 1 - win; x <= 0; ++x) {
+              const double d = sC[sg_slot(pb + k + x)] - rk;
+              a1 += d;
+              a2 = fma(d, d, a2);
+            }
+            const double var = (a2 - a1 * a1 * A.inv_w) * A.inv_w;
+            const double sd = var > 0.0 ? sqrt(var) : 0.0;
+            const double mean = rk + a1 * A.inv_w;
+            if (sd > 0.0 && sd == sd) v = (c[k] - mean) / sd;
+          }
+          z[k] = v;
+        }
+      }
     }
     sg_store(ro, tb, T, A.vout, z);
     if (t0 + SG_TT >= T) break;
@@ -270,18 +299,10 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
         sp += sPD[sg_slot(pb + x)];
         sm += sMD[sg_slot(pb + x)];
       });
-#pragma unroll
-      for (int k = 0; k < SG_K; ++k) {
+      auto dx_of =[&](int k, double a, double p, double m) {
         const int t = tb + k;
-        if (k > 0) {
-          const int o = sg_slot(pb + k - win);
-          st = (st + tr[k]) - sTR[o];
-          sp = (sp + pd[k]) - sPD[o];
-          sm = (sm + md[k]) - sMD[o];
-        }
         double v = 0.0;
         if (t >= win - 1) {
-          double a = st, p = sp, m = sm;
           if (ltr[k] <= t - win + 1) {   // constant window: value * nobs
             a = tr[k] * (double)win;
             p = pd[k] * (double)win;
@@ -292,9 +313,39 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
           v = tot != 0.0 ? 100.0 * fabs(pdi - mdi) / tot : qnan();
           if (v != v) v = 0.0;
         }
-        dx[k] = v;
-        sDX[sg_slot(pb + k)] = v;
+        return v;
+      };
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) {
+        if (k > 0) {
+          const int o = sg_slot(pb + k - win);
+          st = (st + tr[k]) - sTR[o];
+          sp = (sp + pd[k]) - sPD[o];
+          sm = (sm + md[k]) - sMD[o];
+        }
+        dx[k] = dx_of(k, st, sp, sm);
       }
+      // a true range that is NaN (a missing high / low / previous close the
+      // skip-NaN max cannot cover) poisons the sliding sum for the lane's later
+      // candles, whereas pandas' rolling sum is finite again once the window no
+      // longer holds it: re-sum those lanes' windows directly
+      if (st != st) {
+#pragma unroll
+        for (int k = 0; k < SG_K; ++k) {
+          double a = 0.0, p = 0.0, m = 0.0;
+          if (tb + k >= win - 1) {
+            for (int x = 1 - win; x <= 0; ++x) {
+              const int o = sg_slot(pb + k + x);
+              a += sTR[o];
+              p += sPD[o];
+              m += sMD[o];
+            }
+          }
+          dx[k] = dx_of(k, a, p, m);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) sDX[sg_slot(pb + k)] = dx[k];
     }
     __syncthreads();   // dx of every lane visible
     int ldx[SG_K];
@@ -365,6 +416,7 @@ template <bool DIV>
 __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
   __shared__ double sA[SG_NW], sB[2][SG_NW];
   __shared__ double sCarry[2];
+  __shared__ double sX[SG_TT];   // the serial replay's tile (rows with missing candles)
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const int64_t sym = blockIdx.x;
   const double* __restrict__ rc = A.in[0] + sym * A.ld_in;
@@ -373,6 +425,11 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
   // the scan's per-candle map: y -> la * y + lb * x (la = om / den, lb = alpha / den)
   const double la = A.om / A.den, lb = A.alpha / A.den;
   if (tid < 2) sCarry[tid] = 0.0;
+  // pandas' ewm state (thread 0) once the row turns serial: averages, old
+  // weight, observation count, previous close
+  bool serial = false;
+  double wg = qnan(), wl = qnan(), owt = 1.0, prev = qnan();
+  int nobs = 0;
   double nx[SG_K];
   sg_load(rc, SG_K * tid, T, A.vin, nx);
   for (int t0 = 0; t0 < T; t0 += SG_TT) {
@@ -382,6 +439,75 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
     for (int k = 0; k < SG_K; ++k) c[k] = nx[k];
     const double pc0 = tb >= 1 && tb <= T ? rc[tb - 1] : qnan();
     if (t0 + SG_TT < T) sg_load(rc, tb + SG_TT, T, A.vin, nx);
+    // A missing (NaN) or infinite close breaks the scan's fixed per-candle
+    // map: pandas' ewm(ignore_na=False) decays the old weight across a gap
+    // and divides by (old_wt + alpha), counts only observations toward
+    // min_periods and starts at the first observation wherever it is. From
+    // the first tile holding one, the row is replayed serially with pandas'
+    // own update (thread 0; the carry so far seeds it) — exact, and only the
+    // rows with gaps pay for it.
+    {
+      int bad = 0;
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) bad |= (tb + k < T) && !(c[k] - c[k] == 0.0);
+      if (__syncthreads_or(bad) && !serial) {
+        serial = true;
+        if (t0 > 0) {   // candles 1 .. t0 - 1 were all observations
+          wg = sCarry[0];
+          wl = sCarry[1];
+          nobs = t0 - 1;
+          prev = rc[t0 - 1];
+        }
+      }
+    }
+    if (serial) {
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) sX[SG_K * tid + k] = c[k];
+      __syncthreads();
+      if (tid == 0) {
+        const int n = min(SG_TT, T - t0);
+        for (int i = 0; i < n; ++i) {
+          const double cur = sX[i];
+          const double d = cur - prev;
+          prev = cur;
+          const double g = d != d ? d : (d > 0.0 ? d : 0.0);
+          const double l = d != d ? d : (d < 0.0 ? -d : 0.0);
+          const bool obs = g == g;
+          nobs += obs ? 1 : 0;
+          if (wg == wg) {
+            owt *= A.om;
+            if (obs) {
+              if (wg != g) {
+                wg = owt * wg + A.alpha * g;
+                wg /= owt + A.alpha;
+              }
+              if (wl != l) {
+                wl = owt * wl + A.alpha * l;
+                wl /= owt + A.alpha;
+              }
+              owt = 1.0;
+            }
+          } else if (obs) {
+            wg = g;
+            wl = l;
+          }
+          double v = qnan();
+          if (nobs >= A.win) {
+            const double den = wg + wl;
+            v = den != 0.0 ? (100.0 * wg) / den : 50.0;
+          }
+          sX[i] = v;
+        }
+      }
+      __syncthreads();
+      double rsi[SG_K];
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) rsi[k] = sX[SG_K * tid + k];
+      sg_store(ro, tb, T, A.vout, rsi);
+      if (t0 + SG_TT >= T) break;
+      __syncthreads();
+      continue;
+    }
     double g[SG_K], l[SG_K];
     {
       double pc = pc0;
@@ -544,8 +670,9 @@ int bq_wilder_rsi(const double* close, int64_t S, int64_t T, int64_t ld_in, int3
   A.ld_out = ld_out;
   A.T = (int)T;
   A.win = window;
-  // pandas: ewm(alpha = 1 / w): old_wt_factor = 1 - alpha, new_wt = alpha
-  A.alpha = 1.0 / (double)window;
+  // pandas: ewm(alpha = 1 / w) keeps com = 1 / alpha - 1 and recomputes
+  // alpha = 1 / (1 + com); old_wt_factor = 1 - alpha, new_wt = alpha
+  A.alpha = 1.0 / (1.0 + (1.0 / (1.0 / (double)window) - 1.0));
   A.om = 1.0 - A.alpha;
   A.den = A.om + A.alpha;
   set_vec(A, ld_in, ld_out, 1);

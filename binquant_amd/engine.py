@@ -134,8 +134,12 @@ def launch_scope(device: torch.device | None, stream: torch.cuda.Stream | None, 
         with torch.cuda.device(device):
             yield
         return
-    if device is not None and stream.device != device:
-        raise ValueError(f"stream is on {stream.device}, operands on {device}")
+    if device is not None:
+        # torch.device("cuda") (index None) means the current device
+        want = device.index if device.index is not None else torch.cuda.current_device()
+        have = stream.device.index if stream.device.index is not None else torch.cuda.current_device()
+        if want != have:
+            raise ValueError(f"stream is on {stream.device}, operands on {device}")
     with torch.cuda.device(stream.device):
         stream.wait_stream(torch.cuda.current_stream(stream.device))
         for t in tensors:

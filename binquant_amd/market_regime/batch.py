@@ -74,14 +74,17 @@ def reduce_partials(part: torch.Tensor, n_local: int, group=None) -> tuple[torch
     rank the partials are returned with column 9 = n_local."""
     part[:, TRACKED_COLUMN] = float(n_local)
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        if part.is_cuda and dist.get_backend(group) == "gloo":   # CPU rehearsal of the RCCL path
-            host = part.cpu()
+        # no timestamps (T == 0, the same on every rank): the count alone travels,
+        # so every rank still agrees on the admission gate's total
+        buf = part if part.shape[0] else torch.full((1, part.shape[1]), float(n_local), dtype=part.dtype,
+                                                    device=part.device)
+        if buf.is_cuda and dist.get_backend(group) == "gloo":   # CPU rehearsal of the RCCL path
+            host = buf.cpu()
             dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-            part.copy_(host)
+            buf.copy_(host)
         else:   # RCCL over xGMI
-            dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
-        n_total = int(part[0, TRACKED_COLUMN].item()) if part.shape[0] else int(n_local)
-        return part, n_total
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        return part, int(buf[0, TRACKED_COLUMN].item())
     return part, int(n_local)
 
 

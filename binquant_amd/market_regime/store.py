@@ -228,6 +228,9 @@ class DeviceMarketStateStore:
         v.head, v.count, v.last = head.data_ptr(), count.data_ptr(), last.data_ptr()
         v.capacity, v.max_bars = cap, M
         self._view = v
+        # every (re)allocation is a new generation: anything that baked the
+        # ring pointers in (the live context's hipGraph) keys on it
+        self.generation = getattr(self, "generation", -1) + 1
 
     def _slot(self, symbol: str) -> int:
         s = self._slots.get(symbol)
@@ -524,7 +527,7 @@ class DeviceLiveMarketContextAccumulator:
         store = self.state_store
         btc_slot = store.slot_of(self.btc_symbol)
         btc_counted = btc_slot is not None and (not self._sharded() or dist.get_rank(self.group) == 0)
-        key = (store.n_tracked, store._view.ts, btc_slot, btc_counted)
+        key = (store.n_tracked, store.generation, btc_slot, btc_counted)
         b = getattr(self, "_ctx_bufs", None)
         if b is None or b.key != key:
             tracked = store.n_tracked - (0 if btc_counted or btc_slot is None else 1)

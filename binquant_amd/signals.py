@@ -23,6 +23,9 @@ bq_signals.hip (one launch each, 1e-9 of pandas); exact=True runs the
 replay composition instead — the bq_rolling / bq_ewm kernels plus fused
 element-wise programs (binquant_amd.fused) in the reference's operation
 order, equal to pandas bit for bit. The other helpers use that composition.
+Rows with missing candles (NaN) keep pandas' NaN rules on the fast kernels
+too (bq_signals.hip: z-score / ADX re-sum the windows a gap touched; the
+Wilder RSI row is replayed with pandas' own ewm update from the first gap).
 There is no CPU path.
 """
 

@@ -106,6 +106,35 @@ def test_two_rank_breadth_equals_reference(label):
             assert g[k] == pytest.approx(want[k], rel=1e-11, abs=1e-13), k
 
 
+def _empty_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from binquant_amd.market_regime.batch import reduce_partials
+
+        part, n = reduce_partials(torch.zeros((0, 10), dtype=torch.float64), 5 + rank)
+        q.put((rank, n, tuple(part.shape)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduce_partials_without_timestamps_agrees_on_total():
+    """a [0, 10] partial (no timestamps) still yields the total
+    tracked count over all ranks, the same on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_empty_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(n for _, n, _ in res) == [18, 18, 18]
+    assert all(shape == (0, 10) for _, _, shape in res)
+
+
 def test_shard_bounds_cover_exactly():
     from binquant_amd.market_regime.batch import shard_bounds
 

@@ -112,6 +112,57 @@ def test_time_parallel_helpers_match_exact_replay(cuda, T):
             np.testing.assert_array_equal((g > c)[far], (w > c)[far], err_msg=f"{name} cut {c}")
 
 
+def _gap_panel(S: int, T: int, seed: int):
+    """numpy_panel rows with missing candles (all fields NaN): single gaps,
+    a 5-candle gap, a late listing (leading NaN), gaps at the 2048-candle tile
+    boundary, a gap in the first window, a row that is all NaN, and a NaN high
+    with a valid low (the true range's skip-NaN max covers it)."""
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(S, T, seed0=seed)
+    rng = np.random.default_rng(seed)
+    gaps = {0: [300], 1: list(range(500, 505)), 2: list(range(0, 150)), 3: [2047, 2048] if T > 2048 else [T - 2],
+            4: [5], 5: list(range(T)), 6: [int(x) for x in rng.integers(1, T, 12)], 7: [1, 2, 3],
+            8: list(range(0, 20)) + [600]}
+    for r, ts in gaps.items():
+        for k in ("open", "high", "low", "close", "volume"):
+            p[k][r, ts] = np.nan
+    p["high"][9, [40, 41, 900 % T]] = np.nan
+    return p
+
+
+@pytest.mark.parametrize("T", [700, 2049, 4100])
+def test_time_parallel_helpers_missing_candles(cuda, T):
+    """the time-parallel kernels on rows with missing candles
+    (NaN gaps, late listings) follow pandas' NaN rules — Wilder RSI against
+    pandas' own ewm(adjust=False, ignore_na=False, min_periods) on every row,
+    all three against the bit-exact replay composition."""
+    import pandas as pd
+
+    from binquant_amd import signals
+
+    p = _gap_panel(70, T, seed=T + 7)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    rsi = signals.wilder_rsi(d["close"]).cpu().numpy()
+    for r in range(12):
+        delta = pd.Series(p["close"][r]).diff()
+        ag = delta.clip(lower=0).ewm(alpha=1 / 14, min_periods=14, adjust=False).mean()
+        al = (-delta.clip(upper=0)).ewm(alpha=1 / 14, min_periods=14, adjust=False).mean()
+        den = ag + al
+        want = (100 * ag / den).where(den != 0, 50.0).to_numpy()
+        assert_close(rsi[r], want, f"rsi row {r}", rtol=1e-9, scale=100.0)
+    for name, fast, exact in (
+        ("rsi", rsi, signals.wilder_rsi(d["close"], exact=True).cpu().numpy()),
+        ("adx", signals.adx(d["high"], d["low"], d["close"]).cpu().numpy(),
+         signals.adx(d["high"], d["low"], d["close"], exact=True).cpu().numpy()),
+        ("zscore", signals.zscore(d["close"]).cpu().numpy(), signals.zscore(d["close"], exact=True).cpu().numpy()),
+    ):
+        if name == "zscore":
+            assert_close_or_exact(fast, exact, p["close"], 20, indicators_ref.exact_zscore, name, scale=1.0)
+        else:
+            assert_close(fast, exact, name, rtol=1e-9, scale=100.0)
+
+
 @pytest.mark.parametrize("T", [700, 2049])
 def test_time_parallel_helpers_other_windows(cuda, T):
     """The kernels are instantiated for the reference's windows (z-score 20,
