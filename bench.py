@@ -254,31 +254,53 @@ def bench_tick(args, dev):
     }
 
 
+CONTEXT_BYTES_PER_CANDLE = 3 * 8   # C5: high, low, close read once; the [T x 10] partials are O(T)
+
+
 def bench_breadth(args, panel, world, dev):
-    """C5 leg: features -> partials -> ONE all-reduce(sum) of the [T x 10]
-    partials (tracked-symbol count folded into the spare column;
-    market_regime.batch.reduce_partials, RCCL over xGMI at N > 1)."""
+    """C5 leg: the fused panel context build (bq_context_partials: features
+    reduced straight into the [T x 10] partials, the feature columns never
+    written) -> ONE all-reduce(sum) of the partials (tracked-symbol count
+    folded into the spare column; market_regime.batch.reduce_partials, RCCL
+    over xGMI at N > 1). Roofline on the algorithmic bytes: 3 fp64 inputs
+    per candle (the group records the kernels exchange are intermediate);
+    the unfused features + breadth_partial pair is timed beside it."""
     h, l, c = panel["high"], panel["low"], panel["close"]
     S, T = c.shape
-    feats = engine.market_features(h, l, c, max_bars=400)
-    part = engine.breadth_partial(c, feats)
+    part, _ = engine.context_partials(h, l, c, max_bars=400)
     steps = max(1, args.breadth_steps)
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier(world)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        engine.market_features(h, l, c, max_bars=400, out=feats)
-        engine.breadth_partial(c, feats, out=part)
+    for i in range(steps):
+        evs[i][0].record(stream)
+        engine.context_partials(h, l, c, max_bars=400, out=part)
+        evs[i][1].record(stream)
         _, n_total = reduce_partials(part, S)
     barrier(world)
     dt = max_over_ranks(time.perf_counter() - t0, world) / steps
-    del feats
+    kern_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world)
+    achieved = S * T * CONTEXT_BYTES_PER_CANDLE / (kern_ms * 1e-3) / 1e9
+    # the unfused pair (what round 2 ran): features written, re-read by breadth_partial
+    feats = engine.market_features(h, l, c, max_bars=400)
+    up = engine.breadth_partial(c, feats)
+    unfused_ms = _time_call(lambda: (engine.market_features(h, l, c, max_bars=400, out=feats),
+                                     engine.breadth_partial(c, feats, out=up)), reps=2)
+    del feats, up
+    traffic, traffic_src = pmc_traffic("context_partials", S * T)
     return {
         "value": n_total * T / dt,
         "unit": "symbol-candles/s",
         "ms_per_step": dt * 1e3,
         "tracked_symbols": n_total,
-        "workload": f"{S} symbols x {T} candles per GPU, max_bars 400, features + partials"
+        "workload": f"{S} symbols x {T} candles per GPU, max_bars 400, fused features -> partials"
         + (" + one RCCL all_reduce of [T x 10] fp64" if world > 1 else ""),
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "bq_context_partials (3 launches)", "kernel_ms": kern_ms,
+                     "algorithmic_bytes_per_candle": CONTEXT_BYTES_PER_CANDLE, "candles_per_launch": S * T},
+        "unfused_ms": unfused_ms,
     }
 
 

@@ -1,0 +1,595 @@
+// Fused market-context partials for gfx950 (BASELINE configs[4], C5):
+// _compute_symbol_features at every timestamp of a [S][T] panel under the
+// MarketStateStore history cap, reduced straight into the per-timestamp
+// breadth partials of _build_context without materialising the six feature
+// columns (market_regime/live_market_context_accumulator.py:95-163, 244-297).
+//
+// bq_market_features + bq_breadth_partial write 48 B of features per candle
+// and read 56 B back; the panel context build needs only the [T][10]
+// partials (plus, optionally, the features of the last timestamp). Here:
+//
+// pass 1  context_partials_kernel: one WAVE per symbol (4 symbols per
+//         workgroup), tiles of 256 candles (4 per lane). The features are
+//         those of bq_market.hip's features_kernel, reorganised for a wave:
+//         * scans (double-double prefixes of close and true range, the EMA
+//           affine maps, the pandas same-value run starts) are wave scans on
+//           DPP with tile carries held in registers — no workgroup barrier;
+//         * the history-capped EMA uses the exact window identity
+//             y_t = Y_t - a^(M-1) (Y_s - c_s),  s = t - M + 1,
+//           with Y_s from a second, lagged EMA chain over c[t - M + 1] (a
+//           re-read that hits L2 / MALL: the row was streamed M - 1 candles
+//           earlier) instead of an LDS ring of M values per symbol;
+//         * the 4 symbols' contributions at each t are summed in the
+//           workgroup in a fixed order, (s0 + s1) + (s2 + s3), through LDS,
+//           and written as one group record per t: 4 fp64 sums + the 5
+//           counts packed in 16 bits (34 B per 4 candles).
+// pass 2  context_group_reduce_kernel: lane = timestamp, the group records
+//         of a chunk of groups summed in a fixed order -> [chunk][T][9];
+// pass 3  context_chunk_reduce_kernel: the chunks in order -> [T][10].
+//
+// No atomics: the result is bitwise reproducible run to run.
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+#include <string.h>
+
+namespace bq {
+
+constexpr int CX_NW = 4;                // waves = symbols per workgroup = per group record
+constexpr int CX_NT = CX_NW * WAVE;
+constexpr int CX_K = 4;                 // candles per lane
+constexpr int CX_TT = WAVE * CX_K;      // 256-candle wave tile
+constexpr int CX_HS = 20;               // short-window halo (BB 20, ATR 14)
+constexpr int CX_RS = CX_HS + CX_TT;    // 276
+constexpr int CX_Q = CX_RS / CX_K;
+static_assert(CX_HS % CX_K == 0 && CX_RS % CX_K == 0, "ring shape");
+// ring position i -> LDS slot, lane-interleaved (the lanes' k-th candles side
+// by side: conflict-free; qb = CX_HS + 4 lane is a multiple of 4)
+#define CXS(i) ((((i) & (CX_K - 1)) * CX_Q) + ((i) >> 2))
+constexpr int CX_ATR = 14;   // live_market_context_accumulator.py:268
+constexpr int CX_BB = 20;    // :269-270
+
+// packed group counts: 3 bits per field (<= 4 symbols per group)
+constexpr int CNT_VALID = 0, CNT_ADV = 3, CNT_DEC = 6, CNT_A20 = 9, CNT_A50 = 12;
+
+struct CtxArgs {
+  const double* h;
+  const double* l;
+  const double* c;
+  int64_t S, ld_in;
+  int T, M;
+  int vin;
+  double alpha[2], om[2], den[2], lin_a[2], lin_b[2];
+  double apow[2][8];   // lin_a^(4 * 2^j)
+  double corr[2];      // lin_a^(M - 1)
+  double* gsum[4];     // group sums [ngrp][ld_g]: return, trend, atr_pct, bb_width
+  uint16_t* gcnt;      // packed counts [ngrp][ld_g]
+  int64_t ld_g;
+  double* last[BQ_NUM_FEATURES];   // optional features at t = T - 1, [S] each
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void cx_load(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[CX_K]) {
+  if (vec && tb + CX_K <= T) {
+    const double2* p = reinterpret_cast<const double2*>(row + tb);
+    const double2 a = p[0], b = p[1];
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = b.x;
+    x[3] = b.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) x[k] = (tb + k < T) ? row[tb + k] : 0.0;
+  }
+}
+
+// DIV: pandas' EMA divide by (old_wt + new_wt) is needed (not exactly 1.0)
+template <bool DIV>
+__global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArgs A) {
+  __shared__ double sPc[CX_NW][CX_RS], sPt[CX_NW][CX_RS], sC[CX_NW][CX_RS];
+  __shared__ double sR[3][4][CX_TT];   // reduction slots: 4 sums, index k * 64 + lane
+  __shared__ uint16_t sN[3][CX_TT];
+
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int64_t grp = blockIdx.x;
+  const int64_t sym = grp * CX_NW + w;
+  const bool live = sym < A.S;                  // wave-uniform
+  const int64_t row = live ? sym : A.S - 1;     // idle waves walk a valid row, contribute nothing
+  const int T = A.T, M = A.M;
+  const double* __restrict__ rH = A.h + row * A.ld_in;
+  const double* __restrict__ rL = A.l + row * A.ld_in;
+  const double* __restrict__ rC = A.c + row * A.ld_in;
+  double* __restrict__ pc = sPc[w];
+  double* __restrict__ pt = sPt[w];
+  double* __restrict__ cr = sC[w];
+  const bool vin = A.vin != 0;
+
+  if (lane < CX_HS) {
+    pc[CXS(lane)] = 0.0;
+    pt[CXS(lane)] = 0.0;
+    cr[CXS(lane)] = qnan();
+  }
+  // tile carries (wave-uniform): candle t0 - 1 (and close t0 - 2), run starts, EMA states
+  double c1c = qnan(), c2c = qnan(), hc = qnan(), lc = qnan();
+  int rcC = -1, rtC = -1;
+  double ecar[2] = {0.0, 0.0}, lcar[2] = {0.0, 0.0};
+  wave_sync();
+
+  for (int t0 = 0; t0 < T; t0 += CX_TT) {
+    const int tb = t0 + CX_K * lane, qb = CX_HS + CX_K * lane;
+    double h[CX_K], l[CX_K], c[CX_K], xl[CX_K];
+    cx_load(rH, tb, T, vin, h);
+    cx_load(rL, tb, T, vin, l);
+    cx_load(rC, tb, T, vin, c);
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) {   // lagged closes c[t - M + 1] (0 before the row starts)
+      const int s = tb + k - (M - 1);
+      xl[k] = (s >= 0 && s < T) ? rC[s] : 0.0;
+    }
+
+    double p1 = dpp_f64<DPP_WAVE_SHR1>(c[CX_K - 1]);
+    double p2 = dpp_f64<DPP_WAVE_SHR1>(c[CX_K - 2]);
+    double ph = dpp_f64<DPP_WAVE_SHR1>(h[CX_K - 1]);
+    double pl = dpp_f64<DPP_WAVE_SHR1>(l[CX_K - 1]);
+    if (lane == 0) {
+      p1 = c1c;
+      p2 = c2c;
+      ph = hc;
+      pl = lc;
+    }
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) cr[CXS(qb + k)] = c[k];
+
+    double tr[CX_K];
+    int lcc[CX_K], lct[CX_K];
+    {
+      double pcv = p1, ptr = true_range(ph, pl, p2), cp = p1;
+      int rc = -1, rt = -1;
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        const int t = tb + k;
+        tr[k] = true_range(h[k], l[k], cp);
+        if (t == 0 || c[k] != pcv) rc = t;
+        if (t == 0 || tr[k] != ptr) rt = t;
+        lcc[k] = rc;
+        lct[k] = rt;
+        pcv = c[k];
+        ptr = tr[k];
+        cp = c[k];
+      }
+    }
+    // prefix sums of close and true range (double-double, rounded once)
+    {
+      dd tc = {0.0, 0.0}, tt = {0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        tc = dd_add1(tc, c[k]);
+        tt = dd_add1(tt, tr[k]);
+      }
+      const dd ic = wave_scan_dd_dpp(tc, lane), it = wave_scan_dd_dpp(tt, lane);
+      const double a0 = dpp_f64<DPP_WAVE_SHR1>(ic.hi), a1 = dpp_f64<DPP_WAVE_SHR1>(ic.lo);
+      const double b0 = dpp_f64<DPP_WAVE_SHR1>(it.hi), b1 = dpp_f64<DPP_WAVE_SHR1>(it.lo);
+      dd bc = lane == 0 ? dd{0.0, 0.0} : dd{a0, a1};
+      dd bt = lane == 0 ? dd{0.0, 0.0} : dd{b0, b1};
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        bc = dd_add1(bc, c[k]);
+        bt = dd_add1(bt, tr[k]);
+        pc[CXS(qb + k)] = dd_round(bc);
+        pt[CXS(qb + k)] = dd_round(bt);
+      }
+    }
+    // run starts: exclusive wave max (+1 so DPP's zero fill is the identity) and the tile carry
+    {
+      const int ic = wave_scan_max_dpp(lcc[CX_K - 1] + 1, lane) - 1;
+      const int it = wave_scan_max_dpp(lct[CX_K - 1] + 1, lane) - 1;
+      const int a = dpp_i32<DPP_WAVE_SHR1>(ic + 1) - 1, b = dpp_i32<DPP_WAVE_SHR1>(it + 1) - 1;
+      const int ec = max(lane == 0 ? -1 : a, rcC), et = max(lane == 0 ? -1 : b, rtC);
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        lcc[k] = max(lcc[k], ec);
+        lct[k] = max(lct[k], et);
+      }
+    }
+    // EMA 20 / 50: full-history Y (candle 0 starts it) and the lagged chain
+    // Y_s at s = t - M + 1 (candle 0 starts it M - 1 candles later), each an
+    // affine wave scan + the exact pandas replay of the lane's 4 steps
+    double Y[2][CX_K], D[2][CX_K];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const double al = A.alpha[e], om = A.om[e], dn = A.den[e];
+      {
+        double y = 0.0;
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) y = (tb + k == 0) ? c[k] : fma(A.lin_a[e], y, A.lin_b[e] * c[k]);
+        const double inc = wave_scan_affine_dpp(y, A.apow[e], lane);
+        const double ex = dpp_f64<DPP_WAVE_SHR1>(inc);
+        double v = lane == 0 ? ecar[e] : fma(pow_bits<6>(A.apow[e], lane), ecar[e], ex);
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+          const double x = c[k];
+          if (tb + k == 0) v = x;
+          else if (v != x) v = DIV ? (om * v + al * x) / dn : om * v + al * x;
+          Y[e][k] = v;
+        }
+        ecar[e] = readlane_f64(v, WAVE - 1);
+      }
+      {
+        const int s0 = tb - (M - 1);
+        double y = 0.0;
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) y = (s0 + k == 0) ? xl[k] : fma(A.lin_a[e], y, A.lin_b[e] * xl[k]);
+        const double inc = wave_scan_affine_dpp(y, A.apow[e], lane);
+        const double ex = dpp_f64<DPP_WAVE_SHR1>(inc);
+        double v = lane == 0 ? lcar[e] : fma(pow_bits<6>(A.apow[e], lane), lcar[e], ex);
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+          const int s = s0 + k;
+          const double x = xl[k];
+          if (s == 0) v = x;
+          else if (s > 0 && v != x) v = DIV ? (om * v + al * x) / dn : om * v + al * x;
+          D[e][k] = v - x;
+        }
+        lcar[e] = readlane_f64(v, WAVE - 1);
+      }
+    }
+    wave_sync();   // the rings (close, prefixes) of every lane are visible
+
+    // ---- features (bq_market.hip features_kernel, same operations) -----------
+    double fr[CX_K], fe20[CX_K], fe50[CX_K], ftr[CX_K], fap[CX_K], fbw[CX_K];
+    const bool steady = M >= CX_BB && tb >= CX_BB - 1;
+    double bmid[CX_K], bacc[CX_K];
+    if (steady) {
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        bmid[k] = div_count(pc[CXS(qb + k)] - pc[CXS(qb + k - CX_BB)], (double)CX_BB, 1.0 / CX_BB);
+        bacc[k] = 0.0;
+      }
+#pragma unroll
+      for (int m = 0; m < CX_BB + CX_K - 1; ++m) {
+        const double v = cr[CXS(qb - (CX_BB - 1) + m)];
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+          if (m - k >= 0 && m - k < CX_BB) {
+            const double d = v - bmid[k];
+            bacc[k] = fma(d, d, bacc[k]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) {
+      const int t = tb + k, q = qb + k;
+      const int n = min(t + 1, M);
+      if (n < 2) {   // history.empty or len < 2 -> None (:248-249)
+        fr[k] = fe20[k] = fe50[k] = ftr[k] = fap[k] = fbw[k] = qnan();
+        continue;
+      }
+      const double cl = c[k];
+      const double prev = k > 0 ? c[k - 1] : p1;
+      double e20 = Y[0][k], e50 = Y[1][k];
+      if (t + 1 > M) {   // the history window starts at s = t - M + 1 > 0
+        e20 = e20 - A.corr[0] * D[0][k];
+        e50 = e50 - A.corr[1] * D[1][k];
+      }
+      const int ma = min(CX_ATR, n);
+      double atr;
+      if (lct[k] <= t - ma + 1) atr = tr[k];
+      else {
+        double Sx = pt[CXS(q)] - pt[CXS(q - ma)];
+        Sx = Sx < 0.0 ? 0.0 : Sx;
+        atr = steady ? div_count(Sx, (double)CX_ATR, 1.0 / CX_ATR) : Sx / (double)ma;
+      }
+      const int mb = min(CX_BB, n);
+      double mid, sd;
+      if (lcc[k] <= t - mb + 1) {
+        mid = cl;
+        sd = 0.0;
+      } else if (steady) {
+        mid = bmid[k];
+        sd = sqrt(div_count(bacc[k], (double)CX_BB, 1.0 / CX_BB));
+      } else {
+        mid = (pc[CXS(q)] - pc[CXS(q - mb)]) / (double)mb;
+        double acc = 0.0;
+        for (int i = q - mb + 1; i <= q; ++i) {
+          const double d = cr[CXS(i)] - mid;
+          acc = fma(d, d, acc);
+        }
+        sd = sqrt(acc / (double)mb);
+      }
+      const double up = mid + (2.0 * sd), lo = mid - (2.0 * sd);
+      fr[k] = safe_pct(cl, prev);
+      fe20[k] = e20;
+      fe50[k] = e50;
+      ftr[k] = e50 != 0.0 ? (e20 - e50) / fabs(e50) : 0.0;
+      fap[k] = cl != 0.0 ? atr / cl : 0.0;
+      fbw[k] = mid != 0.0 ? (up - lo) / fabs(mid) : 0.0;
+    }
+    // the last timestamp's feature row, when asked (the context's symbol_features)
+    if (live && tb <= T - 1 && T - 1 < tb + CX_K) {
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        if (tb + k != T - 1) continue;
+        const double v[BQ_NUM_FEATURES] = {fr[k], fe20[k], fe50[k], ftr[k], fap[k], fbw[k]};
+#pragma unroll
+        for (int f = 0; f < BQ_NUM_FEATURES; ++f)
+          if (A.last[f]) A.last[f][sym] = v[f];
+      }
+    }
+
+    // ---- this symbol's contributions, then the group's (fixed order) --------
+    double cs[4][CX_K];
+    unsigned cn[CX_K];
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) {
+      const double r = fr[k];
+      const bool ok = live && tb + k < T && r == r;   // no features at t: nothing counted
+      cn[k] = ok ? ((1u << CNT_VALID) | ((r > 0.0 ? 1u : 0u) << CNT_ADV) | ((r < 0.0 ? 1u : 0u) << CNT_DEC) |
+                    ((c[k] > fe20[k] ? 1u : 0u) << CNT_A20) | ((c[k] > fe50[k] ? 1u : 0u) << CNT_A50))
+                 : 0u;
+      cs[0][k] = ok ? r : 0.0;
+      cs[1][k] = ok ? ftr[k] : 0.0;
+      cs[2][k] = ok ? fap[k] : 0.0;
+      cs[3][k] = ok ? fbw[k] : 0.0;
+    }
+    if (w & 1) {   // waves 1, 3 -> slots 0, 1
+      const int sl = w >> 1;
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) sR[sl][f][k * WAVE + lane] = cs[f][k];
+        sN[sl][k * WAVE + lane] = (uint16_t)cn[k];
+      }
+    }
+    __syncthreads();
+    if (!(w & 1)) {   // wave 0: s0 + s1, wave 2: s2 + s3
+      const int sl = w >> 1;
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) cs[f][k] = cs[f][k] + sR[sl][f][k * WAVE + lane];
+        cn[k] += sN[sl][k * WAVE + lane];
+      }
+      if (w == 2) {
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f) sR[2][f][k * WAVE + lane] = cs[f][k];
+          sN[2][k * WAVE + lane] = (uint16_t)cn[k];
+        }
+      }
+    }
+    __syncthreads();
+    if (w == 0) {   // (s0 + s1) + (s2 + s3) -> the group record at t
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) cs[f][k] = cs[f][k] + sR[2][f][k * WAVE + lane];
+        cn[k] += sN[2][k * WAVE + lane];
+      }
+      const int64_t orow = grp * A.ld_g;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) store_lines<CX_K>(A.gsum[f] + orow, tb, T, true, cs[f]);
+      uint16_t* gc = A.gcnt + orow;
+      if (tb + CX_K <= T) {
+        const uint64_t packed = (uint64_t)cn[0] | ((uint64_t)cn[1] << 16) | ((uint64_t)cn[2] << 32) |
+                                ((uint64_t)cn[3] << 48);
+        __builtin_nontemporal_store(packed, reinterpret_cast<uint64_t*>(gc + tb));
+      } else {
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k)
+          if (tb + k < T) gc[tb + k] = (uint16_t)cn[k];
+      }
+    }
+
+    if (t0 + CX_TT >= T) break;
+    wave_sync();   // every lane's reads of this tile's rings are done
+    if (lane < CX_HS) {   // short halos; prefixes re-based to the tile end
+      const int src = CX_TT + lane;
+      const double bc = pc[CXS(CX_RS - 1)], bt = pt[CXS(CX_RS - 1)];
+      pc[CXS(lane)] = pc[CXS(src)] - bc;
+      pt[CXS(lane)] = pt[CXS(src)] - bt;
+      cr[CXS(lane)] = cr[CXS(src)];
+    }
+    wave_sync();
+    c1c = readlane_f64(c[CX_K - 1], WAVE - 1);
+    c2c = readlane_f64(c[CX_K - 2], WAVE - 1);
+    hc = readlane_f64(h[CX_K - 1], WAVE - 1);
+    lc = readlane_f64(l[CX_K - 1], WAVE - 1);
+    rcC = __builtin_amdgcn_readlane(lcc[CX_K - 1], WAVE - 1);
+    rtC = __builtin_amdgcn_readlane(lct[CX_K - 1], WAVE - 1);
+  }
+}
+
+// ---- pass 2: group records -> chunk partials ------------------------------------
+constexpr int GR_TW = 64;   // timestamps per workgroup (lane = t)
+constexpr int GR_NW = 4;
+constexpr int CX_NSUM = 9;  // the first 9 partial columns
+
+struct GroupReduceArgs {
+  const double* gsum[4];
+  const uint16_t* gcnt;
+  int64_t ngrp, ld_g, per_chunk;
+  int T;
+  double* chunk;   // [nchunk][T][9]
+};
+
+__global__ __launch_bounds__(GR_TW * GR_NW) void context_group_reduce_kernel(const GroupReduceArgs A) {
+  __shared__ double sAcc[GR_NW][CX_NSUM][GR_TW + 1];
+  const int lane = threadIdx.x & (WAVE - 1), u = threadIdx.x / WAVE;
+  const int t = blockIdx.x * GR_TW + lane;
+  const int64_t g0 = (int64_t)blockIdx.y * A.per_chunk;
+  const int64_t g1 = min(A.ngrp, g0 + A.per_chunk);
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  int n[5] = {0, 0, 0, 0, 0};
+  if (t < A.T) {
+    for (int64_t g = g0 + u; g < g1; g += GR_NW) {   // ascending, fixed per wave
+      const int64_t o = g * A.ld_g + t;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) s[f] += A.gsum[f][o];
+      const unsigned v = A.gcnt[o];
+      n[0] += (v >> CNT_VALID) & 7u;
+      n[1] += (v >> CNT_ADV) & 7u;
+      n[2] += (v >> CNT_DEC) & 7u;
+      n[3] += (v >> CNT_A20) & 7u;
+      n[4] += (v >> CNT_A50) & 7u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) sAcc[u][i][lane] = (double)n[i];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) sAcc[u][5 + f][lane] = s[f];
+  __syncthreads();
+  if (u == 0 && t < A.T) {
+    double acc[CX_NSUM];
+#pragma unroll
+    for (int i = 0; i < CX_NSUM; ++i) acc[i] = sAcc[0][i][lane];
+    for (int v = 1; v < GR_NW; ++v)
+#pragma unroll
+      for (int i = 0; i < CX_NSUM; ++i) acc[i] += sAcc[v][i][lane];
+    double* o = A.chunk + ((int64_t)blockIdx.y * A.T + t) * CX_NSUM;
+#pragma unroll
+    for (int i = 0; i < CX_NSUM; ++i) o[i] = acc[i];
+  }
+}
+
+// ---- pass 3: chunk partials -> [T][10] ---------------------------------------------
+__global__ __launch_bounds__(256) void context_chunk_reduce_kernel(const double* __restrict__ chunk, int nchunk, int T,
+                                                                   double* __restrict__ partial) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= T) return;
+  double acc[CX_NSUM];
+#pragma unroll
+  for (int i = 0; i < CX_NSUM; ++i) acc[i] = 0.0;
+  for (int j = 0; j < nchunk; ++j) {
+    const double* c = chunk + ((int64_t)j * T + t) * CX_NSUM;
+#pragma unroll
+    for (int i = 0; i < CX_NSUM; ++i) acc[i] += c[i];
+  }
+  double* o = partial + (int64_t)t * BQ_NUM_PARTIALS;
+#pragma unroll
+  for (int i = 0; i < CX_NSUM; ++i) o[i] = acc[i];
+  o[BQ_P_RESERVED] = 0.0;
+}
+
+// ---- workspace layout ---------------------------------------------------------------
+struct CtxLayout {
+  int64_t ngrp, ld_g, nchunk, per_chunk;
+  size_t off_sum[4], off_cnt, off_chunk, bytes;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static CtxLayout ctx_layout(int64_t S, int64_t T) {
+  CtxLayout L;
+  L.ngrp = (S + CX_NW - 1) / CX_NW;
+  L.ld_g = (T + 63) & ~(int64_t)63;
+  // enough pass-2 workgroups to fill the chip: ~2048 (t-block, chunk) pairs
+  const int64_t tblocks = (T + GR_TW - 1) / GR_TW;
+  int64_t nch = (2048 + tblocks - 1) / (tblocks > 0 ? tblocks : 1);
+  nch = nch < 1 ? 1 : nch;
+  const int64_t maxch = (L.ngrp + 3) / 4;   // at least ~4 groups per chunk
+  if (nch > maxch) nch = maxch < 1 ? 1 : maxch;
+  L.per_chunk = (L.ngrp + nch - 1) / nch;
+  L.nchunk = (L.ngrp + L.per_chunk - 1) / L.per_chunk;
+  size_t o = 0;
+  for (int f = 0; f < 4; ++f) {
+    L.off_sum[f] = o;
+    o = align256(o + (size_t)L.ngrp * L.ld_g * sizeof(double));
+  }
+  L.off_cnt = o;
+  o = align256(o + (size_t)L.ngrp * L.ld_g * sizeof(uint16_t));
+  L.off_chunk = o;
+  o = align256(o + (size_t)L.nchunk * T * CX_NSUM * sizeof(double));
+  L.bytes = o;
+  return L;
+}
+
+static double cx_alpha_from_span(double span) {
+  const double com = (span - 1.0) / 2.0;
+  return 1.0 / (1.0 + com);
+}
+
+}  // namespace bq
+
+extern "C" {
+
+size_t bq_context_workspace_bytes(int64_t S, int64_t T) {
+  if (S <= 0 || T <= 0) return 0;
+  return bq::ctx_layout(S, T).bytes;
+}
+
+int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t max_bars,
+                        void* workspace, size_t workspace_bytes, double* partial, double* const* last_feat,
+                        void* stream) {
+  using namespace bq;
+  if (!hlc || !hlc[0] || !hlc[1] || !hlc[2] || !partial || S < 0 || T < 0 || ld_in < T || max_bars < 15 ||
+      max_bars > BQ_MAX_HISTORY + 1 || T > (int64_t)0x7fffffff - CX_TT || S > (int64_t)0x7fffffff * CX_NW)
+    return BQ_EINVAL;
+  if (S == 0 || T == 0) {
+    if (T > 0 && hipMemsetAsync(partial, 0, (size_t)T * BQ_NUM_PARTIALS * sizeof(double), (hipStream_t)stream) != hipSuccess)
+      return BQ_EHIP;
+    return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+  }
+  const CtxLayout L = ctx_layout(S, T);
+  if (!workspace || workspace_bytes < L.bytes || (((uintptr_t)workspace) & 255u)) return BQ_EINVAL;
+  CtxArgs A;
+  memset(&A, 0, sizeof(A));
+  A.h = hlc[0];
+  A.l = hlc[1];
+  A.c = hlc[2];
+  A.S = S;
+  A.ld_in = ld_in;
+  A.T = (int)T;
+  A.M = max_bars;
+  auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
+  A.vin = (ld_in % 2) == 0 && aligned(A.h) && aligned(A.l) && aligned(A.c);
+  const double spans[2] = {20.0, 50.0};   // live_market_context_accumulator.py:266-267
+  for (int e = 0; e < 2; ++e) {
+    const double al = cx_alpha_from_span(spans[e]);
+    A.alpha[e] = al;
+    A.om[e] = 1.0 - al;
+    A.den[e] = A.om[e] + al;
+    A.lin_a[e] = A.om[e] / A.den[e];
+    A.lin_b[e] = al / A.den[e];
+    double ak = 1.0;
+    for (int k = 0; k < CX_K; ++k) ak *= A.lin_a[e];
+    for (int j = 0; j < 8; ++j) {
+      A.apow[e][j] = ak;
+      ak *= ak;
+    }
+    double cp = 1.0;
+    for (int k = 0; k < max_bars - 1; ++k) cp *= A.lin_a[e];
+    A.corr[e] = cp;
+  }
+  char* ws = (char*)workspace;
+  for (int f = 0; f < 4; ++f) A.gsum[f] = (double*)(ws + L.off_sum[f]);
+  A.gcnt = (uint16_t*)(ws + L.off_cnt);
+  A.ld_g = L.ld_g;
+  for (int f = 0; f < BQ_NUM_FEATURES; ++f) A.last[f] = last_feat ? last_feat[f] : nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  if (A.den[0] != 1.0 || A.den[1] != 1.0)
+    hipLaunchKernelGGL(context_partials_kernel<true>, dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+  else
+    hipLaunchKernelGGL(context_partials_kernel<false>, dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+  GroupReduceArgs G;
+  for (int f = 0; f < 4; ++f) G.gsum[f] = A.gsum[f];
+  G.gcnt = A.gcnt;
+  G.ngrp = L.ngrp;
+  G.ld_g = L.ld_g;
+  G.per_chunk = L.per_chunk;
+  G.T = (int)T;
+  G.chunk = (double*)(ws + L.off_chunk);
+  hipLaunchKernelGGL(context_group_reduce_kernel, dim3((unsigned)((T + GR_TW - 1) / GR_TW), (unsigned)L.nchunk),
+                     dim3(GR_TW * GR_NW), 0, st, G);
+  hipLaunchKernelGGL(context_chunk_reduce_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st,
+                     (const double*)G.chunk, (int)L.nchunk, (int)T, partial);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+}  // extern "C"

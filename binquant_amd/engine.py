@@ -322,6 +322,49 @@ def breadth_partial(
     return out
 
 
+@device_entry
+def context_partials(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    max_bars: int = 400,
+    out: torch.Tensor | None = None,
+    last: bool = False,
+    stream: torch.cuda.Stream | None = None,
+):
+    """The [T, 10] breadth partials of every timestamp straight from the
+    panel (bq_context_partials): market_features + breadth_partial fused, the
+    feature columns never written (live_market_context_accumulator.py:95-163
+    over _compute_symbol_features :244-297). Counts equal breadth_partial's,
+    sums agree to rounding. last=True also returns the features at t = T - 1
+    ({name: [S]}, what a context's symbol_features reads); returns
+    (partial, last_features | None)."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    hlc = [_check_panel(t, n, (S, T)) for t, n in zip((high, low, close), ("high", "low", "close"))]
+    ld_in = _row_stride(hlc[0])
+    if any(_row_stride(t) != ld_in for t in hlc):
+        hlc = [t.contiguous() for t in hlc]
+        ld_in = T
+    dev = close.device
+    if out is None:
+        out = torch.empty((T, len(PARTIAL_COLUMNS)), dtype=torch.float64, device=dev)
+    elif not (isinstance(out, torch.Tensor) and out.dtype == torch.float64 and out.device == dev
+              and tuple(out.shape) == (T, len(PARTIAL_COLUMNS)) and out.is_contiguous()):
+        raise ValueError(f"out: expected a contiguous float64 [{T}, {len(PARTIAL_COLUMNS)}] tensor on {dev}")
+    lib = _lib.load()
+    nbytes = int(lib.bq_context_workspace_bytes(S, T))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)   # caching allocator: 512-B aligned
+    lastf = {n: torch.empty(S, dtype=torch.float64, device=dev) for n in FEATURE_COLUMNS} if last else None
+    st = lib.bq_context_partials(
+        _lib.ptr_array([t.data_ptr() for t in hlc]), S, T, ld_in, int(max_bars),
+        ctypes.c_void_p(ws.data_ptr()), nbytes, ctypes.c_void_p(out.data_ptr()),
+        _lib.ptr_array([lastf[n].data_ptr() for n in FEATURE_COLUMNS]) if last else None,
+        _stream_handle(stream))
+    _lib.check(st, "bq_context_partials")
+    return out, lastf
+
+
 class TickState:
     """Device-resident streaming state for S symbols (bq_state)."""
 

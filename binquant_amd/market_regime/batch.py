@@ -41,9 +41,19 @@ class MarketContextBatch:
     def symbol_features_at(self, i: int, close: torch.Tensor, btc_return_t: float | None,
                            btc_index: int | None = None) -> dict[str, np.ndarray]:
         """Per-symbol feature row at timestamp index i (this rank's symbols),
-        with relative strength and the micro-regime annotation."""
-        f = {k: v[:, i].double().cpu().numpy() for k, v in self.features.items()}
-        c = close[:, i].cpu().numpy()
+        with relative strength and the micro-regime annotation. After a fused
+        build (keep_features=False) only the last timestamp is held."""
+        T = close.shape[1]
+        j = i % T if i < 0 else i
+        fcols = next(iter(self.features.values())).shape[1]
+        if fcols == 1 and T > 1:
+            if j != T - 1:
+                raise ValueError("fused context build: only the last timestamp's features are kept")
+            j_f = 0
+        else:
+            j_f = j
+        f = {k: v[:, j_f].double().cpu().numpy() for k, v in self.features.items()}
+        c = close[:, j].cpu().numpy()
         ret = f["return_pct"]
         rs = np.zeros_like(ret) if btc_return_t is None else ret - btc_return_t
         if btc_index is not None:
@@ -108,14 +118,22 @@ def market_context_batch(
     total_tracked: int | None = None,
     group=None,
     previous_context: dict | None = None,
+    keep_features: bool = True,
 ) -> MarketContextBatch:
     """Contexts at every timestamp of a (possibly sharded) [S, T] panel.
 
     btc_hlc: the benchmark's (high, low, close) [1, T] rows, replicated.
     total_tracked: symbols tracked across ALL ranks (default: sum of shards).
+    keep_features=False: the fused build (engine.context_partials) — the
+    feature columns are never written; ``features`` then holds the last
+    timestamp's row only ([S, 1] each: symbol_features_at(T - 1) works).
     """
-    feats = engine.market_features(high, low, close, max_bars=max_bars)
-    part = engine.breadth_partial(close, feats)
+    if keep_features:
+        feats = engine.market_features(high, low, close, max_bars=max_bars)
+        part = engine.breadth_partial(close, feats)
+    else:
+        part, last = engine.context_partials(high, low, close, max_bars=max_bars, last=True)
+        feats = {k: v[:, None] for k, v in last.items()}
     part, n_total = reduce_partials(part, close.shape[0], group)
     bh, bl, bc = btc_hlc
     bf = engine.market_features(bh, bl, bc, max_bars=max_bars)

@@ -53,6 +53,7 @@
 #define BINQUANT_AMD_H
 
 #include <stdint.h>
+#include <stddef.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -202,6 +203,26 @@ int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t l
  */
 int bq_breadth_partial(const double* close, const double* const* feat, int64_t S, int64_t T,
                        int64_t ld_close, int64_t ld_feat, double* partial, void* stream);
+
+/*
+ * Fused panel context build (BASELINE configs[4]): the features of
+ * bq_market_features reduced straight into the partials of
+ * bq_breadth_partial, without writing the feature columns
+ * (live_market_context_accumulator.py:95-163 over :244-297 at every t).
+ * Replaces bq_market_features + bq_breadth_partial when only the [T][10]
+ * partials (and, optionally, the last timestamp's features) are read.
+ * hlc = {high, low, close} [S][ld_in]; partial[T][BQ_NUM_PARTIALS]
+ * overwritten (column BQ_P_RESERVED = 0). last_feat: NULL, or
+ * BQ_NUM_FEATURES device pointers (each NULL or [S]) receiving the features
+ * at t = T - 1. workspace: device memory of bq_context_workspace_bytes(S, T)
+ * bytes, 256-byte aligned (group records of 4 symbols; the library
+ * allocates nothing). Counts equal bq_breadth_partial's; the sums agree to
+ * rounding (another fixed order). Deterministic: no atomics.
+ */
+size_t bq_context_workspace_bytes(int64_t S, int64_t T);
+int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in,
+                        int32_t max_bars, void* workspace, size_t workspace_bytes,
+                        double* partial, double* const* last_feat, void* stream);
 
 /* ---- benchmark-relative statistics ---------------------------------------- */
 /*

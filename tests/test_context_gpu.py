@@ -1,0 +1,179 @@
+"""GPU parity of the fused panel context build (bq_context_partials, the
+C5 leg): _compute_symbol_features at every timestamp reduced straight into
+the _build_context partials (market_regime/live_market_context_accumulator.py
+:95-163, :244-297), against
+
+* bq_market_features + bq_breadth_partial (the unfused path, itself pinned to
+  the reference's fixtures in test_market_gpu.py): counts exactly, sums to
+  1e-12 of their magnitude;
+* the oracle restatement at sampled timestamps (counts exactly where no close
+  lies within 1e-9 of its EMA; sums 1e-9);
+* the reference's own golden contexts (market_context.json);
+and checks the optional last-timestamp feature row and run-to-run bitwise
+reproducibility. Shapes cover S not a multiple of the 4-symbol group, T not
+a multiple of the 256-candle tile, T < max_bars, and max_bars 15 .. 513."""
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from binquant_amd import engine
+from binquant_amd._lib import FEATURE_COLUMNS
+from binquant_amd.market_regime.regime import annotate_market, score_contexts
+from binquant_amd.synth import numpy_panel
+from oracle import market_ref
+from tests.util import assert_close
+
+pytestmark = pytest.mark.gpu
+G = Path(__file__).resolve().parent / "golden"
+
+
+def _unfused(h, l, c, M):
+    f = engine.market_features(h, l, c, max_bars=M)
+    return engine.breadth_partial(c, f), f
+
+
+def _near_ties(c, f):
+    """timestamps where some close lies within 1e-12 of its EMA (a count may
+    legitimately differ there: the two kernels' EMAs agree to rounding)"""
+    tie = torch.zeros(c.shape[1], dtype=torch.bool, device=c.device)
+    for e in ("ema20", "ema50"):
+        tie |= ((c - f[e]).abs() <= 1e-12 * c.abs()).any(dim=0)
+    return tie.cpu().numpy()
+
+
+def _check_against_unfused(h, l, c, M):
+    want, f = _unfused(h, l, c, M)
+    got, last = engine.context_partials(h, l, c, max_bars=M, last=True)
+    got2, _ = engine.context_partials(h, l, c, max_bars=M)
+    torch.cuda.synchronize()
+    g, w = got.cpu().numpy(), want.cpu().numpy()
+    np.testing.assert_array_equal(g, got2.cpu().numpy())   # bitwise reproducible
+    ok = ~_near_ties(c, f)
+    np.testing.assert_array_equal(g[ok, :5], w[ok, :5])
+    assert (g[:, 9] == 0).all()
+    valid = ~torch.isnan(f["return_pct"])
+    for i, k in ((5, "return_pct"), (6, "trend_score"), (7, "atr_pct"), (8, "bb_width")):
+        mag = torch.where(valid, f[k].abs(), torch.zeros_like(f[k])).sum(dim=0).cpu().numpy()
+        assert_close(g[:, i], w[:, i], k, rtol=0.0, scale=mag + 1e-300, atol_rel=1e-12)
+    for k in FEATURE_COLUMNS:
+        want_last = f[k][:, -1].cpu().numpy()
+        scale = np.abs(c[:, -1].cpu().numpy()) if k in ("ema20", "ema50") else 1e-3
+        assert_close(last[k].cpu().numpy(), want_last, f"last {k}", rtol=1e-12, scale=scale, atol_rel=1e-12)
+
+
+@pytest.mark.parametrize("S,T,M", [(1, 1, 400), (3, 2, 400), (5, 60, 15), (7, 255, 400), (9, 256, 400),
+                                   (13, 257, 20), (64, 1000, 400), (33, 2100, 512), (130, 700, 200),
+                                   (6, 1500, 513)])
+def test_context_partials_equal_unfused(cuda, S, T, M):
+    p = numpy_panel(S, T, seed0=S * 31 + T, edges=False)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    _check_against_unfused(d["high"], d["low"], d["close"], M)
+
+
+def test_context_partials_edges_and_strides(cuda):
+    """constant runs / halted bars / zero volume (numpy_panel edges) and a
+    row stride wider than T"""
+    S, T, M = 41, 1300, 400
+    p = numpy_panel(S, T, seed0=4242, edges=True)
+    big = {k: np.concatenate([v, np.zeros((S, 37))], axis=1) for k, v in p.items()}
+    d = {k: torch.from_numpy(v).cuda()[:, :T] for k, v in big.items()}
+    _check_against_unfused(d["high"], d["low"], d["close"], M)
+
+
+@pytest.mark.parametrize("label", ["trend_up_40", "random_64", "selloff_64"])
+def test_context_partials_match_reference_golden(cuda, label):
+    """the reference's contexts (refresh_context_for_timestamp +
+    annotate_context, tests/golden/market_context.json) from the fused
+    partials"""
+    meta = json.loads((G / "market_context.json").read_text())
+    panels = np.load(G / "market_context_panels.npz")
+    sc = meta[label]
+    syms = sc["symbols"]
+    ts_all = panels[f"{label}__timestamp"][0]
+    h, l, c = (torch.from_numpy(panels[f"{label}__{k}"]).cuda() for k in ("high", "low", "close"))
+    part, _ = engine.context_partials(h, l, c, max_bars=sc["max_bars"])
+    part = part.cpu().numpy()
+    b = syms.index(sc["btc"])
+    f = engine.market_features(h[b:b + 1], l[b:b + 1], c[b:b + 1], max_bars=sc["max_bars"])
+    btc_ret, btc_trend = f["return_pct"][0].cpu().numpy(), f["trend_score"][0].cpu().numpy()
+    idx = [int(np.flatnonzero(ts_all == ts)[0]) for ts in sc["timestamps"]]
+    ok = ~np.isnan(btc_ret[idx])
+    batch = score_contexts(part[idx], np.nan_to_num(btc_ret[idx]), np.nan_to_num(btc_trend[idx]), ok,
+                           total_tracked=len(syms), timestamps=np.array(sc["timestamps"]))
+    annotate_market(batch)
+    for i, want in enumerate(sc["contexts"]):
+        got = batch.context_at(i)
+        if want is None:
+            assert got is None
+            continue
+        for k, v in want.items():
+            if k in ("symbol_features", "metadata", "btc_symbol", "confidence", "is_provisional", "timestamp"):
+                continue
+            if isinstance(v, (bool, str, int)) or v is None:
+                assert got[k] == v, (k, got[k], v)
+            else:
+                assert got[k] == pytest.approx(v, rel=1e-9, abs=1e-12), k
+
+
+def test_context_partials_c5_shard_vs_oracle(cuda):
+    """The C5 per-GPU leg at the C4 shard (12 500 x 10 000, 400-bar cap):
+    the fused partials equal the unfused kernels' (counts exactly away from
+    near-ties) on every timestamp and the oracle restatement at sampled
+    timestamps (counts exactly, sums 1e-9)."""
+    from binquant_amd.synth import device_panel
+
+    S, T, M = 12_500, 10_000, 400
+    p = device_panel(S, T, seed=5150)
+    h, l, c = p["high"], p["low"], p["close"]
+    del p
+    _check_against_unfused(h, l, c, M)
+    part, _ = engine.context_partials(h, l, c, max_bars=M)
+    part = part.cpu().numpy()
+    for t in (1, 19, 399, 400, 5_000, 9_999):
+        s0 = max(0, t - M + 1)
+        hw, lw, cw = (x[:, s0: t + 1].cpu().numpy() for x in (h, l, c))
+        want = market_ref.window_features(hw, lw, cw)
+        wp = market_ref.partials_from_features(want)
+        close_t = cw[:, -1]
+        tie = any((np.abs(close_t - want[e]) <= 1e-9 * np.abs(close_t)).any() for e in ("ema20", "ema50"))
+        if not tie:
+            np.testing.assert_array_equal(part[t, :5], wp[:5], err_msg=f"counts@{t}")
+        for i, k in ((5, "return_pct"), (6, "trend_score"), (7, "atr_pct"), (8, "bb_width")):
+            mag = np.abs(want[k]).sum()
+            assert abs(part[t, i] - wp[i]) <= 1e-9 * mag + 1e-300, (t, i, part[t, i], wp[i])
+
+
+def test_market_context_batch_fused_equals_unfused(cuda):
+    """market_context_batch(keep_features=False) — the fused build — gives the
+    same contexts and the same last-timestamp symbol rows as the unfused one"""
+    from binquant_amd.market_regime.batch import market_context_batch
+
+    S, T = 300, 900
+    p = numpy_panel(S, T, seed0=77, edges=False)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    btc = tuple(d[k][:1] for k in ("high", "low", "close"))
+    a = market_context_batch(d["high"], d["low"], d["close"], btc, max_bars=400)
+    b = market_context_batch(d["high"], d["low"], d["close"], btc, max_bars=400, keep_features=False)
+    for i in (0, 1, 2, 399, 400, T - 1):
+        ca, cb = a.context_at(i), b.context_at(i)
+        assert (ca is None) == (cb is None)
+        if ca is None:
+            continue
+        for k, v in ca.items():
+            if isinstance(v, float):
+                assert cb[k] == pytest.approx(v, rel=1e-12, abs=1e-15), (i, k)
+            else:
+                assert cb[k] == v, (i, k)
+    ra = a.symbol_features_at(T - 1, d["close"], 0.001, btc_index=0)
+    rb = b.symbol_features_at(-1, d["close"], 0.001, btc_index=0)
+    for k, v in ra.items():
+        if v.dtype == bool or v.dtype.kind in "OU":
+            np.testing.assert_array_equal(rb[k], v, err_msg=k)
+        else:
+            np.testing.assert_allclose(rb[k], v, rtol=1e-12, atol=1e-15, err_msg=k)
+    with pytest.raises(ValueError):
+        b.symbol_features_at(5, d["close"], 0.0)
