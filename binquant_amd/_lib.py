@@ -66,7 +66,8 @@ SCORE_FIELDS = ("confidence", "breadth_score", "btc_alignment_score", "cross_ass
 AGG_CODES = {"first": 0, "last": 1, "max": 2, "min": 3, "sum": 4}
 MAX_ROLLING_WINDOW = 96
 ROLL_MODES = {"quantile": 0, "median": 1, "mean": 2, "sum": 3, "var": 4, "std": 5, "var0": 6, "std0": 7,
-              "isum": 10}   # isum: sum of an integer-valued series (flag counts), bq_roll_mode BQ_ROLL_ISUM
+              "isum": 10,   # isum: sum of an integer-valued series (flag counts), bq_roll_mode BQ_ROLL_ISUM
+              "qlower": 11}   # quantile(q, interpolation="lower"), BQ_ROLL_QLOWER
 ROLL_EWM = 8
 ROLL_FFILL = 9
 ROLL_ISUM = 10

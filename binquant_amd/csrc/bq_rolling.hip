@@ -67,6 +67,7 @@ struct RollJob {
   double* out;
   int64_t ld_in, ld_out;
   int win, minp, shift, mode, seg, nseg;
+  int lower;   // BQ_ROLL_QLOWER: the quantile's lower order statistic, no interpolation
   double q, alpha;
   int64_t rows;   // this job's rows (<= the batch's S; a benchmark row beside a panel)
 };
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
     } else {   // roll_quantile, linear interpolation
       const double idxf = A.q * (double)(n - 1);
       const int idx = (int)idxf;
-      if ((double)idx == idxf) r = win.get(idx);
+      if ((double)idx == idxf || A.lower) r = win.get(idx);
       else {
         const double lo = win.get(idx), hi = win.get(idx + 1);
         r = lo + (hi - lo) * (idxf - (double)idx);
@@ -891,7 +892,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
         } else {
           const double idxf = A.q * (double)(n - 1);
           a = (int)idxf;
-          two = n > 1 && (double)a != idxf;
+          two = n > 1 && (double)a != idxf && !A.lower;
           frac = idxf - (double)a;
         }
         const double lo = okey_value(s_key[wv][select_bit<NWORD>(M, a)]);
@@ -929,7 +930,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
     } else {
       idxf[o] = A.q * (double)(n - 1);
       a = (int)idxf[o];
-      need2[o] = n > 1 && (double)a != idxf[o];
+      need2[o] = n > 1 && (double)a != idxf[o] && !A.lower;
     }
     tlo[o] = desc ? n - a : a + 1;
     thi[o] = desc ? n - a - 1 : a + 2;
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) 
     } else {   // roll_quantile, linear interpolation (max / min: q = 1 / 0)
       const double idxf = A.q * (double)(n - 1);
       const int idx = (int)idxf;
-      if ((double)idx == idxf) r = pick(v, idx);
+      if ((double)idx == idxf || A.lower) r = pick(v, idx);
       else {
         const double lo = pick(v, idx), hi = pick(v, idx + 1);
         r = lo + (hi - lo) * (idxf - (double)idx);
@@ -1133,7 +1134,8 @@ bool job_ok(const bq_roll_job& j, int64_t S, int64_t T) {
   if (j.mode == BQ_ROLL_EWM) return j.alpha > 0.0 && j.alpha <= 1.0;
   if (j.mode == BQ_ROLL_FFILL) return j.shift == 0;
   return j.window >= 1 && j.window <= bq::RW_MAXW && j.shift >= 0 && j.shift <= bq::RW_MAXSHIFT &&
-         ((j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0) || j.mode == BQ_ROLL_ISUM) && j.q >= 0.0 &&
+         ((j.mode >= BQ_ROLL_QUANTILE && j.mode <= BQ_ROLL_STD0) || j.mode == BQ_ROLL_ISUM ||
+          j.mode == BQ_ROLL_QLOWER) && j.q >= 0.0 &&
          j.q <= 1.0;
 }
 
@@ -1407,6 +1409,10 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     J.q = in.q;
     J.alpha = in.alpha;
     J.rows = in.rows > 0 ? in.rows : S;
+    if (J.mode == BQ_ROLL_QLOWER) {   // an order statistic like the quantile, no interpolation
+      J.mode = BQ_ROLL_QUANTILE;
+      J.lower = 1;
+    }
     if (J.mode == BQ_ROLL_FFILL) {   // a scan, not a replay (ffill_kernel)
       ff.j[nff++] = J;
       if (nff == RW_MAXJOBS) flush_ff();
@@ -1465,7 +1471,8 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
 
 int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window, int32_t min_periods,
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream) {
-  if ((mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0) && mode != BQ_ROLL_ISUM) return BQ_EINVAL;
+  if ((mode < BQ_ROLL_QUANTILE || mode > BQ_ROLL_STD0) && mode != BQ_ROLL_ISUM && mode != BQ_ROLL_QLOWER)
+    return BQ_EINVAL;
   bq_roll_job j;
   memset(&j, 0, sizeof(j));
   j.x = x;

@@ -188,6 +188,52 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     return out, status_f.to(torch.int8)
 
 
+def gradual_gainer_leadership(open_time: torch.Tensor, close: torch.Tensor, btc_time: torch.Tensor,
+                              btc_close: torch.Tensor, rs_quantile: float = 0.80, rs_lookback: int = 96,
+                              min_history: int = 100, min_count: int = 20, short: int = 8, long: int = 24):
+    """GradualGainerRetest._leadership_allows at every t (column t = the
+    method on the prefix frame df.iloc[:t + 1]; strategies/gradual_gainer_retest.py
+    :131-196), against the benchmark frame (btc_time ascending, duplicates:
+    the later row wins, as the reference's dict does).
+
+    * btc close at each candle's open_time: the left merge bq_align;
+    * _relative_strengths: all of the last short·3+1 = 25 times present in the
+      benchmark and every close > 0 (a rolling(25) integer sum of that flag),
+      rs_2h / rs_6h = c/c[-8] - b/b[-8], c/c[-24] - b/b[-24];
+    * the history: one entry per position i >= 24 of the last 96 whose times i,
+      i-8, i-24 are all in the benchmark with the six closes > 0 — NaN
+      elsewhere, so the 80th-percentile threshold sorted(h)[int((n-1) q)] is
+      rolling(96, min_periods=20).quantile(q, interpolation="lower")
+      (bq_rolling_batch, BQ_ROLL_QLOWER; order statistics by bit selection);
+    * leader = rs_2h > 0 and rs_6h > 0 and rs >= threshold for both.
+
+    Returns {"leader": bool [S, T], "rs_2h": [S, T], "rs_6h": [S, T]} with the
+    method's fall-backs: (False, 0.0, 0.0) when the strengths are None or the
+    frame is shorter than min_history, (False, rs_2h, rs_6h) when fewer than
+    min_count history entries exist."""
+    S, T = close.shape
+    recent = long + 1
+    b = engine.align(open_time, btc_time, btc_close)
+    C, B = F.inp(close), F.inp(b)
+    pos = ((C > 0) & (F.shift(C, short) > 0) & (F.shift(C, long) > 0)
+           & (B > 0) & (F.shift(B, short) > 0) & (F.shift(B, long) > 0))
+    rs2 = C / F.shift(C, short) - B / F.shift(B, short)
+    rs6 = C / F.shift(C, long) - B / F.shift(B, long)
+    st = F.run({"h2": F.where(pos, rs2, NAN), "h6": F.where(pos, rs6, NAN),
+                "ok": F.where((C > 0) & (B > 0), 1.0, 0.0), "rs2": rs2, "rs6": rs6}, S, T)
+    R = engine.Roll
+    thr2, thr6, okn = engine.rolling_many(
+        R(st["h2"], rs_lookback, "qlower", q=rs_quantile, min_periods=min_count),
+        R(st["h6"], rs_lookback, "qlower", q=rs_quantile, min_periods=min_count),
+        R(st["ok"], recent, "isum", min_periods=recent))
+    n = torch.arange(1, T + 1, device=close.device, dtype=torch.float64)
+    R2, R6, T2, T6 = F.inp(st["rs2"]), F.inp(st["rs6"]), F.inp(thr2), F.inp(thr6)
+    strengths = (F.inp(okn) == float(recent)) & (F.inp(n) >= float(min_history))
+    leader = strengths & ~F.isnan(T2) & (R2 > 0) & (R6 > 0) & (R2 >= T2) & (R6 >= T6)
+    res = F.run({"leader": leader, "rs_2h": F.where(strengths, R2, 0.0), "rs_6h": F.where(strengths, R6, 0.0)}, S, T)
+    return res
+
+
 def mean_reversion_features(o, h, l, c, v, atr, rsi_window: int = 14, volume_ma_window: int = 20,
                             atr_ma_window: int = 20, fast: int = 20, slow: int = 50) -> dict[str, torch.Tensor]:
     """The per-candle inputs MeanReversionFade reads (strategies/mean_reversion_fade.py:240-255):

@@ -247,11 +247,16 @@ enum bq_roll_mode {
   BQ_ROLL_EWM = 8,   /* bq_rolling_batch only: ewm(alpha, adjust=False, min_periods) */
   BQ_ROLL_FFILL = 9, /* bq_rolling_batch only: ffill() (leading NaNs stay), shift 0;
                         Series.pct_change's default fill_method='pad' */
-  BQ_ROLL_ISUM = 10  /* rolling sum of a series whose values are integers with
+  BQ_ROLL_ISUM = 10, /* rolling sum of a series whose values are integers with
                         |sum| < 2^53 (counts of boolean flags): pandas' result
                         is then exact in any summation order, so the window is
                         summed directly (no sequential replay); same values,
                         same-value rule and min_periods as BQ_ROLL_SUM */
+  BQ_ROLL_QLOWER = 11 /* quantile(q, interpolation="lower"): the int((n-1) q)-th
+                        smallest of the window's n values, no interpolation —
+                        sorted(history)[int((len(history) - 1) * q)] of
+                        GradualGainerRetest._leadership_allows
+                        (strategies/gradual_gainer_retest.py:182-187) */
 };
 /*
  * out = x.shift(shift).rolling(window, min_periods).<mode>() per symbol row,

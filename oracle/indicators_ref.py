@@ -301,3 +301,39 @@ def exact_zscore(window_closes) -> float:
     if var == 0:
         return 0.0
     return float(w[-1] - m) / sqrt(float(var))
+
+
+def gradual_gainer_leadership(open_time, close, btc_time, btc_close, q: float = 0.80, lookback: int = 96,
+                              min_history: int = 100, min_count: int = 20, short: int = 8, long: int = 24):
+    """GradualGainerRetest._leadership_allows (strategies/gradual_gainer_retest.py:131-196)
+    at every prefix t of each row, vectorised with pandas: the benchmark
+    close by open_time (a dict in the reference: the later of duplicated
+    times wins), the history entry at i needs times i, i-8, i-24 present and
+    the six closes > 0, threshold = sorted(history)[int((len - 1) * q)] over
+    the last `lookback` positions (rolling quantile, interpolation "lower"),
+    the strengths need the last 25 times present and every close > 0.
+    Returns (leader bool [S, T], rs_2h, rs_6h) with the method's fall-backs."""
+    open_time = np.asarray(open_time, dtype=np.int64)
+    close = np.asarray(close, dtype=np.float64)
+    S, T = close.shape
+    bmap = pd.Series(np.asarray(btc_close, float), index=np.asarray(btc_time, np.int64))
+    bmap = bmap[~bmap.index.duplicated(keep="last")]
+    lead = np.zeros((S, T), dtype=bool)
+    r2o, r6o = np.zeros((S, T)), np.zeros((S, T))
+    for s in range(S):
+        c = pd.Series(close[s])
+        b = pd.Series(bmap.reindex(open_time[s]).to_numpy())
+        pos = ((c > 0) & (c.shift(short) > 0) & (c.shift(long) > 0) & (b > 0) & (b.shift(short) > 0)
+               & (b.shift(long) > 0))
+        rs2 = c / c.shift(short) - b / b.shift(short)
+        rs6 = c / c.shift(long) - b / b.shift(long)
+        h2, h6 = rs2.where(pos), rs6.where(pos)
+        t2 = h2.rolling(lookback, min_periods=min_count).quantile(q, interpolation="lower")
+        t6 = h6.rolling(lookback, min_periods=min_count).quantile(q, interpolation="lower")
+        ok = ((c > 0) & (b > 0)).astype(float).rolling(long + 1).sum() == long + 1
+        strengths = ok.to_numpy() & (np.arange(1, T + 1) >= min_history)
+        lead[s] = strengths & t2.notna().to_numpy() & (rs2 > 0).to_numpy() & (rs6 > 0).to_numpy() \
+            & (rs2 >= t2).to_numpy() & (rs6 >= t6).to_numpy()
+        r2o[s] = np.where(strengths, rs2.to_numpy(), 0.0)
+        r6o[s] = np.where(strengths, rs6.to_numpy(), 0.0)
+    return lead, r2o, r6o

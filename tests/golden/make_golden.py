@@ -33,6 +33,9 @@ Fixtures:
                         (tests/test_coinrule_price_tracker.py:148-189) behind its
                         Indicators.mfi pins (:226-248) and the docstring's RSI < 30 /
                         MACD < 0 claim for the oversold frame
+  leadership.npz        GradualGainerRetest._leadership_allows on every prefix frame
+                        (strategies/gradual_gainer_retest.py:131-196): the reference
+                        test's make_frames + a 20 x 360 panel with BTC gaps
   strategy_panel.npz    64 symbols x 1100 candles (tests/golden/panel_gen.py, inputs
                         regenerated from seeds, digest stored) through the real
                         ActivityBurstPump.compute_indicators, LiquidationSweepPump
@@ -41,7 +44,7 @@ Fixtures:
                         helpers; outputs recorded at 48 sampled positions per symbol
                         (panel_gen.sample_positions: last rows, tile boundary, random)
 
-Usage: python tests/golden/make_golden.py [--only pins,panel]
+Usage: python tests/golden/make_golden.py [--only pins,panel,leadership]
 """
 
 from __future__ import annotations
@@ -156,6 +159,8 @@ def child(out_dir: Path, only: set[str] | None = None) -> None:
             ohlcv_pins(out_dir)
         if "panel" in only:
             strategy_panel(out_dir)
+        if "leadership" in only:
+            leadership(out_dir)
         return
     import numpy as np
     import pandas as pd
@@ -569,6 +574,72 @@ def strategy_panel(out_dir: Path) -> None:
     out["tg_keys"] = np.array(tg_keys)
     out["feature_columns"] = np.array(feat_cols)
     np.savez_compressed(out_dir / "strategy_panel.npz", **out)
+
+
+def leadership(out_dir: Path) -> None:
+    """leadership.npz: GradualGainerRetest._leadership_allows (and the
+    _relative_strengths it starts from; strategies/gradual_gainer_retest.py:131-196)
+    on every prefix frame df.iloc[:t + 1] of
+      ref_*   the frames of the reference's own test
+              (tests/test_gradual_gainer_retest.py make_frames, imported from it);
+      pan_*   20 symbols x 360 candles of 15-minute random walks against a BTC
+              frame with missing candles, a duplicated timestamp (the dict keeps
+              the last row) and a zero close; symbols with zero / negative
+              closes, a late-listed symbol, steady gainers.
+    Outputs: leader (bool), rs_2h, rs_6h per (symbol, t) as the method returns
+    them (False, 0.0, 0.0 when strengths are None or history is short)."""
+    import importlib.util
+
+    import numpy as np
+    import pandas as pd
+
+    from strategies.gradual_gainer_retest import GradualGainerRetest
+
+    spec = importlib.util.spec_from_file_location("ref_test_ggr", REFERENCE / "tests" / "test_gradual_gainer_retest.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = {}
+
+    def run(name, times, closes, btc_t, btc_c):
+        S, T = closes.shape
+        lead = np.zeros((S, T), dtype=bool)
+        r2 = np.zeros((S, T))
+        r6 = np.zeros((S, T))
+        btc_df = pd.DataFrame({"open_time": btc_t, "close": btc_c})
+        for s in range(S):
+            df = pd.DataFrame({"open_time": times[s], "close": closes[s]})
+            for t in range(T):
+                a, b, c = GradualGainerRetest._leadership_allows(df.iloc[: t + 1], btc_df)
+                lead[s, t], r2[s, t], r6[s, t] = bool(a), float(b), float(c)
+        out.update({f"{name}__open_time": times, f"{name}__close": closes, f"{name}__btc_time": btc_t,
+                    f"{name}__btc_close": btc_c, f"{name}__leader": lead, f"{name}__rs_2h": r2,
+                    f"{name}__rs_6h": r6})
+
+    sym, btc = mod.make_frames()
+    run("ref", sym["open_time"].to_numpy(np.int64)[None], sym["close"].to_numpy(float)[None],
+        btc["open_time"].to_numpy(np.int64), btc["close"].to_numpy(float))
+
+    rng = np.random.default_rng(20261017)
+    S, T = 20, 360
+    t0 = 1_800_000_000_000
+    times = np.broadcast_to(t0 + 900_000 * np.arange(T, dtype=np.int64), (S, T)).copy()
+    drift = np.where(np.arange(S) % 4 == 0, 0.004, 0.0)[:, None]
+    closes = 50.0 * np.exp(np.cumsum(rng.normal(0.0, 0.006, (S, T)) + drift, axis=1))
+    closes[3, 200] = 0.0
+    closes[5, 150:153] = -1.0
+    times[7] = t0 + 900_000 * (np.arange(T, dtype=np.int64) + 40)   # late listing: its frame starts 40 bars later
+    keep = rng.random(T) > 0.03
+    keep[:30] = True
+    bt = t0 + 900_000 * np.arange(T + 40, dtype=np.int64)
+    bc = 30_000.0 * np.exp(np.cumsum(rng.normal(0.0, 0.004, T + 40)))
+    keep = np.concatenate([keep, np.ones(40, dtype=bool)])
+    bt, bc = bt[keep], bc[keep]
+    j = 120   # a duplicated timestamp: the later row wins in the reference's dict
+    bt = np.insert(bt, j + 1, bt[j])
+    bc = np.insert(bc, j + 1, bc[j] * 1.01)
+    bc[250] = 0.0
+    run("pan", times, closes, bt, bc)
+    np.savez_compressed(out_dir / "leadership.npz", **out)
 
 
 def scoring_and_selection(out_dir: Path) -> None:

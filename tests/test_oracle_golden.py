@@ -159,3 +159,19 @@ def test_strategy_panel_inputs_regenerate_bit_exact():
     z = np.load(Path(__file__).resolve().parent / "golden" / "strategy_panel.npz")
     assert pg.digest(pg.strategy_panel(*z["positions"].shape[:1], 1100)) == str(z["digest"])
     np.testing.assert_array_equal(pg.sample_positions(64, 1100), z["positions"])
+
+
+def test_leadership_oracle_equals_reference():
+    """oracle.indicators_ref.gradual_gainer_leadership vs the reference's own
+    GradualGainerRetest._leadership_allows on every prefix frame
+    (tests/golden/leadership.npz: the reference test's make_frames and a
+    20 x 360 panel with BTC gaps, a duplicated BTC time and non-positive
+    closes): booleans and relative strengths bit-exact."""
+    z = np.load(G / "leadership.npz")
+    for case in ("ref", "pan"):
+        lead, r2, r6 = indicators_ref.gradual_gainer_leadership(
+            z[f"{case}__open_time"], z[f"{case}__close"], z[f"{case}__btc_time"], z[f"{case}__btc_close"])
+        np.testing.assert_array_equal(lead, z[f"{case}__leader"])
+        np.testing.assert_array_equal(r2, z[f"{case}__rs_2h"])
+        np.testing.assert_array_equal(r6, z[f"{case}__rs_6h"])
+    assert z["ref__leader"][0, -1]   # the reference test's assertion (leader, rs > 0)
