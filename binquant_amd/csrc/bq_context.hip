@@ -62,6 +62,8 @@ struct CtxArgs {
   double alpha[2], om[2], den[2], lin_a[2], lin_b[2];
   double apow[2][8];   // lin_a^(4 * 2^j)
   double corr[2];      // lin_a^(M - 1)
+  int lag20, lag50;    // the lagged chain is run where corr >= 1e-15 (below, corr * |Y_s - c_s|
+                       // is under 1e-15 of the price move: far inside the 1e-9 bar)
   double* gsum[4];     // group sums [ngrp][ld_g]: return, trend, atr_pct, bb_width
   uint16_t* gcnt;      // packed counts [ngrp][ld_g]
   int64_t ld_g;
@@ -88,10 +90,17 @@ __device__ __forceinline__ void cx_load(const double* __restrict__ row, int tb, 
   }
 }
 
+// a / b with the hardware reciprocal + two Newton steps (~1 ulp; the sign of
+// a / b and a zero numerator are exact, which is all the counts look at)
+__device__ __forceinline__ double cx_div(double a, double b) {
+  const double r = rcp_nr(fabs(b));
+  return b < 0.0 ? -(a * r) : a * r;
+}
+
 // DIV: pandas' EMA divide by (old_wt + new_wt) is needed (not exactly 1.0)
 template <bool DIV>
 __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArgs A) {
-  __shared__ double sPc[CX_NW][CX_RS], sPt[CX_NW][CX_RS], sC[CX_NW][CX_RS];
+  __shared__ double sTr[CX_NW][CX_RS], sC[CX_NW][CX_RS];   // true range / close rings per wave
   __shared__ double sR[3][4][CX_TT];   // reduction slots: 4 sums, index k * 64 + lane
   __shared__ uint16_t sN[3][CX_TT];
 
@@ -104,20 +113,26 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
   const double* __restrict__ rH = A.h + row * A.ld_in;
   const double* __restrict__ rL = A.l + row * A.ld_in;
   const double* __restrict__ rC = A.c + row * A.ld_in;
-  double* __restrict__ pc = sPc[w];
-  double* __restrict__ pt = sPt[w];
+  double* __restrict__ trr = sTr[w];
   double* __restrict__ cr = sC[w];
   const bool vin = A.vin != 0;
+  const int WB = M < CX_BB ? M : CX_BB;   // Bollinger window under the history cap
 
   if (lane < CX_HS) {
-    pc[CXS(lane)] = 0.0;
-    pt[CXS(lane)] = 0.0;
+    trr[CXS(lane)] = 0.0;
     cr[CXS(lane)] = qnan();
   }
   // tile carries (wave-uniform): candle t0 - 1 (and close t0 - 2), run starts, EMA states
   double c1c = qnan(), c2c = qnan(), hc = qnan(), lc = qnan();
   int rcC = -1, rtC = -1;
   double ecar[2] = {0.0, 0.0}, lcar[2] = {0.0, 0.0};
+  // the scans' lane-constant powers: A^(4 lane) and the row-carry factor
+  double lpow[2], rpow[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    lpow[e] = pow_bits<6>(A.apow[e], lane);
+    rpow[e] = pow_bits<5>(A.apow[e], (lane & 15) + 1);
+  }
   wave_sync();
 
   for (int t0 = 0; t0 < T; t0 += CX_TT) {
@@ -126,10 +141,12 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
     cx_load(rH, tb, T, vin, h);
     cx_load(rL, tb, T, vin, l);
     cx_load(rC, tb, T, vin, c);
+    if (A.lag20 || A.lag50) {
 #pragma unroll
-    for (int k = 0; k < CX_K; ++k) {   // lagged closes c[t - M + 1] (0 before the row starts)
-      const int s = tb + k - (M - 1);
-      xl[k] = (s >= 0 && s < T) ? rC[s] : 0.0;
+      for (int k = 0; k < CX_K; ++k) {   // lagged closes c[t - M + 1] (0 before the row starts)
+        const int s = tb + k - (M - 1);
+        xl[k] = (s >= 0 && s < T) ? rC[s] : 0.0;
+      }
     }
 
     double p1 = dpp_f64<DPP_WAVE_SHR1>(c[CX_K - 1]);
@@ -142,9 +159,6 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
       ph = hc;
       pl = lc;
     }
-#pragma unroll
-    for (int k = 0; k < CX_K; ++k) cr[CXS(qb + k)] = c[k];
-
     double tr[CX_K];
     int lcc[CX_K], lct[CX_K];
     {
@@ -163,26 +177,10 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         cp = c[k];
       }
     }
-    // prefix sums of close and true range (double-double, rounded once)
-    {
-      dd tc = {0.0, 0.0}, tt = {0.0, 0.0};
 #pragma unroll
-      for (int k = 0; k < CX_K; ++k) {
-        tc = dd_add1(tc, c[k]);
-        tt = dd_add1(tt, tr[k]);
-      }
-      const dd ic = wave_scan_dd_dpp(tc, lane), it = wave_scan_dd_dpp(tt, lane);
-      const double a0 = dpp_f64<DPP_WAVE_SHR1>(ic.hi), a1 = dpp_f64<DPP_WAVE_SHR1>(ic.lo);
-      const double b0 = dpp_f64<DPP_WAVE_SHR1>(it.hi), b1 = dpp_f64<DPP_WAVE_SHR1>(it.lo);
-      dd bc = lane == 0 ? dd{0.0, 0.0} : dd{a0, a1};
-      dd bt = lane == 0 ? dd{0.0, 0.0} : dd{b0, b1};
-#pragma unroll
-      for (int k = 0; k < CX_K; ++k) {
-        bc = dd_add1(bc, c[k]);
-        bt = dd_add1(bt, tr[k]);
-        pc[CXS(qb + k)] = dd_round(bc);
-        pt[CXS(qb + k)] = dd_round(bt);
-      }
+    for (int k = 0; k < CX_K; ++k) {
+      cr[CXS(qb + k)] = c[k];
+      trr[CXS(qb + k)] = tr[k];
     }
     // run starts: exclusive wave max (+1 so DPP's zero fill is the identity) and the tile carry
     {
@@ -196,9 +194,10 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         lct[k] = max(lct[k], et);
       }
     }
-    // EMA 20 / 50: full-history Y (candle 0 starts it) and the lagged chain
-    // Y_s at s = t - M + 1 (candle 0 starts it M - 1 candles later), each an
-    // affine wave scan + the exact pandas replay of the lane's 4 steps
+    // EMA 20 / 50: full-history Y (candle 0 starts it), an affine wave scan +
+    // the exact pandas replay of the lane's 4 steps; for the history cap the
+    // lagged chain Y_s at s = t - M + 1 (candle 0 starts it M - 1 candles
+    // later) where its weight a^(M-1) matters (host: A.lag*)
     double Y[2][CX_K], D[2][CX_K];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -207,9 +206,9 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         double y = 0.0;
 #pragma unroll
         for (int k = 0; k < CX_K; ++k) y = (tb + k == 0) ? c[k] : fma(A.lin_a[e], y, A.lin_b[e] * c[k]);
-        const double inc = wave_scan_affine_dpp(y, A.apow[e], lane);
+        const double inc = wave_scan_affine_dpp_rp(y, A.apow[e], rpow[e], lane);
         const double ex = dpp_f64<DPP_WAVE_SHR1>(inc);
-        double v = lane == 0 ? ecar[e] : fma(pow_bits<6>(A.apow[e], lane), ecar[e], ex);
+        double v = lane == 0 ? ecar[e] : fma(lpow[e], ecar[e], ex);
 #pragma unroll
         for (int k = 0; k < CX_K; ++k) {
           const double x = c[k];
@@ -219,14 +218,17 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         }
         ecar[e] = readlane_f64(v, WAVE - 1);
       }
-      {
+      const bool lag = e == 0 ? A.lag20 : A.lag50;
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) D[e][k] = 0.0;
+      if (lag) {
         const int s0 = tb - (M - 1);
         double y = 0.0;
 #pragma unroll
         for (int k = 0; k < CX_K; ++k) y = (s0 + k == 0) ? xl[k] : fma(A.lin_a[e], y, A.lin_b[e] * xl[k]);
-        const double inc = wave_scan_affine_dpp(y, A.apow[e], lane);
+        const double inc = wave_scan_affine_dpp_rp(y, A.apow[e], rpow[e], lane);
         const double ex = dpp_f64<DPP_WAVE_SHR1>(inc);
-        double v = lane == 0 ? lcar[e] : fma(pow_bits<6>(A.apow[e], lane), lcar[e], ex);
+        double v = lane == 0 ? lcar[e] : fma(lpow[e], lcar[e], ex);
 #pragma unroll
         for (int k = 0; k < CX_K; ++k) {
           const int s = s0 + k;
@@ -238,33 +240,82 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         lcar[e] = readlane_f64(v, WAVE - 1);
       }
     }
-    wave_sync();   // the rings (close, prefixes) of every lane are visible
+    wave_sync();   // the rings (close, true range) of every lane are visible
 
-    // ---- features (bq_market.hip features_kernel, same operations) -----------
-    double fr[CX_K], fe20[CX_K], fe50[CX_K], ftr[CX_K], fap[CX_K], fbw[CX_K];
-    const bool steady = M >= CX_BB && tb >= CX_BB - 1;
-    double bmid[CX_K], bacc[CX_K];
-    if (steady) {
+    // ---- features (_compute_symbol_features, :244-297) ------------------------
+    // ATR = TR.rolling(14, min_periods=1).mean(), BB = rolling(20, min_periods=1)
+    // mean / std(ddof=0) over the history cap: sliding window sums per lane
+    // (the BB sums about a lane-local reference, no cancellation); windows
+    // still short of their length (the row's first 19 candles) re-sum
+    // directly; pandas' constant-window rule from the run starts.
+    double atr[CX_K], mid[CX_K], sd[CX_K];
+    if (tb >= CX_BB - 1 && WB == CX_BB) {   // every candle of the lane has full windows
+      {
+        double a[CX_ATR - 1];
 #pragma unroll
-      for (int k = 0; k < CX_K; ++k) {
-        bmid[k] = div_count(pc[CXS(qb + k)] - pc[CXS(qb + k - CX_BB)], (double)CX_BB, 1.0 / CX_BB);
-        bacc[k] = 0.0;
-      }
+        for (int i = 0; i < CX_ATR - 1; ++i) a[i] = trr[CXS(qb - (CX_ATR - 1) + i)];
+        double Sx = 0.0;
 #pragma unroll
-      for (int m = 0; m < CX_BB + CX_K - 1; ++m) {
-        const double v = cr[CXS(qb - (CX_BB - 1) + m)];
+        for (int i = 0; i < CX_ATR - 1; ++i) Sx += a[i];
 #pragma unroll
         for (int k = 0; k < CX_K; ++k) {
-          if (m - k >= 0 && m - k < CX_BB) {
-            const double d = v - bmid[k];
-            bacc[k] = fma(d, d, bacc[k]);
-          }
+          Sx = k == 0 ? Sx + tr[0] : (Sx + tr[k]) - a[k - 1];
+          atr[k] = div_count(Sx < 0.0 ? 0.0 : Sx, (double)CX_ATR, 1.0 / CX_ATR);
         }
       }
+      {
+        const double r = c[0];
+        double d0[CX_K - 1];
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < CX_BB - 1; ++i) {
+          const double d = cr[CXS(qb - (CX_BB - 1) + i)] - r;
+          if (i < CX_K - 1) d0[i] = d;
+          s1 += d;
+          s2 = fma(d, d, s2);
+        }
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+          const double dn = c[k] - r;
+          if (k == 0) {
+            s1 += dn;
+            s2 = fma(dn, dn, s2);
+          } else {
+            const double dol = d0[k - 1];
+            s1 = (s1 + dn) - dol;
+            s2 = fma(-dol, dol, fma(dn, dn, s2));
+          }
+          const double m1 = s1 * (1.0 / CX_BB);
+          const double var = fma(-m1, s1, s2) * (1.0 / CX_BB);
+          mid[k] = r + m1;
+          sd[k] = sqrt_nr(var > 0.0 ? var : 0.0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        const int t = tb + k, q = qb + k;
+        const int n = min(t + 1, M);
+        const int ma = min(CX_ATR, n), mb = min(WB, n);
+        double Sx = 0.0;
+        for (int i = q - ma + 1; i <= q; ++i) Sx += trr[CXS(i)];
+        atr[k] = (Sx < 0.0 ? 0.0 : Sx) / (double)ma;
+        double m = 0.0;
+        for (int i = q - mb + 1; i <= q; ++i) m += cr[CXS(i)];
+        m = m / (double)mb;
+        double acc = 0.0;
+        for (int i = q - mb + 1; i <= q; ++i) {
+          const double d = cr[CXS(i)] - m;
+          acc = fma(d, d, acc);
+        }
+        mid[k] = m;
+        sd[k] = sqrt(acc / (double)mb);
+      }
     }
+    double fr[CX_K], fe20[CX_K], fe50[CX_K], ftr[CX_K], fap[CX_K], fbw[CX_K];
 #pragma unroll
     for (int k = 0; k < CX_K; ++k) {
-      const int t = tb + k, q = qb + k;
+      const int t = tb + k;
       const int n = min(t + 1, M);
       if (n < 2) {   // history.empty or len < 2 -> None (:248-249)
         fr[k] = fe20[k] = fe50[k] = ftr[k] = fap[k] = fbw[k] = qnan();
@@ -277,38 +328,19 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         e20 = e20 - A.corr[0] * D[0][k];
         e50 = e50 - A.corr[1] * D[1][k];
       }
-      const int ma = min(CX_ATR, n);
-      double atr;
-      if (lct[k] <= t - ma + 1) atr = tr[k];
-      else {
-        double Sx = pt[CXS(q)] - pt[CXS(q - ma)];
-        Sx = Sx < 0.0 ? 0.0 : Sx;
-        atr = steady ? div_count(Sx, (double)CX_ATR, 1.0 / CX_ATR) : Sx / (double)ma;
+      const double a = lct[k] <= t - min(CX_ATR, n) + 1 ? tr[k] : atr[k];
+      double m = mid[k], s = sd[k];
+      if (lcc[k] <= t - min(WB, n) + 1) {
+        m = cl;
+        s = 0.0;
       }
-      const int mb = min(CX_BB, n);
-      double mid, sd;
-      if (lcc[k] <= t - mb + 1) {
-        mid = cl;
-        sd = 0.0;
-      } else if (steady) {
-        mid = bmid[k];
-        sd = sqrt(div_count(bacc[k], (double)CX_BB, 1.0 / CX_BB));
-      } else {
-        mid = (pc[CXS(q)] - pc[CXS(q - mb)]) / (double)mb;
-        double acc = 0.0;
-        for (int i = q - mb + 1; i <= q; ++i) {
-          const double d = cr[CXS(i)] - mid;
-          acc = fma(d, d, acc);
-        }
-        sd = sqrt(acc / (double)mb);
-      }
-      const double up = mid + (2.0 * sd), lo = mid - (2.0 * sd);
-      fr[k] = safe_pct(cl, prev);
+      const double up = m + (2.0 * s), lo = m - (2.0 * s);
+      fr[k] = prev == 0.0 ? 0.0 : cx_div(cl - prev, prev);   // safe_pct (shared/utils.py:20-23)
       fe20[k] = e20;
       fe50[k] = e50;
-      ftr[k] = e50 != 0.0 ? (e20 - e50) / fabs(e50) : 0.0;
-      fap[k] = cl != 0.0 ? atr / cl : 0.0;
-      fbw[k] = mid != 0.0 ? (up - lo) / fabs(mid) : 0.0;
+      ftr[k] = e50 != 0.0 ? cx_div(e20 - e50, e50 < 0.0 ? -e50 : e50) : 0.0;
+      fap[k] = cl != 0.0 ? cx_div(a, cl) : 0.0;
+      fbw[k] = m != 0.0 ? cx_div(up - lo, m < 0.0 ? -m : m) : 0.0;
     }
     // the last timestamp's feature row, when asked (the context's symbol_features)
     if (live && tb <= T - 1 && T - 1 < tb + CX_K) {
@@ -389,11 +421,9 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
 
     if (t0 + CX_TT >= T) break;
     wave_sync();   // every lane's reads of this tile's rings are done
-    if (lane < CX_HS) {   // short halos; prefixes re-based to the tile end
+    if (lane < CX_HS) {   // short halos
       const int src = CX_TT + lane;
-      const double bc = pc[CXS(CX_RS - 1)], bt = pt[CXS(CX_RS - 1)];
-      pc[CXS(lane)] = pc[CXS(src)] - bc;
-      pt[CXS(lane)] = pt[CXS(src)] - bt;
+      trr[CXS(lane)] = trr[CXS(src)];
       cr[CXS(lane)] = cr[CXS(src)];
     }
     wave_sync();
@@ -567,6 +597,10 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
     for (int k = 0; k < max_bars - 1; ++k) cp *= A.lin_a[e];
     A.corr[e] = cp;
   }
+  A.lag20 = A.corr[0] >= 1e-15;
+  A.lag50 = A.corr[1] >= 1e-15;
+  if (!A.lag20) A.corr[0] = 0.0;
+  if (!A.lag50) A.corr[1] = 0.0;
   char* ws = (char*)workspace;
   for (int f = 0; f < 4; ++f) A.gsum[f] = (double*)(ws + L.off_sum[f]);
   A.gcnt = (uint16_t*)(ws + L.off_cnt);

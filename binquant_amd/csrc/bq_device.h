@@ -178,6 +178,24 @@ __device__ __forceinline__ double wave_scan_affine_dpp(double b, const double* a
   return b;
 }
 
+// wave_scan_affine_dpp with the lane-constant row-carry factor
+// rp = pow_bits<5>(apow, (lane & 15) + 1) computed once by the caller
+__device__ __forceinline__ double wave_scan_affine_dpp_rp(double b, const double* apow, double rp, int lane) {
+  b = fma(apow[0], dpp_f64<DPP_ROW_SHR1>(b), b);
+  b = fma(apow[1], dpp_f64<DPP_ROW_SHR2>(b), b);
+  b = fma(apow[2], dpp_f64<DPP_ROW_SHR4>(b), b);
+  b = fma(apow[3], dpp_f64<DPP_ROW_SHR8>(b), b);
+  const double c1 = readlane_f64(b, 15);
+  const double c2 = fma(apow[4], c1, readlane_f64(b, 31));
+  const double c3 = fma(apow[4], c2, readlane_f64(b, 47));
+  const int row = lane >> 4;
+  if (row > 0) {
+    const double c = row == 1 ? c1 : (row == 2 ? c2 : c3);
+    b = fma(rp, c, b);
+  }
+  return b;
+}
+
 // ---- element-wise restatements of the pandas formulas ----------------------
 // delta.where(delta > 0, 0): NaN -> 0   (coinrule/bb_extreme_reversion.py:145)
 __device__ __forceinline__ double gain_of(double d) { return d > 0.0 ? d : 0.0; }

