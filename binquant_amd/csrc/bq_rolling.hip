@@ -294,7 +294,7 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
 // divide of the mean), not in a shortage of waves.
 // staged values per lane and chunk: 16 for the class kernels, 8 for the
 // all-classes kernel (its register footprint then allows 2 waves per SIMD
-// instead of 1; measured tools/pipe_ab.sh: failed-spike replay 3.6 -> 3.2 ms,
+// instead of 1; measured an A/B harness of rounds 1-2 (tools/pipe_ab.sh, removed in round 3: git history): failed-spike replay 3.6 -> 3.2 ms,
 // while the class kernels are faster with 16)
 #ifndef BQ_RS_V
 #define BQ_RS_V 16
@@ -1197,7 +1197,7 @@ int replay_impl(int nclasses, int64_t waves64) {
                                              : -1);
   }();
   if (forced >= 0) return forced;
-  // mixed classes: one launch (measured, tools/replay_ab.sh, identical
+  // mixed classes: one launch (measured, an A/B harness of rounds 1-2 (tools/replay_ab.sh, removed in round 3: git history), identical
   // digests: 1000 x 400 batch16 0.18 vs 0.33 ms per class; 12.5k x 2k
   // batch16 2.69 vs 2.87 ms — the classes' replays overlap instead of
   // running one after the other)
@@ -1210,7 +1210,7 @@ int replay_impl(int nclasses, int64_t waves64) {
 // not shorten the replay even for small batches — ADX's 3 series over 12.5k
 // symbols (588 waves of 64) took 1.12 ms at 64 and 1.49 ms at 16 symbols per
 // wave: the step cost is the wave's own instruction stream, not a shortage of
-// waves — tools/spw_ab.sh, tools/replay_ab.sh).
+// waves — an A/B harness of rounds 1-2 (tools/spw_ab.sh, removed in round 3: git history), an A/B harness of rounds 1-2 (tools/replay_ab.sh, removed in round 3: git history)).
 int replay_spw(int64_t waves64) {
   static const int forced = [] {
     const char* e = getenv("BQ_REPLAY_SPW");
@@ -1303,7 +1303,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     (void)lds_opt_in;
     // re-staging kernels: class-specialised when the batch has one class,
     // the mixed kernel otherwise (the LDS ring kernel only when forced;
-    // measured: tools/replay_ab.sh, identical outputs)
+    // measured: an A/B harness of rounds 1-2 (tools/replay_ab.sh, removed in round 3: git history), identical outputs)
     int ncls[4] = {0, 0, 0, 0};
     for (int i = 0; i < nrep; ++i) ++ncls[replay_class(rep.j[i].mode)];
     const int nclasses = (ncls[0] > 0) + (ncls[1] > 0) + (ncls[2] > 0) + (ncls[3] > 0);

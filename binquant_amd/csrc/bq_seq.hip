@@ -34,7 +34,7 @@ namespace bq {
 #define BQ_ST_CT 8
 #endif
 // candles per staged chunk (the global loads in flight per wave): 8 measured
-// 0.836 ms against 0.880 at 16 and 0.910 at 4 (12.5k x 2k, tools/st_ab.sh) —
+// 0.836 ms against 0.880 at 16 and 0.910 at 4 (12.5k x 2k, an A/B harness of rounds 1-2 (tools/st_ab.sh, removed in round 3: git history)) —
 // the loading wave's prefetch registers shrink by half and the band wave
 // starts a chunk sooner
 constexpr int ST_CT = BQ_ST_CT;
