@@ -14,7 +14,7 @@ LIB       := binquant_amd/lib/libbinquant_amd.so
 
 all: $(LIB)
 
-build/%.o: binquant_amd/csrc/%.hip binquant_amd/csrc/bq_device.h binquant_amd/csrc/bq_fused_jit.h include/binquant_amd.h
+build/%.o: binquant_amd/csrc/%.hip $(wildcard binquant_amd/csrc/*.h) include/binquant_amd.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -405,8 +405,10 @@ def bench_live(args, dev):
     ins = [p[k] for k in ("open", "high", "low", "close", "volume")]
     pipes = {
         "a17_activity_burst": (lambda o, h, l, c, v: strategies.activity_burst_features(o, h, l, c, v, v * c), 9.1),
-        "a18_pump_score": (lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0]), 9.8),
-        "a19_failed_spike": (lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c), 24.3),
+        "a18_pump_score": (lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0], exact=True),
+                           9.8),
+        "a19_failed_spike": (lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c, exact=True),
+                             24.3),
         "a20_top_gainer": (lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c), None),
     }
     out = {"workload": f"{S} symbols x {T}-bar frames (one message cohort)"}

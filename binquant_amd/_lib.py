@@ -156,6 +156,8 @@ class BqRollJob(ctypes.Structure):
         ("q", ctypes.c_double),
         ("alpha", ctypes.c_double),
         ("rows", ctypes.c_int64),
+        ("panel", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

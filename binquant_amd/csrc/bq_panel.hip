@@ -1,0 +1,349 @@
+// Time-parallel ("panel mode") rolling sums / means and ewm (gfx950) for the
+// strategy pipelines of SURVEY §8a a17-a19 on a [S][T] panel, at the
+// north_star tolerance (1e-9 of pandas) instead of the bit-exact replay:
+//
+//   x.shift(shift).rolling(window, min_periods).sum() / .mean()
+//       strategies/failed_spike_fade.py:260-318, liquidation_sweep_pump.py:220
+//   x.ewm(alpha, adjust=False, min_periods).mean()
+//       strategies/liquidation_sweep_pump.py:215-217, 252-253, 265-266
+//
+// The exact replays of bq_rolling.hip are lane = symbol, sequential along T:
+// 12.5k symbols are 196 waves per series for 1 024 SIMDs, each a 2 000-step
+// dependent chain. Here one 256-thread workgroup per (row, series) walks the
+// row in tiles of 2 048 candles (8 per lane, 64-byte loads, the next tile in
+// flight), the values in an LDS ring with a 128-candle halo (window + shift
+// <= 128), lane-interleaved (conflict-free):
+//
+// * sum / mean: one sliding walk per lane (window + 8 ring reads per 8
+//   outputs), NaN skipped with pandas' observation count and min_periods, the
+//   same-value rule (the window's values all equal -> the value itself, x
+//   nobs for sums) from the run starts of the row (a block max-scan of the
+//   last index where the value changed) — a window holding a NaN compares its
+//   values directly — and calc_mean's sign rule from sliding negative counts;
+// * ewm: an associative scan of the affine maps y -> la y + lb x (wave
+//   shuffles, LDS across waves, a tile carry), then each lane replays its 8
+//   steps with pandas' update (weighted = old_wt w + alpha x, / (old_wt +
+//   alpha), skipped when w == x). A row with a missing or infinite value
+//   continues serially from the first tile that holds one with pandas' own
+//   recursion (gap decay of the old weight, the observation count, a late
+//   first observation): exact, and only such rows pay for it.
+//
+// Values agree with pandas to rounding (the replay's Kahan / online sums are
+// not reproduced bit for bit); bq_rolling_batch keeps the replays for
+// bq_roll_job.panel == 0 (the live path and every bit-exact test).
+#include "bq_panel.h"
+
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+namespace bq {
+
+constexpr int PN_NT = 256;
+constexpr int PN_NW = PN_NT / WAVE;
+constexpr int PN_K = 8;
+constexpr int PN_TT = PN_NT * PN_K;   // 2048
+constexpr int PN_H = 128;             // >= window + shift
+constexpr int PN_R = PN_H + PN_TT;    // 2176
+constexpr int PN_Q = PN_R / PN_K;     // 272
+
+__device__ __forceinline__ int pn_slot(int p) { return (p & (PN_K - 1)) * PN_Q + (p >> 3); }
+
+typedef double pn_dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void pn_load(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[PN_K]) {
+  if (vec && tb + PN_K <= T) {
+    const pn_dbl2* p = reinterpret_cast<const pn_dbl2*>(row + tb);
+#pragma unroll
+    for (int j = 0; j < PN_K / 2; ++j) {
+      const pn_dbl2 a = p[j];
+      x[2 * j] = a.x;
+      x[2 * j + 1] = a.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) x[k] = tb + k < T ? row[tb + k] : qnan();
+  }
+}
+
+__device__ __forceinline__ bool pn_aligned(const void* p, int64_t ld) { return (((uintptr_t)p) & 15u) == 0 && (ld % 2) == 0; }
+
+// exclusive block max of a per-lane int >= -1 combined with `carry`
+__device__ __forceinline__ int pn_block_excl_max(int v, int carry, int* sW, int lane, int w) {
+  const int inc = wave_scan_max_dpp(v + 1, lane) - 1;
+  if (lane == WAVE - 1) sW[w] = inc;
+  const int lpre = dpp_i32<DPP_WAVE_SHR1>(inc + 1) - 1;
+  __syncthreads();
+  int c = max(carry, lpre);
+  for (int u = 0; u < w; ++u) c = max(c, sW[u]);
+  return c;
+}
+
+// ---- sum / mean -----------------------------------------------------------------------
+__global__ __launch_bounds__(PN_NT) void panel_window_kernel(const PanelBatch B) {
+  __shared__ double sX[PN_R];
+  __shared__ int sL[PN_R];   // run start (last index where the value changed) per ring position
+  __shared__ int sW[PN_NW];
+  __shared__ int sCar;
+  const PanelJob& A = B.j[blockIdx.y];
+  const int64_t row = blockIdx.x;
+  if (row >= A.rows) return;   // the job's own row count (a benchmark row): uniform per block
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const double* __restrict__ x = A.x + row * A.ld_in;
+  double* __restrict__ out = A.out + row * A.ld_out;
+  const int T = B.T, win = A.win, sh = A.shift, minp = A.minp;
+  const bool mean = A.mode == BQ_ROLL_MEAN;
+  const bool vin = pn_aligned(A.x, A.ld_in), vout = pn_aligned(A.out, A.ld_out);
+  if (tid < PN_H) {   // before the row: missing values
+    sX[pn_slot(tid)] = qnan();
+    sL[pn_slot(tid)] = -1;
+  }
+  if (tid == 0) sCar = -1;
+  double nx[PN_K];
+  pn_load(x, PN_K * tid, T, vin, nx);
+  for (int t0 = 0; t0 < T; t0 += PN_TT) {
+    const int tb = t0 + PN_K * tid, pb = PN_H + PN_K * tid;
+    double c[PN_K];
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
+    const double pc0 = tb >= 1 && tb <= T ? x[tb - 1] : qnan();
+    if (t0 + PN_TT < T) pn_load(x, tb + PN_TT, T, vin, nx);
+    // run starts of the values (NaN counts as a change)
+    int lcl[PN_K];
+    {
+      double pv = pc0;
+      int run = -1;
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) {
+        if (tb + k == 0 || !(c[k] == pv)) run = tb + k;
+        lcl[k] = run;
+        pv = c[k];
+      }
+      const int carry = pn_block_excl_max(lcl[PN_K - 1], sCar, sW, lane, w);
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) lcl[k] = max(lcl[k], carry);
+    }
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) {
+      sX[pn_slot(pb + k)] = c[k];
+      sL[pn_slot(pb + k)] = lcl[k];
+    }
+    __syncthreads();
+    // window of output t = tb + k: ring positions [pb + k - sh - win + 1, pb + k - sh]
+    double s = 0.0;
+    int nobs = 0, neg = 0;
+    const int e0 = pb - sh;   // position of the entering value of output k = 0
+    for (int j = 1 - win; j <= 0; ++j) {
+      const double v = sX[pn_slot(e0 + j)];
+      const bool ok = v == v;
+      s += ok ? v : 0.0;
+      nobs += ok;
+      neg += ok && signbit(v);
+    }
+    double res[PN_K];
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) {
+      const int e = e0 + k;   // entering position
+      if (k > 0) {
+        const double vi = sX[pn_slot(e)], vo = sX[pn_slot(e - win)];
+        const bool oi = vi == vi, oo = vo == vo;
+        s = (s + (oi ? vi : 0.0)) - (oo ? vo : 0.0);
+        nobs += (int)oi - (int)oo;
+        neg += (int)(oi && signbit(vi)) - (int)(oo && signbit(vo));
+      }
+      double r;
+      if (!mean && nobs == 0 && minp == 0) r = 0.0;
+      else if (nobs < minp || nobs <= 0) r = qnan();
+      else {
+        // pandas' same-value rule: every value of the window equal to the last one
+        bool same;
+        double last;
+        if (nobs == win) {   // no missing value: the run start decides
+          last = sX[pn_slot(e)];
+          same = sL[pn_slot(e)] <= tb + k - sh - win + 1;
+        } else {             // missing values: compare the observed ones directly
+          last = qnan();
+          same = true;
+          for (int j = 0; j > -win; --j) {
+            const double v = sX[pn_slot(e + j)];
+            if (v != v) continue;
+            if (last != last) last = v;
+            else same = same && v == last;
+          }
+        }
+        if (mean) {
+          r = s / (double)nobs;
+          if (same) r = last;
+          else if (neg == 0 && r < 0.0) r = 0.0;
+          else if (neg == nobs && r > 0.0) r = 0.0;
+        } else {
+          r = same ? last * (double)nobs : s;
+        }
+      }
+      res[k] = r;
+    }
+    store_lines<PN_K>(out, tb, T, vout, res);
+    if (t0 + PN_TT >= T) break;
+    __syncthreads();   // every read of this tile's ring is done
+    if (pb >= PN_TT) {
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) {
+        sX[pn_slot(pb + k - PN_TT)] = c[k];
+        sL[pn_slot(pb + k - PN_TT)] = lcl[k];
+      }
+    }
+    if (tid == PN_NT - 1) sCar = lcl[PN_K - 1];
+  }
+}
+
+// ---- ewm ------------------------------------------------------------------------------
+__global__ __launch_bounds__(PN_NT) void panel_ewm_kernel(const PanelBatch B) {
+  __shared__ double sA[PN_NW], sB[PN_NW];
+  __shared__ double sCarry;
+  __shared__ double sX[PN_TT];   // the serial replay's tile
+  const PanelJob& A = B.j[blockIdx.y];
+  const int64_t row = blockIdx.x;
+  if (row >= A.rows) return;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const double* __restrict__ x = A.x + row * A.ld_in;
+  double* __restrict__ out = A.out + row * A.ld_out;
+  const int T = B.T, minp = A.minp;
+  const bool vin = pn_aligned(A.x, A.ld_in), vout = pn_aligned(A.out, A.ld_out);
+  const double alpha = A.alpha, om = 1.0 - alpha, den = om + alpha;
+  const bool div = den != 1.0;
+  const double la = om / den, lb = alpha / den;
+  if (tid == 0) sCarry = 0.0;
+  bool serial = false;
+  double wv = qnan(), owt = 1.0;   // pandas' state (thread 0) once the row turns serial
+  int nobs = 0;
+  double nx[PN_K];
+  pn_load(x, PN_K * tid, T, vin, nx);
+  for (int t0 = 0; t0 < T; t0 += PN_TT) {
+    const int tb = t0 + PN_K * tid;
+    double c[PN_K];
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
+    if (t0 + PN_TT < T) pn_load(x, tb + PN_TT, T, vin, nx);
+    {
+      int bad = 0;
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) bad |= (tb + k < T) && !(c[k] - c[k] == 0.0);
+      if (__syncthreads_or(bad) && !serial) {
+        serial = true;
+        if (t0 > 0) {   // candles 0 .. t0 - 1 were all observations
+          wv = sCarry;
+          nobs = t0;
+        }
+      }
+    }
+    double res[PN_K];
+    if (serial) {
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) sX[PN_K * tid + k] = c[k];
+      __syncthreads();
+      if (tid == 0) {
+        const int n = min(PN_TT, T - t0);
+        for (int i = 0; i < n; ++i) {
+          const double cur = sX[i];
+          const bool obs = cur == cur;
+          if (t0 + i == 0) {   // pandas: weighted = vals[0], nobs = its observation
+            wv = cur;
+            nobs = obs ? 1 : 0;
+          } else {
+            nobs += obs ? 1 : 0;
+            if (wv == wv) {
+              owt *= om;
+              if (obs) {
+                if (wv != cur) {
+                  wv = owt * wv + alpha * cur;
+                  wv /= owt + alpha;
+                }
+                owt = 1.0;
+              }
+            } else if (obs) {
+              wv = cur;
+            }
+          }
+          sX[i] = nobs >= minp ? wv : qnan();
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) res[k] = sX[PN_K * tid + k];
+      store_lines<PN_K>(out, tb, T, vout, res);
+      if (t0 + PN_TT >= T) break;
+      __syncthreads();
+      continue;
+    }
+    // lane map over its candles from the zero state (candle 0 resets: a = 0, b = x)
+    double a_ = 1.0, b_ = 0.0;
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) {
+      if (tb + k == 0) {
+        a_ = 0.0;
+        b_ = c[k];
+      } else {
+        a_ *= la;
+        b_ = fma(la, b_, lb * c[k]);
+      }
+    }
+    double sa = a_, sb = b_;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const double pa = __shfl_up(sa, d, WAVE), pbv = __shfl_up(sb, d, WAVE);
+      if (lane >= d) {
+        sb = fma(sa, pbv, sb);
+        sa *= pa;
+      }
+    }
+    if (lane == WAVE - 1) {
+      sA[w] = sa;
+      sB[w] = sb;
+    }
+    double ea = __shfl_up(sa, 1, WAVE), eb = __shfl_up(sb, 1, WAVE);
+    if (lane == 0) {
+      ea = 1.0;
+      eb = 0.0;
+    }
+    __syncthreads();
+    double y = sCarry;
+    for (int u = 0; u < w; ++u) y = fma(sA[u], y, sB[u]);
+    y = fma(ea, y, eb);
+    // exact replay of the lane's steps
+#pragma unroll
+    for (int k = 0; k < PN_K; ++k) {
+      const int t = tb + k;
+      const double v = c[k];
+      if (t == 0) y = v;
+      else if (y != v) {
+        y = om * y + alpha * v;
+        if (div) y = y / den;
+      }
+      res[k] = t + 1 >= minp ? y : qnan();
+    }
+    store_lines<PN_K>(out, tb, T, vout, res);
+    if (t0 + PN_TT >= T) break;
+    __syncthreads();
+    if (tid == PN_NT - 1) sCarry = y;
+    __syncthreads();
+  }
+}
+
+bool panel_supported(int mode, int window, int shift) {
+  if (mode == BQ_ROLL_EWM) return true;
+  return (mode == BQ_ROLL_SUM || mode == BQ_ROLL_MEAN) && window >= 1 && shift >= 0 && window + shift <= PN_H;
+}
+
+void launch_panel(const PanelBatch& B, int n, hipStream_t st) {
+  PanelBatch win, ewm;
+  win.S = ewm.S = B.S;
+  win.T = ewm.T = B.T;
+  int nw = 0, ne = 0;
+  for (int i = 0; i < n; ++i) {
+    if (B.j[i].mode == BQ_ROLL_EWM) ewm.j[ne++] = B.j[i];
+    else win.j[nw++] = B.j[i];
+  }
+  if (nw) hipLaunchKernelGGL(panel_window_kernel, dim3((unsigned)B.S, (unsigned)nw), dim3(PN_NT), 0, st, win);
+  if (ne) hipLaunchKernelGGL(panel_ewm_kernel, dim3((unsigned)B.S, (unsigned)ne), dim3(PN_NT), 0, st, ewm);
+}
+
+}  // namespace bq

@@ -48,6 +48,7 @@
 //       segment first rebuilds its window from the w values before it; cheap
 //       for short windows on large panels.
 #include "bq_device.h"
+#include "bq_panel.h"
 #include "binquant_amd.h"
 
 #include <stdlib.h>
@@ -1394,8 +1395,33 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     launch_stencil(b, sten[b], nsten[b], st);
     nsten[b] = 0;
   };
+  PanelBatch pan;
+  memset(&pan, 0, sizeof(pan));
+  pan.S = S;
+  pan.T = (int)T;
+  int npan = 0;
+  auto flush_pan = [&]() {
+    if (!npan) return;
+    launch_panel(pan, npan, st);
+    npan = 0;
+  };
   for (int i = 0; i < n_jobs; ++i) {
     const bq_roll_job& in = jobs[i];
+    if (in.panel && panel_supported(in.mode, in.window, in.shift)) {   // time-parallel (bq_panel.hip)
+      PanelJob& P = pan.j[npan++];
+      P.x = in.x;
+      P.out = in.out;
+      P.ld_in = in.ld_in;
+      P.ld_out = in.ld_out;
+      P.rows = in.rows > 0 ? in.rows : S;
+      P.win = in.window;
+      P.minp = in.min_periods;
+      P.shift = in.shift;
+      P.mode = in.mode;
+      P.alpha = in.alpha;
+      if (npan == PN_MAXJOBS) flush_pan();
+      continue;
+    }
     RollJob J;
     memset(&J, 0, sizeof(J));
     J.x = in.x;
@@ -1461,6 +1487,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       if (nrank[b] == RW_MAXJOBS) flush_rank(b);
     }
   }
+  flush_pan();
   flush_rep();
   flush_ff();
   for (int b = 0; b < 6; ++b) flush_rank(b);

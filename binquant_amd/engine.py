@@ -593,14 +593,17 @@ class Ffill:
 
 
 @device_entry
-def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
+def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
     """Independent Roll / Ewm / Ffill series over one [S, T] shape in as few
     launches as the kernel families allow (bq_rolling_batch): the
     lane-per-symbol replays of different series run side by side instead of
     one launch each. A moment / ewm / ffill series may have fewer rows than
     the panel (e.g. the [1, T] benchmark beside an [S, T] panel): it joins
     the same launch (bq_roll_job.rows) instead of paying a replay walk of
-    its own."""
+    its own. exact=False: sums / means (window + shift <= 128) and ewm run
+    time-parallel (bq_panel.hip, panel mode), within rounding of pandas
+    (1e-9) instead of the bit-exact sequential replay; var / std, order
+    statistics and the rest are unchanged."""
     if not specs:
         return []
     xs = [_check_panel(sp.x, "x") for sp in specs]
@@ -619,6 +622,7 @@ def rolling_many(*specs, stream: torch.cuda.Stream | None = None) -> list[torch.
         j = _lib.BqRollJob()
         j.x, j.out, j.ld_in, j.ld_out = x.data_ptr(), out.data_ptr(), _row_stride(x), T
         j.rows = rows if rows != S else 0
+        j.panel = 0 if exact else 1
         if isinstance(sp, Ffill):
             j.mode = _lib.ROLL_FFILL
         elif isinstance(sp, Ewm):

@@ -146,10 +146,13 @@ class PumpParams:
     score_quantile: float = 0.80
 
 
-def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -> dict[str, torch.Tensor]:
+def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
+                        exact: bool = False) -> dict[str, torch.Tensor]:
     """btc_close: [T] benchmark closes already left-merged onto the panel's
     open_time grid (NaN where the benchmark has no candle), as
-    `result[["open_time"]].merge(btc_by_open_time, how="left")` yields."""
+    `result[["open_time"]].merge(btc_by_open_time, how="left")` yields.
+    exact=True: the ewm / rolling-mean columns by the bit-exact replay (the
+    live path); default: time-parallel within rounding of pandas (panel mode)."""
     p = p or PumpParams()
     H, L, C, V = (F.inp(t) for t in (h, l, c, v))
     prev = F.shift(C, 1)
@@ -159,7 +162,7 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None) -
     atr, vmean, hmax, lmin, e20, e50, cf, bf, be20, be50 = engine.rolling_many(
         E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
         R(h, p.compression_bars, "max", shift=1), R(l, p.compression_bars, "min", shift=1),
-        E(c, span=20), E(c, span=50), FF(c), FF(bench), E(bench, span=20), E(bench, span=50),
+        E(c, span=20), E(c, span=50), FF(c), FF(bench), E(bench, span=20), E(bench, span=50), exact=exact,
     )
     e: dict[str, object] = {}
     e["candidate_atr"] = atr
@@ -230,11 +233,15 @@ class SpikeParams:
     min_price_abs_floor: float = 0.015
 
 
-def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> dict[str, torch.Tensor]:
+def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None,
+                          exact: bool = False) -> dict[str, torch.Tensor]:
     """FailedSpikeFade.detect on an [S, T] panel (one row per symbol's df_15m,
     RangeIndex). Integer columns come back as torch.bool (label_pre /
     label_short_pre likewise); 'volume_cluster_min_ratio' and
-    'price_break_base_threshold' hold the per-symbol auto-calibrated values."""
+    'price_break_base_threshold' hold the per-symbol auto-calibrated values.
+    exact=True: the rolling sums / means by the bit-exact replay (the live
+    path); default: time-parallel within rounding of pandas (panel mode; the
+    rolling std / var stay the replay of pandas' online variance)."""
     p = p or SpikeParams()
     eps = 1e-6
     S, T = c.shape
@@ -275,7 +282,7 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None) -> di
         specs += [R(b["_clip_pos"], cw, "sum"), R(b["_neg"], cw, "sum")]
     if p.price_break_use_dynamic:
         specs.append(R(b["price_change_abs"], 60, "quantile", q=p.price_break_dynamic_q, min_periods=20))
-    res = engine.rolling_many(*specs)
+    res = engine.rolling_many(*specs, exact=exact)
     (price_ma, price_std, volume_ma, volume_std, qv_ma, s8, s20, pc2, pc3, pos5, abs5, bsp_ma, bsp_sd, green,
      red) = res[:15]
     cum_pos, cum_neg = (res[15], res[16]) if cw > 1 else (None, None)

@@ -292,6 +292,10 @@ typedef struct bq_roll_job {
                            /* benchmark series beside the panel); 0 = all S.  */
                            /* Moments / ewm / ffill only: order statistics    */
                            /* need 0 or S.                                     */
+  int32_t panel;           /* 1: sum / mean (window + shift <= 128) and ewm    */
+                           /* time-parallel, within rounding of pandas (1e-9) */
+                           /* instead of the bit-exact sequential replay      */
+  int32_t reserved;
 } bq_roll_job;
 int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream);
 

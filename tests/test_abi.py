@@ -70,7 +70,7 @@ def test_roll_job_rows_validated_without_device():
 
     lib = _lib.load()
     null = ctypes.c_void_p()
-    assert ctypes.sizeof(_lib.BqRollJob) == 72   # the header's bq_roll_job
+    assert ctypes.sizeof(_lib.BqRollJob) == 80   # the header's bq_roll_job (rows, panel, reserved)
 
     def job(mode, rows, **kw):
         j = _lib.BqRollJob()
