@@ -22,8 +22,10 @@ Also reported (same JSON line):
                  time-bounded sample;
   tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
                  latency p50/p99;
-  breadth      — C5 leg (market features + breadth partials + ONE all-reduce
-                 of the [T x 10] partials, tracked count folded in);
+  breadth      — C5 leg: the fused panel context build (bq_context_partials:
+                 features reduced straight into the [T x 10] partials) + ONE
+                 all-reduce of the partials (tracked count folded in), with its
+                 roofline on 24 B/candle and the unfused pair timed beside it;
   rows         — every other SURVEY §8 row on the device at 12 500 x 2 000
                  (HIP-event time per call, algorithmic bytes -> GB/s and
                  fraction of HBM peak) with a bounded CPU timing of the
@@ -317,6 +319,17 @@ def _time_call(fn, reps=3):
     return a.elapsed_time(b) / reps
 
 
+def output_bytes(res) -> int:
+    """Bytes of every tensor a call returns (dicts, tuples, lists walked)."""
+    if isinstance(res, torch.Tensor):
+        return res.numel() * res.element_size()
+    if isinstance(res, dict):
+        return sum(output_bytes(v) for v in res.values())
+    if isinstance(res, (tuple, list)):
+        return sum(output_bytes(v) for v in res)
+    return 0
+
+
 def _cpu_rate(fn, candles_per_call, budget=1.0):
     """Candles/s of a single-core oracle call pattern, time-bounded."""
     n, t0 = 0, time.perf_counter()
@@ -341,28 +354,35 @@ def bench_rows(args, dev):
     btc = c[0].clone()
     ts = (1_700_000_000_000 + 900_000 * torch.arange(T, device=dev, dtype=torch.int64)).expand(S, T).contiguous()
     agg = {"open": "first", "high": "max", "low": "min", "close": "last", "volume": "sum"}
-    # name -> (device call, algorithmic bytes per candle, row reference)
+    # name -> (device call, input bytes read per candle, row reference). The
+    # algorithmic bytes are those inputs read once plus every output the call
+    # returns written once at its dtype (bool columns 1 B, [S] / [T] results
+    # counted too): output_bytes() of the call's own result.
     rows = {
-        "a11_beta_corr": (lambda: engine.beta_corr(c, btc, 50), 8 + 16, "producers/context_evaluator.py:154-194"),
-        "a13_market_features": (lambda: engine.market_features(h, l, c, max_bars=400), 24 + 48,
+        "a11_beta_corr": (lambda: engine.beta_corr(c, btc, 50), 8, "producers/context_evaluator.py:154-194"),
+        "a13_market_features": (lambda: engine.market_features(h, l, c, max_bars=400), 24,
                                 "live_market_context_accumulator.py:244-297"),
-        "a17_activity_burst": (lambda: strategies.activity_burst_features(o, h, l, c, v, qv), 48 + 8 * 23,
+        "a17_activity_burst": (lambda: strategies.activity_burst_features(o, h, l, c, v, qv), 48,
                                "strategies/activity_burst_pump.py:51-158"),
-        "a18_pump_score": (lambda: strategies.pump_score_features(o, h, l, c, v, btc), 40 + 8 * 17,
+        "a18_pump_score": (lambda: strategies.pump_score_features(o, h, l, c, v, btc), 32,
                            "strategies/liquidation_sweep_pump.py:195-269"),
-        "a19_failed_spike": (lambda: strategies.failed_spike_features(o, h, l, c, v, qv), 48 + 8 * 56,
+        "a19_failed_spike": (lambda: strategies.failed_spike_features(o, h, l, c, v, qv), 48,
                              "strategies/failed_spike_fade.py:260-544"),
-        "a20_wilder_rsi": (lambda: signals.wilder_rsi(c), 16, "strategies/mean_reversion_fade.py:88-109"),
-        "a20_adx": (lambda: signals.adx(h, l, c), 32, "strategies/range_bb_rsi_mean_reversion.py:101-122"),
-        "a20_zscore": (lambda: signals.zscore(c), 16, "strategies/range_bb_rsi_mean_reversion.py:124-138"),
-        "supertrend": (lambda: engine.supertrend(h, l, c), 3 * 8 + 1 + 16, "strategies/coinrule/coinrule.py:143"),
+        "a20_wilder_rsi": (lambda: signals.wilder_rsi(c), 8, "strategies/mean_reversion_fade.py:88-109"),
+        "a20_adx": (lambda: signals.adx(h, l, c), 24, "strategies/range_bb_rsi_mean_reversion.py:101-122"),
+        "a20_zscore": (lambda: signals.zscore(c), 8, "strategies/range_bb_rsi_mean_reversion.py:124-138"),
+        "a20_leadership": (lambda: signals.gradual_gainer_leadership(ts, c, ts[0], btc), 16,
+                           "strategies/gradual_gainer_retest.py:131-196"),
+        "supertrend": (lambda: engine.supertrend(h, l, c), 24, "strategies/coinrule/coinrule.py:143"),
         "a9_resample_1h": (lambda: engine.resample(ts, {"open": o, "high": h, "low": l, "close": c, "volume": v},
-                                                   agg, 3_600_000), 48 + 48 / 4, "producers/context_evaluator.py:403-407"),
-        "f4_btc_join_returns": (lambda: engine.join_returns(ts, c, ts[0], btc), 16 + 16,
+                                                   agg, 3_600_000), 48, "producers/context_evaluator.py:403-407"),
+        "f4_btc_join_returns": (lambda: engine.join_returns(ts, c, ts[0], btc), 16,
                                 "producers/context_evaluator.py:161-177"),
     }
-    out = {"workload": f"{S} symbols x {T} candles (synthetic, HBM-resident)"}
-    for name, (fn, bpc, ref) in rows.items():
+    out = {"workload": f"{S} symbols x {T} candles (synthetic, HBM-resident)",
+           "bytes_rule": "inputs read once + every returned output written once at its dtype"}
+    for name, (fn, in_bpc, ref) in rows.items():
+        bpc = in_bpc + output_bytes(fn()) / (S * T)
         ms = _time_call(fn)
         gbs = S * T * bpc / (ms * 1e-3) / 1e9
         out[name] = {"ms": ms, "value": S * T / (ms * 1e-3), "unit": "symbol-candles/s", "GBps": gbs,

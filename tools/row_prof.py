@@ -45,11 +45,28 @@ calls = {
     "supertrend": lambda: engine.supertrend(h, l, c),
     "f4_btc_join_returns": lambda: engine.join_returns(ts, c, ts[0], btc),
 }
+# input bytes read per candle; the algorithmic bytes add every returned output
+# at its dtype (bench.py output_bytes)
+IN = {"enrich": 40, "context": 24, "a9_resample_1h": 48, "a11_beta_corr": 8, "a13_market_features": 24,
+      "a17_activity_burst": 48, "a18_pump_score": 32, "a19_failed_spike": 48, "a20_wilder_rsi": 8, "a20_adx": 24,
+      "a20_zscore": 8, "a20_leadership": 16, "supertrend": 24, "f4_btc_join_returns": 16}
+
+
+def output_bytes(res) -> int:
+    if isinstance(res, torch.Tensor):
+        return res.numel() * res.element_size()
+    if isinstance(res, dict):
+        return sum(output_bytes(v) for v in res.values())
+    if isinstance(res, (tuple, list)):
+        return sum(output_bytes(v) for v in res)
+    return 0
+
+
 fn = calls[name]
 torch.cuda.synchronize()
 time.sleep(0.3)   # a gap in the kernel trace: tools/row_summary.py keeps the kernels after it
-for _ in range(2):
-    fn()
+bpc = IN[name] + output_bytes(fn()) / (S * T)
+fn()
 torch.cuda.synchronize()
 a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 reps = 5   # 7 calls in all: PMC sums are divided by CALLS = 7
@@ -58,4 +75,4 @@ for _ in range(reps):
     fn()
 e.record()
 torch.cuda.synchronize()
-print(f"{name} {S}x{T} ms/call {a.elapsed_time(e) / reps:.4f}", flush=True)
+print(f"{name} {S}x{T} ms/call {a.elapsed_time(e) / reps:.4f} alg_bpc {bpc:.3f}", flush=True)

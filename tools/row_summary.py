@@ -2,7 +2,7 @@
 (from the kernel trace, after the generation gap), their mean durations, and
 the PMC counters per call with the HBM traffic (FETCH_SIZE x 2 on gfx950 for
 16-byte streaming reads, WRITE_SIZE; KiB -> bytes) against the row's
-algorithmic bytes. Writes <dir>/rows_summary.json.
+algorithmic bytes (printed by row_prof.py). Writes <dir>/rows_summary.json.
 
     python tools/row_summary.py <dir> ROW [ROW ...]
 """
@@ -14,14 +14,9 @@ import sys
 from collections import defaultdict
 
 CALLS = 7   # tools/row_prof.py: 2 warm-up + 5 timed calls
-# algorithmic bytes per candle (inputs read once + outputs written once)
-BPC = {
-    "enrich": 152, "context": 24, "a9_resample_1h": 48 + 48 / 4, "a11_beta_corr": 8 + 16,
-    "a13_market_features": 24 + 48, "a17_activity_burst": 48 + 8 * 23, "a18_pump_score": 40 + 8 * 17,
-    "a19_failed_spike": 48 + 8 * 56, "a20_wilder_rsi": 16, "a20_adx": 32, "a20_zscore": 16,
-    "a20_leadership": 16 + 8 + 17, "supertrend": 3 * 8 + 1 + 16, "f4_btc_join_returns": 16 + 16,
-}
-SHAPE = re.compile(r"(\d+)x(\d+) ms/call ([0-9.]+)")
+# algorithmic bytes per candle: printed by tools/row_prof.py (the inputs the
+# row reads once + every output it returns written once at its dtype)
+SHAPE = re.compile(r"(\d+)x(\d+) ms/call ([0-9.]+)(?: alg_bpc ([0-9.]+))?")
 
 
 def trace_kernels(d):
@@ -63,15 +58,16 @@ def main():
         except OSError:
             pass
         S, T, ms = (int(m.group(1)), int(m.group(2)), float(m.group(3))) if m else (None, None, None)
+        bpc = float(m.group(4)) if m and m.group(4) else 0.0
         kern, _ = trace_kernels(d)
         cnt, cnt_k = pmc(d)
         fetch = cnt.get("FETCH_SIZE", 0.0) * 1024 * 2
         write = cnt.get("WRITE_SIZE", 0.0) * 1024
-        alg = BPC.get(row, 0) * S * T if S else None
+        alg = bpc * S * T if S else None
         dev_us = sum(k["per_call_us"] for k in kern.values())
         s = {
             "shape": [S, T], "ms_per_call_hip_events": ms, "kernel_us_per_call": dev_us,
-            "algorithmic_bytes_per_candle": BPC.get(row), "algorithmic_bytes": alg,
+            "algorithmic_bytes_per_candle": bpc, "algorithmic_bytes": alg,
             "traffic_bytes": fetch + write, "fetch_bytes_x2": fetch, "write_bytes": write,
             "traffic_over_algorithmic": (fetch + write) / alg if alg else None,
             "achieved_GBps_alg": alg / (ms * 1e-3) / 1e9 if alg and ms else None,
@@ -82,7 +78,7 @@ def main():
             "counters_per_call_by_kernel": cnt_k,
         }
         summary[row] = s
-        print(f"{row:22s} {S}x{T} {ms if ms else float('nan'):8.3f} ms  alg {BPC.get(row, 0):6.1f} B/c  "
+        print(f"{row:22s} {S}x{T} {ms if ms else float('nan'):8.3f} ms  alg {bpc:6.1f} B/c  "
               f"frac {s['frac_of_8TBps'] or 0:.3f}  traffic/alg {s['traffic_over_algorithmic'] or 0:.2f}  "
               f"valu {s['valu_busy'] or 0:.2f} wait {s['wait_share'] or 0:.2f}")
         for n, k in sorted(kern.items(), key=lambda x: -x[1]["per_call_us"])[:6]:
