@@ -1163,7 +1163,15 @@ void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
 // the walk where the rank is near an end of the window (tile_rank_kernel)
 int tile_group(int w, int mode, double q) {
   if (w <= 65) return 0;
-  const bool central = mode == BQ_ROLL_MEDIAN || (q >= 0.25 && q <= 0.75);
+  // BQ_TILE_SEL=1|0 forces selection / the walk for 128-output tiles (measurement)
+  static const int forced = [] {
+    const char* e = getenv("BQ_TILE_SEL");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0) return forced ? 1 : 2;
+  // central ranks select (measured, tools/tile_sel_ab.sh: w 96 q 0.8 2.64 vs 3.27 ms
+  // a call; w 80 q 0.92 2.70 vs 2.57 — the walk from the top end is short)
+  const bool central = mode == BQ_ROLL_MEDIAN || (q >= 0.2 && q <= 0.8);
   return BQ_RANK_SEL && central ? 1 : 2;
 }
 

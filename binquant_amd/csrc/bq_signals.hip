@@ -24,9 +24,9 @@
 // pandas' rules are kept: constant windows (rolling mean returns the value,
 // var returns 0), min_periods warm-up NaN, the helpers' fillna / where.
 //
-// Missing candles (NaN) follow pandas' rules: z-score / ADX lanes whose
-// sliding sums a NaN entered re-sum their windows directly (finite again once
-// the gap leaves the window); the Wilder RSI row is replayed serially with
+// Missing candles (NaN) follow pandas' rules: the z-score / ADX sliding sums
+// exclude a missing value and count it (NaN while the window holds it, finite
+// again once it has left); the Wilder RSI row is replayed serially with
 // pandas' ewm update from the first tile holding a non-finite close (gap
 // decay, observation count, a late first observation).
 #include "bq_device.h"
@@ -143,11 +143,20 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
       // candles from 0 on; those outputs are warm-up, but the sliding sums
       // must not carry the halo's NaN into the first complete window
       const int gs = SG_H - t0;   // ring position of candle 0
-      const double r = c[0];
+      // a finite lane-local reference (a missing candle is excluded from the
+      // sums and counted: pandas' rolling(w, min_periods=w) is NaN while the
+      // window holds one, z = 0 there, and finite again once it has left)
+      double r = c[0];
+#pragma unroll
+      for (int k = 1; k < SG_K; ++k) r = r == r ? r : c[k];
+      r = r == r ? r : 0.0;
       double s1 = 0.0, s2 = 0.0;
+      int nn = 0;
       auto walk = [&](int x0) {
         const double v = sC[sg_slot(pb + x0)];
-        const double d = v - r;
+        const bool ok = v == v;
+        const double d = ok ? v - r : 0.0;
+        nn += ok ? 0 : 1;
         s1 += d;
         s2 = fma(d, d, s2);
       };
@@ -161,45 +170,23 @@ __global__ __launch_bounds__(SG_NT) void zscore_kernel(const SigArgs A) {
       for (int k = 0; k < SG_K; ++k) {
         const int t = tb + k;
         if (k > 0) {
-          const double dn = c[k] - r;
-          const double dol = pb + k - win >= gs ? sC[sg_slot(pb + k - win)] - r : 0.0;
+          const bool oi = c[k] == c[k];
+          const double dn = oi ? c[k] - r : 0.0;
+          const double vo = pb + k - win >= gs ? sC[sg_slot(pb + k - win)] : r;
+          const bool oo = vo == vo;
+          const double dol = oo ? vo - r : 0.0;
+          nn += (oi ? 0 : 1) - (oo ? 0 : 1);
           s1 = (s1 + dn) - dol;
           s2 = fma(-dol, dol, fma(dn, dn, s2));
         }
         double v = 0.0;
-        if (t >= win - 1 && lcl[k] > t - win + 1) {
+        if (t >= win - 1 && lcl[k] > t - win + 1 && nn == 0) {
           const double var = (s2 - s1 * s1 * A.inv_w) * A.inv_w;
           const double sd = var > 0.0 ? sqrt(var) : 0.0;
           const double mean = r + s1 * A.inv_w;
           if (sd > 0.0 && sd == sd) v = (c[k] - mean) / sd;
         }
         z[k] = v;
-      }
-      // A missing candle (NaN) that entered the sliding sums poisons the
-      // lane's later outputs, although pandas' windows that no longer hold it
-      // are finite again (rolling(w, min_periods=w) is NaN only while the
-      // window holds the gap: z = 0 there). Such lanes re-sum every window
-      // directly, about a reference inside it.
-      if (s1 != s1 || s2 != s2) {
-#pragma unroll
-        for (int k = 0; k < SG_K; ++k) {
-          const int t = tb + k;
-          double v = 0.0;
-          const double rk = c[k];
-          if (t >= win - 1 && lcl[k] > t - win + 1 && rk == rk) {
-            double a1 = 0.0, a2 = 0.0;
-            for (int x = 1 - win; x <= 0; ++x) {
-              const double d = sC[sg_slot(pb + k + x)] - rk;
-              a1 += d;
-              a2 = fma(d, d, a2);
-            }
-            const double var = (a2 - a1 * a1 * A.inv_w) * A.inv_w;
-            const double sd = var > 0.0 ? sqrt(var) : 0.0;
-            const double mean = rk + a1 * A.inv_w;
-            if (sd > 0.0 && sd == sd) v = (c[k] - mean) / sd;
-          }
-          z[k] = v;
-        }
       }
     }
     sg_store(ro, tb, T, A.vout, z);
@@ -293,16 +280,33 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
     // dx of the lane's candles
     double dx[SG_K];
     {
+      // a true range that is NaN (a missing high / low / previous close the
+      // skip-NaN max cannot cover) is excluded from the sliding sum and
+      // counted: pandas' rolling(w).sum() is NaN while the window holds it
+      // (dx = 0) and finite again once it has left
       double st = 0.0, sp = 0.0, sm = 0.0;
+      int nn = 0;
       walk_window<(W > 0)>(1 - win, [&](int x) {
-        st += sTR[sg_slot(pb + x)];
+        const double a = sTR[sg_slot(pb + x)];
+        st += a == a ? a : 0.0;
+        nn += a == a ? 0 : 1;
         sp += sPD[sg_slot(pb + x)];
         sm += sMD[sg_slot(pb + x)];
       });
-      auto dx_of =[&](int k, double a, double p, double m) {
+#pragma unroll
+      for (int k = 0; k < SG_K; ++k) {
         const int t = tb + k;
+        if (k > 0) {
+          const int o = sg_slot(pb + k - win);
+          const double ai = tr[k], ao = sTR[o];
+          st = (st + (ai == ai ? ai : 0.0)) - (ao == ao ? ao : 0.0);
+          nn += (ai == ai ? 0 : 1) - (ao == ao ? 0 : 1);
+          sp = (sp + pd[k]) - sPD[o];
+          sm = (sm + md[k]) - sMD[o];
+        }
         double v = 0.0;
         if (t >= win - 1) {
+          double a = nn ? qnan() : st, p = sp, m = sm;
           if (ltr[k] <= t - win + 1) {   // constant window: value * nobs
             a = tr[k] * (double)win;
             p = pd[k] * (double)win;
@@ -313,39 +317,9 @@ __global__ __launch_bounds__(SG_NT) void adx_kernel(const SigArgs A) {
           v = tot != 0.0 ? 100.0 * fabs(pdi - mdi) / tot : qnan();
           if (v != v) v = 0.0;
         }
-        return v;
-      };
-#pragma unroll
-      for (int k = 0; k < SG_K; ++k) {
-        if (k > 0) {
-          const int o = sg_slot(pb + k - win);
-          st = (st + tr[k]) - sTR[o];
-          sp = (sp + pd[k]) - sPD[o];
-          sm = (sm + md[k]) - sMD[o];
-        }
-        dx[k] = dx_of(k, st, sp, sm);
+        dx[k] = v;
+        sDX[sg_slot(pb + k)] = v;
       }
-      // a true range that is NaN (a missing high / low / previous close the
-      // skip-NaN max cannot cover) poisons the sliding sum for the lane's later
-      // candles, whereas pandas' rolling sum is finite again once the window no
-      // longer holds it: re-sum those lanes' windows directly
-      if (st != st) {
-#pragma unroll
-        for (int k = 0; k < SG_K; ++k) {
-          double a = 0.0, p = 0.0, m = 0.0;
-          if (tb + k >= win - 1) {
-            for (int x = 1 - win; x <= 0; ++x) {
-              const int o = sg_slot(pb + k + x);
-              a += sTR[o];
-              p += sPD[o];
-              m += sMD[o];
-            }
-          }
-          dx[k] = dx_of(k, a, p, m);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < SG_K; ++k) sDX[sg_slot(pb + k)] = dx[k];
     }
     __syncthreads();   // dx of every lane visible
     int ldx[SG_K];
@@ -417,6 +391,8 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
   __shared__ double sA[SG_NW], sB[2][SG_NW];
   __shared__ double sCarry[2];
   __shared__ double sX[SG_TT];   // the serial replay's tile (rows with missing candles)
+  __shared__ double sSt[4];      // its pandas state: avg gain, avg loss, old weight, previous close
+  __shared__ int sNobs;
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const int64_t sym = blockIdx.x;
   const double* __restrict__ rc = A.in[0] + sym * A.ld_in;
@@ -425,11 +401,14 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
   // the scan's per-candle map: y -> la * y + lb * x (la = om / den, lb = alpha / den)
   const double la = A.om / A.den, lb = A.alpha / A.den;
   if (tid < 2) sCarry[tid] = 0.0;
-  // pandas' ewm state (thread 0) once the row turns serial: averages, old
-  // weight, observation count, previous close
+  // pandas' ewm state once the row turns serial (LDS, thread 0): averages,
+  // old weight, previous close, observation count
   bool serial = false;
-  double wg = qnan(), wl = qnan(), owt = 1.0, prev = qnan();
-  int nobs = 0;
+  if (tid == 0) {
+    sSt[0] = sSt[1] = sSt[3] = qnan();
+    sSt[2] = 1.0;
+    sNobs = 0;
+  }
   double nx[SG_K];
   sg_load(rc, SG_K * tid, T, A.vin, nx);
   for (int t0 = 0; t0 < T; t0 += SG_TT) {
@@ -452,11 +431,11 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
       for (int k = 0; k < SG_K; ++k) bad |= (tb + k < T) && !(c[k] - c[k] == 0.0);
       if (__syncthreads_or(bad) && !serial) {
         serial = true;
-        if (t0 > 0) {   // candles 1 .. t0 - 1 were all observations
-          wg = sCarry[0];
-          wl = sCarry[1];
-          nobs = t0 - 1;
-          prev = rc[t0 - 1];
+        if (t0 > 0 && tid == 0) {   // candles 1 .. t0 - 1 were all observations
+          sSt[0] = sCarry[0];
+          sSt[1] = sCarry[1];
+          sSt[3] = rc[t0 - 1];
+          sNobs = t0 - 1;
         }
       }
     }
@@ -465,6 +444,8 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
       for (int k = 0; k < SG_K; ++k) sX[SG_K * tid + k] = c[k];
       __syncthreads();
       if (tid == 0) {
+        double wg = sSt[0], wl = sSt[1], owt = sSt[2], prev = sSt[3];
+        int nobs = sNobs;
         const int n = min(SG_TT, T - t0);
         for (int i = 0; i < n; ++i) {
           const double cur = sX[i];
@@ -498,6 +479,11 @@ __global__ __launch_bounds__(SG_NT) void wilder_rsi_kernel(const SigArgs A) {
           }
           sX[i] = v;
         }
+        sSt[0] = wg;
+        sSt[1] = wl;
+        sSt[2] = owt;
+        sSt[3] = prev;
+        sNobs = nobs;
       }
       __syncthreads();
       double rsi[SG_K];
