@@ -206,6 +206,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_hlc": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
+    "bq_supertrend_panel": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_resample_count": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P]),
     "bq_resample": (ctypes.c_int, [_P, _PP, _P, _I32, _P, _I64, _I64, _I64, _I64, _P, _PP, _I64, _P]),
     "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),

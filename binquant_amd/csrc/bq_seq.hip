@@ -28,6 +28,8 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <stdlib.h>
+
 namespace bq {
 
 #ifndef BQ_ST_CT
@@ -49,6 +51,7 @@ struct StArgs {
   double *upper, *lower;
   int64_t S, ld_in, ld_out;
   int T, period, ring;   // ring: TR slots per lane (period + ST_SUB)
+  int warm;              // panel mode: warm-up candles before a chunk
   double mult, inv_period;
 };
 
@@ -301,11 +304,232 @@ __global__ __launch_bounds__(2 * WAVE) void supertrend_pipe_kernel(const StArgs 
   }
 }
 
+// ---- panel mode: a row per workgroup, chunk walks with verified starts ----
+// The band / trend recursion only remembers (trend, upper, lower), and two
+// walks started from different states meet as soon as both reset their bands
+// (a flip, or close beyond the raw band) — in practice within a few dozen
+// candles (0.44 % of 96-candle warm-ups end in a different state
+// on random-walk panels, 0.07 % at 128). So one 256-thread workgroup takes
+// one symbol's row (T <= STP_MAXT, held in LDS) and thread k the chunk
+// [kC, kC + C) (C = ceil(T / 256) <= 8): it walks from STP_W candles before
+// the chunk, starting from the series-start state (NaN bands, up), keeps the
+// state it reaches at the chunk start (its guess), and its chunk's results in
+// registers. Chunk k is exact iff its guess equals chunk k - 1's end state
+// (chunk 0 starts at the true start, and so does every thread whose warm-up
+// reaches candle 0): all threads compare in parallel, every mismatching chunk
+// re-walks from its predecessor's end state, and the round repeats until no
+// guess differs (each round fixes at least the first wrong chunk; one round
+// in practice). The flags and bands therefore equal the sequential recursion
+// on the same ATR.
+// ATR: per candle, the period's TR values summed directly in time order
+// (pandas' min_periods = period and same-value rule) — a pure function of the
+// window, equal to pandas' Kahan roll_mean to rounding, not bit for bit (exact
+// mode keeps the replay).
+// LDS: close and the raw bands (hl2 and TR on the way), one pad slot per 32
+// candles so the threads' strided walk positions spread over the banks.
+constexpr int STP_NT = 256;
+constexpr int STP_W = 96;
+constexpr int STP_MAXT = 2048;
+constexpr int STP_MAXC = STP_MAXT / STP_NT;   // 8 candles per thread
+__host__ __device__ __forceinline__ int stp_slot(int t) { return t + (t >> 5); }
+__device__ __forceinline__ bool same_bits(double a, double b) { return a == b || (a != a && b != b); }
+
+__device__ __forceinline__ void st_step(bool& up, double& U, double& L, double c, double bu, double bl) {
+  // (the NaN bands of the warm-up compare false and hold `up`)
+  const bool flip_up = c > U, flip_dn = !flip_up & (c < L), hold = !flip_up & !flip_dn;
+  up = flip_up | (!flip_dn & up);
+  bl = (hold & up & (bl < L)) ? L : bl;
+  bu = (hold & !up & (bu > U)) ? U : bu;
+  U = bu;
+  L = bl;
+}
+
+// PC: the period as a compile-time constant (the reference's 10), 0 = run time
+template <int PC>
+__global__ __launch_bounds__(STP_NT) void supertrend_panel_kernel(const StArgs A) {
+  extern __shared__ double sm[];
+  __shared__ double sBU[STP_NT / WAVE], sBL[STP_NT / WAVE];
+  __shared__ int sBup[STP_NT / WAVE];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const int64_t sym = blockIdx.x;
+  const int T = A.T, P = PC > 0 ? PC : A.period, W = A.warm;
+  const double pd = (double)P;
+  const int NS = stp_slot(T - 1) + 1;
+  double* cA = sm;            // close
+  double* uA = sm + NS;       // hl2 -> raw upper band -> final upper
+  double* lA = sm + 2 * NS;   // TR -> raw lower band -> final lower
+  const double* __restrict__ H = A.h + sym * A.ld_in;
+  const double* __restrict__ L = A.l + sym * A.ld_in;
+  const double* __restrict__ Cl = A.c + sym * A.ld_in;
+  const int nj = (T + STP_NT - 1) / STP_NT;
+
+  // ---- row -> LDS (all loads first), TR from the neighbour's close
+  double hv[STP_MAXC], lv[STP_MAXC], cv[STP_MAXC];
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    const bool in = j < nj && t < T;
+    hv[j] = in ? H[t] : qnan();
+    lv[j] = in ? L[t] : qnan();
+    cv[j] = in ? Cl[t] : qnan();
+  }
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    if (j < nj && t < T) {
+      cA[stp_slot(t)] = cv[j];
+      uA[stp_slot(t)] = (hv[j] + lv[j]) / 2.0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    if (j < nj && t < T) lA[stp_slot(t)] = true_range(hv[j], lv[j], t > 0 ? cA[stp_slot(t - 1)] : qnan());
+  }
+  __syncthreads();
+  // ---- ATR (rolling(P).mean(), min_periods = P, the window in time order)
+  double matr[STP_MAXC];
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    matr[j] = qnan();
+    if (j < nj && t < T && t >= P - 1) {
+      const double first = lA[stp_slot(t - P + 1)];
+      double s = 0.0;
+      int n = 0;
+      bool same = true;
+      auto add = [&](int u) {
+        const double v = lA[stp_slot(u)];
+        const bool ok = v == v;
+        s += ok ? v : 0.0;
+        n += ok;
+        same = same && v == first;
+      };
+      if constexpr (PC > 0) {
+#pragma unroll
+        for (int i = 0; i < PC; ++i) add(t - PC + 1 + i);
+      } else {
+        for (int u = t - P + 1; u <= t; ++u) add(u);
+      }
+      matr[j] = A.mult * (n < P ? qnan() : (same ? first : s / pd));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    if (j < nj && t < T) {
+      const double hl2 = uA[stp_slot(t)];
+      uA[stp_slot(t)] = hl2 + matr[j];
+      lA[stp_slot(t)] = hl2 - matr[j];
+    }
+  }
+  __syncthreads();
+
+  // ---- the threads' walks: warm-up, then the chunk (results in registers)
+  const int C = nj;   // ceil(T / 256)
+  const int a = tid * C, b = min(a + C, T);
+  bool up = true, eup = true;
+  double U = qnan(), Lo = qnan(), eU = qnan(), eL = qnan();
+  double fU[STP_MAXC], fL[STP_MAXC];
+  int fup = 0;
+  // rewalk: a re-walk stops where its state meets the recorded one (the rest
+  // of the chunk, and its end state, are then unchanged)
+  auto walk_chunk = [&](bool rewalk) {
+    bool met = false;
+#pragma unroll
+    for (int j = 0; j < STP_MAXC; ++j) {
+      const int t = a + j;
+      if (j < C && t < b && !met) {
+        const int sl = stp_slot(t);
+        st_step(up, U, Lo, cA[sl], uA[sl], lA[sl]);
+        met = rewalk && up == (((fup >> j) & 1) != 0) && same_bits(U, fU[j]) && same_bits(Lo, fL[j]);
+        fU[j] = U;
+        fL[j] = Lo;
+        fup = up ? fup | (1 << j) : fup & ~(1 << j);
+      }
+    }
+    if (met) {   // the end state is the recorded chunk's
+      const int jl = min(C, b - a) - 1;
+#pragma unroll
+      for (int j = 0; j < STP_MAXC; ++j)
+        if (j == jl) {
+          up = ((fup >> j) & 1) != 0;
+          U = fU[j];
+          Lo = fL[j];
+        }
+    }
+  };
+#pragma unroll 4
+  for (int t = max(0, a - W); t < min(a, T); ++t) {
+    const int sl = stp_slot(t);
+    st_step(up, U, Lo, cA[sl], uA[sl], lA[sl]);
+  }
+  eup = up;
+  eU = U;
+  eL = Lo;
+  walk_chunk(false);
+
+  // ---- verify: chunk k's guess against chunk k - 1's end state, in rounds
+  for (;;) {
+    if (lane == WAVE - 1) {
+      sBup[wv] = up;
+      sBU[wv] = U;
+      sBL[wv] = Lo;
+    }
+    __syncthreads();
+    bool pup = __shfl_up((int)up, 1, WAVE) != 0;
+    double pU = __shfl_up(U, 1, WAVE), pL = __shfl_up(Lo, 1, WAVE);
+    if (lane == 0 && wv > 0) {
+      pup = sBup[wv - 1] != 0;
+      pU = sBU[wv - 1];
+      pL = sBL[wv - 1];
+    }
+    const bool wrong = tid > 0 && a > W && a < T && !(eup == pup && same_bits(eU, pU) && same_bits(eL, pL));
+    __syncthreads();   // the boundary states are read before the next round's writes
+    if (!__syncthreads_or(wrong)) break;
+    if (wrong) {
+      up = eup = pup;
+      U = eU = pU;
+      Lo = eL = pL;
+      walk_chunk(true);
+    }
+  }
+
+  // ---- finals -> LDS (own chunk, in place) -> outputs (coalesced)
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = a + j;
+    if (j < C && t < b) {
+      const int sl = stp_slot(t);
+      uA[sl] = fU[j];
+      lA[sl] = fL[j];
+      cA[sl] = (fup >> j) & 1 ? 1.0 : 0.0;
+    }
+  }
+  __syncthreads();
+  double* __restrict__ ou = A.upper ? A.upper + sym * A.ld_out : nullptr;
+  double* __restrict__ ol = A.lower ? A.lower + sym * A.ld_out : nullptr;
+  uint8_t* __restrict__ of = A.up + sym * A.ld_out;
+#pragma unroll
+  for (int j = 0; j < STP_MAXC; ++j) {
+    const int t = j * STP_NT + tid;
+    if (j < nj && t < T) {
+      const int sl = stp_slot(t);
+      if (ou) ou[t] = uA[sl];
+      if (ol) ol[t] = lA[sl];
+      of[t] = cA[sl] != 0.0 ? 1 : 0;
+    }
+  }
+}
+
 }  // namespace bq
 
 namespace {
 int launch_supertrend(bool fatr, const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t period,
-                      double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream) {
+                      double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream,
+                      bool panel = false) {
   using namespace bq;
   if (!in || !up || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff || !(multiplier == multiplier))
     return BQ_EINVAL;
@@ -332,6 +556,20 @@ int launch_supertrend(bool fatr, const double* const* in, int64_t S, int64_t T, 
   A.inv_period = fatr ? 1.0 / (double)period : 0.0;
   A.ring = ring;
   const unsigned blocks = (unsigned)((S + WAVE - 1) / WAVE);
+  if (fatr && panel && T <= STP_MAXT) {   // one workgroup per row, the row in LDS (< 64 KiB)
+    // BQ_ST_WARM: warm-up candles (measurement; any value gives the same outputs)
+    static const int warm = [] {
+      const char* e = getenv("BQ_ST_WARM");
+      return e ? atoi(e) : STP_W;
+    }();
+    A.warm = warm < 0 ? 0 : warm;
+    const size_t lds = (size_t)3 * (stp_slot((int)T - 1) + 1) * sizeof(double);
+    if (period == 10)
+      hipLaunchKernelGGL(supertrend_panel_kernel<10>, dim3((unsigned)S), dim3(STP_NT), lds, (hipStream_t)stream, A);
+    else
+      hipLaunchKernelGGL(supertrend_panel_kernel<0>, dim3((unsigned)S), dim3(STP_NT), lds, (hipStream_t)stream, A);
+    return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+  }
   if (fatr) {
     // > 64 KiB of LDS at the largest periods: opt in once, before any graph
     // capture can be active (first call of the process)
@@ -362,4 +600,10 @@ extern "C" int bq_supertrend_hlc(const double* const* hlc, int64_t S, int64_t T,
                                  double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out,
                                  void* stream) {
   return launch_supertrend(true, hlc, S, T, ld_in, period, multiplier, up, upper, lower, ld_out, stream);
+}
+
+extern "C" int bq_supertrend_panel(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t period,
+                                   double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out,
+                                   void* stream) {
+  return launch_supertrend(true, hlc, S, T, ld_in, period, multiplier, up, upper, lower, ld_out, stream, true);
 }

@@ -704,11 +704,16 @@ def supertrend(
     multiplier: float = 3.0,
     atr: torch.Tensor | None = None,
     stream: torch.cuda.Stream | None = None,
+    exact: bool = False,
 ) -> dict[str, torch.Tensor]:
     """pybinbot Indicators.set_supertrend (strategies/coinrule/coinrule.py:143-160)
     on a [S, T] panel: {"supertrend": bool (uptrend), "supertrend_upper",
-    "supertrend_lower": final bands}. ATR = TR.rolling(period).mean(), formed in
-    the same walk as pandas' roll_mean (bq_supertrend_hlc) unless given."""
+    "supertrend_lower": final bands}. ATR = TR.rolling(period).mean() unless
+    given: exact=True forms it in the same walk as pandas' roll_mean
+    (bq_supertrend_hlc, bit for bit — the live path, Indicators.set_supertrend);
+    the default panel mode (bq_supertrend_panel) walks chunks of each row in
+    parallel with verified chunk starts (the same recursion) on an ATR equal
+    to pandas' to rounding."""
     high = _check_panel(high, "high")
     S, T = high.shape
     low = _check_panel(low, "low", (S, T))
@@ -718,12 +723,17 @@ def supertrend(
     lower = torch.empty_like(upper)
     if atr is None:
         ins = [t.contiguous() for t in (high, low, close)]
-        st = _lib.load().bq_supertrend_hlc(
-            _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, int(period), float(multiplier),
-            ctypes.c_void_p(up.data_ptr()), ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()), T,
-            _stream_handle(stream),
-        )
-        _lib.check(st, "bq_supertrend_hlc")
+        L = _lib.load()
+        args = [_lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, int(period), float(multiplier),
+                ctypes.c_void_p(up.data_ptr()), ctypes.c_void_p(upper.data_ptr()), ctypes.c_void_p(lower.data_ptr()),
+                T]
+        if exact:
+            fn = "bq_supertrend_hlc"
+            st = L.bq_supertrend_hlc(*args, _stream_handle(stream))
+        else:
+            fn = "bq_supertrend_panel"
+            st = L.bq_supertrend_panel(*args, _stream_handle(stream))
+        _lib.check(st, fn)
     else:
         atr = _check_panel(atr, "atr", (S, T))
         ins = [t.contiguous() for t in (high, low, close, atr)]

@@ -148,7 +148,7 @@ class Indicators:
         host = _frame_inputs(df)
         dev = _device()
         h, l, c = (torch.from_numpy(np.ascontiguousarray(x)).to(dev)[None, :] for x in host[1:4])
-        r = engine.supertrend(h, l, c, period=period, multiplier=float(multiplier))
+        r = engine.supertrend(h, l, c, period=period, multiplier=float(multiplier), exact=True)
         for k, v in r.items():
             df[k] = v[0].cpu().numpy()
         return df

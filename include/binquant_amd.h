@@ -346,6 +346,18 @@ int bq_supertrend(const double* const* hlca, int64_t S, int64_t T, int64_t ld_in
  */
 int bq_supertrend_hlc(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t period,
                       double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream);
+/*
+ * bq_supertrend_hlc in panel mode (engine.supertrend(exact=False)): one
+ * workgroup per row, each thread walks a chunk of it from a warm-up, then
+ * every chunk start is verified against its predecessor's end state (the
+ * rare wrong one re-walked), so the flags and bands equal the sequential
+ * recursion on the same ATR; the ATR (TR.rolling(period).mean(), min_periods
+ * = period, same-value rule) is a direct window sum per candle, equal to
+ * pandas' roll_mean to rounding, not bit for bit. Rows longer than 2048
+ * candles run bq_supertrend_hlc.
+ */
+int bq_supertrend_panel(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t period,
+                        double multiplier, uint8_t* up, double* upper, double* lower, int64_t ld_out, void* stream);
 
 /* ---- frame plumbing: resample and timestamp joins (ragged rows) ------------ */
 /* Timestamps are int64 ms, ascending within a row; lens[s] = valid candles of
