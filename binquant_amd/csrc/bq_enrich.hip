@@ -33,6 +33,7 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <stddef.h>
 #include <string.h>
 
 #include <type_traits>
@@ -92,7 +93,36 @@ static_assert(!BQ_EN_LDSPERM || ((1 << EN_LK) == EN_K && EN_R % EN_K == 0), "LX:
 // EMA slots in the scan state
 enum { E_FAST = 0, E_SLOW, E_SIG, E_0, E_1, NE };
 
+// Power of the per-thread state map M^(K n): lower-triangular 3x3 block for
+// (fast, slow, signal) + two scalars.  Applied to v: (a0 v0, a1 v1,
+// p v0 + q v1 + a2 v2, a3 v3, a4 v4).
+struct Pow {
+  double a0, a1, p, q, a2, a3, a4;
+};
+
+__host__ __device__ __forceinline__ Pow pow_mul(const Pow& T, const Pow& U) {   // T after U
+  Pow r;
+  r.a0 = T.a0 * U.a0;
+  r.a1 = T.a1 * U.a1;
+  r.p = fma(T.p, U.a0, T.a2 * U.p);
+  r.q = fma(T.q, U.a1, T.a2 * U.q);
+  r.a2 = T.a2 * U.a2;
+  r.a3 = T.a3 * U.a3;
+  r.a4 = T.a4 * U.a4;
+  return r;
+}
+
+// the EMA constants a launch shares, formed once on the host (ema_consts):
+// pandas' weights per EMA and the powers of the scan's state map
+struct EmaHost {
+  double al[NE], om[NE], den[NE], la[NE], lb[NE];
+  Pow step;            // M (one candle)
+  Pow wstep[6];        // (M^K)^(2^j)
+  Pow wave[EN_NW + 1]; // (M^K)^(64 m)
+};
+
 struct EnrichArgs {
+  EmaHost ema;
   const double* in[BQ_NUM_INPUTS];
   double* out[BQ_NUM_ENRICH_COLS];
   int64_t ld_in, ld_out;
@@ -105,33 +135,54 @@ struct EnrichArgs {
   double inv_ma[3], inv_rsi, inv_bb, inv_bb_dv, inv_atr, inv_twap;   // 1.0 / window (host)
 };
 
-// Power of the per-thread state map M^(K n): lower-triangular 3x3 block for
-// (fast, slow, signal) + two scalars.  Applied to v: (a0 v0, a1 v1,
-// p v0 + q v1 + a2 v2, a3 v3, a4 v4).
-struct Pow {
-  double a0, a1, p, q, a2, a3, a4;
-};
-
-__device__ __forceinline__ Pow pow_mul(const Pow& T, const Pow& U) {   // T after U
-  Pow r;
-  r.a0 = T.a0 * U.a0;
-  r.a1 = T.a1 * U.a1;
-  r.p = fma(T.p, U.a0, T.a2 * U.p);
-  r.q = fma(T.q, U.a1, T.a2 * U.q);
-  r.a2 = T.a2 * U.a2;
-  r.a3 = T.a3 * U.a3;
-  r.a4 = T.a4 * U.a4;
-  return r;
-}
-
+// per-workgroup LDS copy: the host's constants, then the lane powers
 struct EmaConsts {
   double al[NE], om[NE], den[NE], la[NE], lb[NE];
-  int divide[NE];
   Pow step;            // M (one candle)
   Pow wstep[6];        // (M^K)^(2^j)
-  Pow lane[WAVE];      // (M^K)^lane
   Pow wave[EN_NW + 1]; // (M^K)^(64 m)
+  Pow lane[WAVE];      // (M^K)^lane
 };
+static_assert(sizeof(EmaHost) % sizeof(double) == 0 && offsetof(EmaConsts, lane) == sizeof(EmaHost),
+              "EmaConsts begins with EmaHost's layout");
+
+// pandas: comass = (span - 1) / 2, alpha = 1 / (1 + comass); the scan's
+// state map and its powers (host: the same IEEE operations the kernel used to
+// form per workgroup — one thread's serial chain ahead of every row)
+static EmaHost ema_consts(const int (&span)[NE]) {
+  EmaHost E;
+  for (int e = 0; e < NE; ++e) {
+    const double com = ((double)span[e] - 1.0) / 2.0;
+    const double al = 1.0 / (1.0 + com);
+    E.al[e] = al;
+    E.om[e] = 1.0 - al;
+    E.den[e] = E.om[e] + al;
+    E.la[e] = E.om[e] / E.den[e];
+    E.lb[e] = al / E.den[e];
+  }
+  Pow m;
+  m.a0 = E.la[E_FAST];
+  m.a1 = E.la[E_SLOW];
+  m.a2 = E.la[E_SIG];
+  m.p = E.lb[E_SIG] * E.la[E_FAST];
+  m.q = -(E.lb[E_SIG] * E.la[E_SLOW]);
+  m.a3 = E.la[E_0];
+  m.a4 = E.la[E_1];
+  E.step = m;
+  Pow mk = m;
+  for (int k = 1; k < EN_K; ++k) mk = pow_mul(m, mk);
+  for (int j = 0; j < 6; ++j) {
+    E.wstep[j] = mk;
+    mk = pow_mul(mk, mk);
+  }
+  Pow r = {1.0, 1.0, 0.0, 0.0, 1.0, 1.0, 1.0};
+  const Pow w64 = pow_mul(E.wstep[5], E.wstep[5]);   // (M^K)^64
+  for (int k = 0; k <= EN_NW; ++k) {
+    E.wave[k] = r;
+    r = pow_mul(w64, r);
+  }
+  return E;
+}
 
 __device__ __forceinline__ void pow_apply(const Pow& A, const double (&v)[NE], double (&r)[NE]) {
   r[E_FAST] = A.a0 * v[E_FAST];
@@ -339,48 +390,18 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   Tile nx;
   load_tile(A, irow, EN_K * tid, vin, nx);
 
-  // ---- per-workgroup constants (pandas: comass = (span-1)/2, alpha = 1/(1+comass))
-  if (tid == 0) {
-    for (int e = 0; e < NE; ++e) {
-      const double com = ((double)A.span[e] - 1.0) / 2.0;
-      const double al = 1.0 / (1.0 + com);
-      E.al[e] = al;
-      E.om[e] = 1.0 - al;
-      E.den[e] = E.om[e] + al;
-      E.divide[e] = E.den[e] != 1.0;
-      E.la[e] = E.om[e] / E.den[e];
-      E.lb[e] = al / E.den[e];
-    }
-    Pow m;
-    m.a0 = E.la[E_FAST];
-    m.a1 = E.la[E_SLOW];
-    m.a2 = E.la[E_SIG];
-    m.p = E.lb[E_SIG] * E.la[E_FAST];
-    m.q = -(E.lb[E_SIG] * E.la[E_SLOW]);
-    m.a3 = E.la[E_0];
-    m.a4 = E.la[E_1];
-    E.step = m;
-    Pow mk = m;
-    for (int k = 1; k < EN_K; ++k) mk = pow_mul(m, mk);
-    for (int j = 0; j < 6; ++j) {
-      E.wstep[j] = mk;
-      mk = pow_mul(mk, mk);
-    }
+  // ---- per-workgroup constants: the host's (kernel arguments) copied into
+  // LDS in parallel, the lane powers (M^K)^lane formed by the first wave
+  {
+    const double* src = reinterpret_cast<const double*>(&A.ema);
+    double* dst = reinterpret_cast<double*>(&E);
+    for (int i = tid; i < (int)(sizeof(EmaHost) / sizeof(double)); i += EN_NT) dst[i] = src[i];
   }
-  __syncthreads();
   if (tid < WAVE) {
     Pow r = {1.0, 1.0, 0.0, 0.0, 1.0, 1.0, 1.0};
     for (int j = 0; j < 6; ++j)
-      if (tid & (1 << j)) r = pow_mul(E.wstep[j], r);
+      if (tid & (1 << j)) r = pow_mul(A.ema.wstep[j], r);
     E.lane[tid] = r;
-  }
-  if (tid == WAVE) {
-    Pow r = {1.0, 1.0, 0.0, 0.0, 1.0, 1.0, 1.0};
-    const Pow w64 = pow_mul(E.wstep[5], E.wstep[5]);   // (M^K)^64
-    for (int m = 0; m <= EN_NW; ++m) {
-      E.wave[m] = r;
-      r = pow_mul(w64, r);
-    }
   }
   if (tid < NE) sEcar[tid] = 0.0;
   if (tid == 0) {
@@ -905,6 +926,7 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in, cons
   A.span[E_SIG] = P.macd_signal;
   A.span[E_0] = P.ema_spans[0];
   A.span[E_1] = P.ema_spans[1];
+  A.ema = ema_consts(A.span);
 
   // 16-byte vector access needs every row start 16-byte aligned.
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
