@@ -204,6 +204,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_ewm": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _I32, _P, _I64, _P]),
     "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
+    "bq_pump_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _PP, _I32, _I32, _I32, _PP, _I64, _P]),
     "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_hlc": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_panel": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),

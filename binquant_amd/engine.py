@@ -288,6 +288,54 @@ def market_features(
     return out
 
 
+PUMP_COLUMNS = ("candidate_atr", "momentum_3", "relative_volume", "pre_breakout_compression", "pump_score",
+                "prior_high", "close_location", "ema20", "ema50", "trend_score", "momentum_atr", "btc_momentum_3",
+                "btc_trend_score", "relative_strength")
+
+
+@device_entry
+def pump_features(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    volume: torch.Tensor,
+    candidate_atr: torch.Tensor,
+    ema20: torch.Tensor,
+    ema50: torch.Tensor,
+    bench_ffill: torch.Tensor,
+    bench_ema20: torch.Tensor,
+    bench_ema50: torch.Tensor,
+    momentum_bars: int = 3,
+    volume_lookback: int = 20,
+    compression_bars: int = 6,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """LiquidationSweepPump.compute_pump_score's columns but the two rolling
+    quantiles and score_cross (strategies/liquidation_sweep_pump.py:195-268) in
+    one pass per row (bq_pump_features): the volume mean, the high / low
+    windows and the pad-filled pct_change formed in the kernel. The ewm columns
+    (candidate_atr, ema20, ema50) and the benchmark rows ([T]: ffilled close,
+    ewm 20, ewm 50) are inputs."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in
+           zip((high, low, close, volume, candidate_atr, ema20, ema50),
+               ("high", "low", "close", "volume", "candidate_atr", "ema20", "ema50"))]
+    bench = []
+    for t, n in zip((bench_ffill, bench_ema20, bench_ema50), ("bench_ffill", "bench_ema20", "bench_ema50")):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float64 or t.numel() != T:
+            raise ValueError(f"{n}: expected a float64 CUDA tensor of {T} values")
+        bench.append(t.reshape(T).contiguous())
+    out = {n: torch.empty((S, T), dtype=torch.float64, device=close.device) for n in PUMP_COLUMNS}
+    st = _lib.load().bq_pump_features(
+        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, _lib.ptr_array([t.data_ptr() for t in bench]),
+        int(momentum_bars), int(volume_lookback), int(compression_bars),
+        _lib.ptr_array([out[n].data_ptr() for n in PUMP_COLUMNS]), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_pump_features")
+    return out
+
+
 @device_entry
 def breadth_partial(
     close: torch.Tensor,

@@ -134,6 +134,11 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     return {k: out[k] for k in order}
 
 
+# panel mode of pump_score_features through bq_pump_features (False: the staged
+# panel pipeline; tests compare the two)
+_PUMP_FUSED = True
+
+
 @dataclass
 class PumpParams:
     """LiquidationSweepPump constants used by compute_pump_score
@@ -158,6 +163,8 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
     prev = F.shift(C, 1)
     tr = F.run({"tr": F.fmax(F.fmax(H - L, (H - prev).abs()), (L - prev).abs())})["tr"]   # max(axis=1) skips NaN
     bench = btc_close.reshape(1, -1).contiguous()
+    if _PUMP_FUSED and not exact and max(p.volume_lookback, p.compression_bars) < 31 and p.momentum_bars < 32:
+        return _pump_score_fused(h, l, c, v, tr, bench, p)
     # the benchmark's [1, T] series ride in the panel's batch (one launch)
     atr, vmean, hmax, lmin, e20, e50, cf, bf, be20, be50 = engine.rolling_many(
         E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
@@ -200,6 +207,33 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
         "momentum_atr": st2["momentum_atr"], "btc_momentum_3": st2["btc_momentum_3"],
         "btc_trend_score": st2["btc_trend_score"], "relative_strength": st2["relative_strength"],
     }
+    return out
+
+
+def _pump_score_fused(h, l, c, v, tr, bench, p: PumpParams) -> dict[str, torch.Tensor]:
+    """Panel mode of pump_score_features: the ewm series by bq_rolling_batch,
+    every other column but the quantiles and score_cross in one pass per row
+    (bq_pump_features: the volume mean, the high / low windows and the
+    pad-filled pct_change inside the kernel), then the two rolling quantiles
+    and score_cross."""
+    atr, e20, e50, bf, be20, be50 = engine.rolling_many(
+        E(tr, alpha=1 / 14, min_periods=14), E(c, span=20), E(c, span=50), FF(bench), E(bench, span=20),
+        E(bench, span=50), exact=False,
+    )
+    st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
+                              p.volume_lookback, p.compression_bars)
+    thr_s, thr_v = engine.rolling_many(
+        R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+    )
+    PS, TS = F.inp(st["pump_score"]), F.inp(thr_s)
+    cross = F.run({"score_cross": (PS >= TS) & (F.shift(PS, 1) < F.shift(TS, 1))})["score_cross"]
+    out = {k: st[k] for k in ("candidate_atr", "momentum_3", "relative_volume", "pre_breakout_compression",
+                              "pump_score")}
+    out.update(score_threshold=thr_s, volume_threshold=thr_v, score_cross=cross)
+    for k in ("prior_high", "close_location", "ema20", "ema50", "trend_score", "momentum_atr", "btc_momentum_3",
+              "btc_trend_score", "relative_strength"):
+        out[k] = st[k]
     return out
 
 

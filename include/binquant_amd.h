@@ -327,6 +327,31 @@ int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double
 int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32_t bars, uint8_t* kept,
                 uint8_t* suppressed, int64_t ld_out, void* stream);
 
+/* ---- fused strategy stages -------------------------------------------------- */
+/*
+ * LiquidationSweepPump.compute_pump_score (strategies/liquidation_sweep_pump.py:
+ * 195-269) in one pass per row, panel mode: every column but the two rolling
+ * quantiles (score_threshold / volume_threshold) and score_cross, with the
+ * volume.shift(1).rolling(volume_lookback).mean() and the
+ * high / low .shift(1).rolling(compression_bars).max() / .min() windows and
+ * close.pct_change(momentum_bars) (pad-filled) formed in the kernel.
+ * in = {high, low, close, volume, candidate_atr, ema20, ema50} [S][ld_in]
+ * fp64 (the three ewm columns from bq_rolling_batch); bench = {ffilled
+ * benchmark close, its ewm(span=20), ewm(span=50)} [T] fp64 (the benchmark
+ * left-merged on the panel's open_time grid); out[BQ_NUM_PUMP_COLS] [S][ld_out]
+ * fp64 (NULL = skip). momentum_bars <= 31, volume_lookback and
+ * compression_bars <= 30.
+ */
+enum bq_pump_col {
+  BQ_PUMP_CANDIDATE_ATR = 0, BQ_PUMP_MOMENTUM_3, BQ_PUMP_RELATIVE_VOLUME, BQ_PUMP_COMPRESSION, BQ_PUMP_SCORE,
+  BQ_PUMP_PRIOR_HIGH, BQ_PUMP_CLOSE_LOCATION, BQ_PUMP_EMA20, BQ_PUMP_EMA50, BQ_PUMP_TREND_SCORE,
+  BQ_PUMP_MOMENTUM_ATR, BQ_PUMP_BTC_MOMENTUM_3, BQ_PUMP_BTC_TREND_SCORE, BQ_PUMP_RELATIVE_STRENGTH,
+  BQ_NUM_PUMP_COLS
+};
+int bq_pump_features(const double* const* in, int64_t S, int64_t T, int64_t ld_in, const double* const* bench,
+                     int32_t momentum_bars, int32_t volume_lookback, int32_t compression_bars, double* const* out,
+                     int64_t ld_out, void* stream);
+
 /* ---- sequential state machines (lane = symbol) ----------------------------- */
 /*
  * Supertrend trend flag and final bands (pybinbot Indicators.set_supertrend,
