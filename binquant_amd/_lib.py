@@ -205,6 +205,8 @@ SIGNATURES: dict[str, tuple] = {
     "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_pump_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _PP, _I32, _I32, _I32, _PP, _I64, _P]),
+    "bq_burst_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _P, _PP, _PP, _P, _I64, _P]),
+    "bq_burst_qualify": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P, _P]),
     "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_hlc": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_panel": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
@@ -286,6 +288,16 @@ def default_params() -> BqParams:
     p = BqParams()
     load().bq_default_params(ctypes.byref(p))
     return p
+
+
+class BqBurstParams(ctypes.Structure):
+    """bq_burst_params (include/binquant_amd.h)"""
+
+    _fields_ = [("volume_multiplier", ctypes.c_double), ("quote_volume_multiplier", ctypes.c_double),
+                ("price_threshold", ctypes.c_double), ("min_baseline_volume", ctypes.c_double),
+                ("min_range_frac", ctypes.c_double), ("min_body_frac", ctypes.c_double),
+                ("max_close_to_high", ctypes.c_double), ("min_recent_up_closes", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 def ptr_array(ptrs) -> ctypes.Array:

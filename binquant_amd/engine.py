@@ -336,6 +336,76 @@ def pump_features(
     return out
 
 
+BURST_FLOAT_COLUMNS = ("baseline_volume_safe", "volume_ratio", "baseline_quote_volume_safe", "quote_volume_ratio",
+                       "price_jump", "range_frac", "body_frac", "close_to_high", "recent_up_closes",
+                       "activity_burst_score")
+BURST_BOOL_COLUMNS = ("is_bullish", "vol_spike", "quote_vol_spike", "price_jump_flag", "range_expansion_flag",
+                      "body_quality_flag", "trend_quality_flag")
+
+
+@device_entry
+def burst_features(
+    o: torch.Tensor, h: torch.Tensor, l: torch.Tensor, c: torch.Tensor, v: torch.Tensor,
+    qv: torch.Tensor | None, baseline_volume: torch.Tensor, baseline_quote_volume: torch.Tensor | None,
+    params, stream: torch.cuda.Stream | None = None,
+) -> tuple[dict[str, torch.Tensor], torch.Tensor]:
+    """ActivityBurstPump.compute_indicators' columns of
+    strategies/activity_burst_pump.py:58-133 in one pass (bq_burst_features),
+    given the two baseline medians; returns (columns, the AND of the six flags
+    as uint8 for burst_qualify). Without a quote volume the quote baseline and
+    its safe column alias the volume's (the reference's fallback)."""
+    c = _check_panel(c, "c")
+    S, T = c.shape
+    has_q = qv is not None
+    names = ("o", "h", "l", "c", "v", "qv", "baseline_volume", "baseline_quote_volume")
+    ins = []
+    for t, n in zip((o, h, l, c, v, qv, baseline_volume, baseline_quote_volume), names):
+        ins.append(None if t is None else _check_panel(t, n, (S, T)).contiguous())
+    if has_q != (baseline_quote_volume is not None):
+        raise ValueError("qv and baseline_quote_volume: give both or neither")
+    out = {n: torch.empty((S, T), dtype=torch.float64, device=c.device) for n in BURST_FLOAT_COLUMNS
+           if has_q or n != "baseline_quote_volume_safe"}
+    flags = {n: torch.empty((S, T), dtype=torch.bool, device=c.device) for n in BURST_BOOL_COLUMNS}
+    all_flags = torch.empty((S, T), dtype=torch.uint8, device=c.device)
+    pr = _lib.BqBurstParams(float(params.volume_multiplier), float(params.quote_volume_multiplier),
+                            float(params.price_threshold), float(params.min_baseline_volume),
+                            float(params.min_range_frac), float(params.min_body_frac), float(params.max_close_to_high),
+                            int(params.min_recent_up_closes if has_q else 1), 0)
+    st = _lib.load().bq_burst_features(
+        _lib.ptr_array([0 if t is None else t.data_ptr() for t in ins]), S, T, T, ctypes.byref(pr),
+        _lib.ptr_array([out[n].data_ptr() if n in out else 0 for n in BURST_FLOAT_COLUMNS]),
+        _lib.ptr_array([flags[n].data_ptr() for n in BURST_BOOL_COLUMNS]), ctypes.c_void_p(all_flags.data_ptr()), T,
+        _stream_handle(stream),
+    )
+    _lib.check(st, "bq_burst_features")
+    if not has_q:
+        out["baseline_quote_volume_safe"] = out["baseline_volume_safe"]
+    out.update(flags)
+    return out, all_flags
+
+
+@device_entry
+def burst_qualify(score: torch.Tensor, threshold: torch.Tensor, all_flags: torch.Tensor, cooldown_bars: int = 3,
+                  stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """qualified_signal (strategies/activity_burst_pump.py:140-156): raw = the
+    six flags & (score >= threshold.fillna(0)), cleared where raw fired in the
+    cooldown_bars candles before (bq_burst_qualify). bool [S, T]."""
+    score = _check_panel(score, "score")
+    S, T = score.shape
+    threshold = _check_panel(threshold, "threshold", (S, T)).contiguous()
+    score = score.contiguous()
+    if not isinstance(all_flags, torch.Tensor) or all_flags.dtype != torch.uint8 or tuple(all_flags.shape) != (S, T):
+        raise ValueError("all_flags: expected the uint8 [S, T] tensor of burst_features")
+    all_flags = all_flags.contiguous()
+    q = torch.empty((S, T), dtype=torch.bool, device=score.device)
+    st = _lib.load().bq_burst_qualify(
+        ctypes.c_void_p(score.data_ptr()), ctypes.c_void_p(threshold.data_ptr()), ctypes.c_void_p(all_flags.data_ptr()),
+        S, T, T, T, int(cooldown_bars), ctypes.c_void_p(q.data_ptr()), _stream_handle(stream),
+    )
+    _lib.check(st, "bq_burst_qualify")
+    return q
+
+
 @device_entry
 def breadth_partial(
     close: torch.Tensor,

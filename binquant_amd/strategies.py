@@ -62,6 +62,8 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
     p = p or BurstParams()
     has_q = qv is not None
     bw = max(p.lookback_window, 2)
+    if _BURST_FUSED and p.cooldown_bars <= 8:
+        return _activity_burst_fused(o, h, l, c, v, qv, p)
     O, H, L, C, V = (F.inp(t) for t in (o, h, l, c, v))
     Q = F.inp(qv) if has_q else None
     mb = p.min_baseline_volume
@@ -133,6 +135,37 @@ def activity_burst_features(o, h, l, c, v, qv=None, p: BurstParams | None = None
              "score_threshold", "qualified_signal"]
     return {k: out[k] for k in order}
 
+
+def _activity_burst_fused(o, h, l, c, v, qv, p: BurstParams) -> dict[str, torch.Tensor]:
+    """activity_burst_features through bq_burst_features / bq_burst_qualify:
+    the baseline medians and the score's quantile by bq_rolling_batch, every
+    other column in two streaming passes — bit for bit the staged pipeline."""
+    has_q = qv is not None
+    bw = max(p.lookback_window, 2)
+    specs = [R(v, bw - 1, "median", min_periods=bw - 1, shift=2)]
+    if has_q:
+        specs.append(R(qv, bw - 1, "median", min_periods=bw - 1, shift=2))
+    med = engine.rolling_many(*specs)
+    bq = med[1] if has_q else None
+    cols, all_flags = engine.burst_features(o, h, l, c, v, qv, med[0], bq, p)
+    thr = engine.rolling(cols["activity_burst_score"], p.score_lookback, "quantile", q=p.score_quantile,
+                         min_periods=p.lookback_window, shift=1)
+    out = {"baseline_volume": med[0], "baseline_volume_safe": cols["baseline_volume_safe"],
+           "volume_ratio": cols["volume_ratio"], "baseline_quote_volume": bq if has_q else med[0],
+           "baseline_quote_volume_safe": cols["baseline_quote_volume_safe"],
+           "quote_volume_ratio": cols["quote_volume_ratio"]}
+    for k in ("price_jump", "range_frac", "body_frac", "close_to_high", "is_bullish", "recent_up_closes", "vol_spike",
+              "quote_vol_spike", "price_jump_flag", "range_expansion_flag", "body_quality_flag", "trend_quality_flag",
+              "activity_burst_score"):
+        out[k] = cols[k]
+    out["score_threshold"] = thr
+    out["qualified_signal"] = engine.burst_qualify(cols["activity_burst_score"], thr, all_flags, p.cooldown_bars)
+    return out
+
+
+# activity_burst_features through bq_burst_features (False: the staged
+# pipeline; tests compare the two)
+_BURST_FUSED = True
 
 # panel mode of pump_score_features through bq_pump_features (False: the staged
 # panel pipeline; tests compare the two)

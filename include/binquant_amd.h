@@ -352,6 +352,39 @@ int bq_pump_features(const double* const* in, int64_t S, int64_t T, int64_t ld_i
                      int32_t momentum_bars, int32_t volume_lookback, int32_t compression_bars, double* const* out,
                      int64_t ld_out, void* stream);
 
+/*
+ * ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)
+ * around the score's rolling quantile, bit for bit with the staged pipeline:
+ * bq_burst_features forms every column of :58-133 from in = {open, high, low,
+ * close, volume, quote_volume, baseline_volume, baseline_quote_volume}
+ * [S][ld_in] fp64 (the two baselines: volume.shift(2).rolling(19).median(),
+ * bq_rolling_batch; quote_volume and its baseline NULL without a quote
+ * volume column: the reference's neutral fallbacks), out_f[BQ_NUM_BURST_F]
+ * fp64 and out_b[BQ_NUM_BURST_B] uint8 [S][ld_out] (NULL = skip), all_flags
+ * uint8 [S][ld_out]: the AND of the six flags (NULL = skip). bq_burst_qualify:
+ * qualified_signal from the score, its threshold (rolling quantile) and
+ * all_flags (:140-156), cooldown_bars <= 8; ld_b = the byte arrays' stride.
+ */
+typedef struct bq_burst_params {
+  double volume_multiplier, quote_volume_multiplier, price_threshold, min_baseline_volume;
+  double min_range_frac, min_body_frac, max_close_to_high;
+  int32_t min_recent_up_closes;   /* the effective minimum (1 without a quote volume) */
+  int32_t reserved;
+} bq_burst_params;
+enum bq_burst_fcol {
+  BQ_BURST_BASELINE_VOLUME_SAFE = 0, BQ_BURST_VOLUME_RATIO, BQ_BURST_BASELINE_QUOTE_VOLUME_SAFE,
+  BQ_BURST_QUOTE_VOLUME_RATIO, BQ_BURST_PRICE_JUMP, BQ_BURST_RANGE_FRAC, BQ_BURST_BODY_FRAC, BQ_BURST_CLOSE_TO_HIGH,
+  BQ_BURST_RECENT_UP_CLOSES, BQ_BURST_SCORE, BQ_NUM_BURST_F
+};
+enum bq_burst_bcol {
+  BQ_BURST_IS_BULLISH = 0, BQ_BURST_VOL_SPIKE, BQ_BURST_QUOTE_VOL_SPIKE, BQ_BURST_PRICE_JUMP_FLAG,
+  BQ_BURST_RANGE_EXPANSION_FLAG, BQ_BURST_BODY_QUALITY_FLAG, BQ_BURST_TREND_QUALITY_FLAG, BQ_NUM_BURST_B
+};
+int bq_burst_features(const double* const* in, int64_t S, int64_t T, int64_t ld_in, const bq_burst_params* p,
+                      double* const* out_f, uint8_t* const* out_b, uint8_t* all_flags, int64_t ld_out, void* stream);
+int bq_burst_qualify(const double* score, const double* threshold, const uint8_t* all_flags, int64_t S, int64_t T,
+                     int64_t ld_in, int64_t ld_b, int32_t cooldown_bars, uint8_t* qualified, void* stream);
+
 /* ---- sequential state machines (lane = symbol) ----------------------------- */
 /*
  * Supertrend trend flag and final bands (pybinbot Indicators.set_supertrend,

@@ -129,43 +129,3 @@ def test_strategies_panel_mode_vs_exact(cuda):
             assert_close(x, y, f"{name}.{k}", rtol=1e-9, scale=np.broadcast_to(sc, y.shape))
         assert flips <= S * T * 5e-6, (name, flips)
 
-
-def test_pump_fused_equals_staged_panel(cuda):
-    """bq_pump_features (one pass per row) against the staged panel pipeline
-    on a 200 x 2500 panel with halts, gaps and zero volume: columns whose
-    windows are order statistics / shifts equal bit for bit, the volume mean
-    and what depends on it within 1e-12 of each row's magnitude (its sliding
-    sum restarts at each lane's 4 candles instead of 8), flags equal away
-    from near-ties."""
-    from binquant_amd import strategies
-    from binquant_amd.synth import numpy_panel
-
-    S, T = 200, 2500
-    p = numpy_panel(S, T, seed0=31, edges=True)
-    p["volume"][3, 700:760] = 0.0
-    p["close"][4, 900:905] = np.nan
-    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
-    btc = d["close"][0].clone()
-    btc[::17] = float("nan")
-    run = lambda: strategies.pump_score_features(d["open"], d["high"], d["low"], d["close"], d["volume"], btc)
-    fused = run()
-    strategies._PUMP_FUSED = False
-    try:
-        staged = run()
-    finally:
-        strategies._PUMP_FUSED = True
-    assert list(fused) == list(staged)
-    exact_cols = ("candidate_atr", "momentum_3", "pre_breakout_compression", "prior_high", "close_location", "ema20",
-                  "ema50", "trend_score", "momentum_atr", "btc_momentum_3", "btc_trend_score", "relative_strength")
-    for k in staged:
-        x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
-        if k in exact_cols:
-            np.testing.assert_array_equal(x, y, err_msg=k)
-        elif y.dtype == bool:
-            assert int((x != y).sum()) <= 5, k
-        else:
-            with np.errstate(all="ignore"):
-                fin = np.where(np.isfinite(y), np.abs(y), np.nan)
-                sc = np.nan_to_num(np.nanmax(fin, axis=1, initial=0.0), nan=1.0)
-            sc = np.where(sc > 0, sc, 1.0)
-            assert_close(x, y, f"fused.{k}", rtol=1e-12, scale=np.broadcast_to(sc[:, None], y.shape), atol_rel=1e-13)

@@ -258,8 +258,10 @@ def test_plan_cache_hits_are_bit_exact(cuda):
     from binquant_amd import signals, strategies
     from binquant_amd.synth import device_panel
 
+    # (the staged burst pipeline: its fused path, bq_burst_features, runs no
+    # JIT programs)
     calls = {
-        "burst": lambda o, h, l, c, v: strategies.activity_burst_features(o, h, l, c, v, v * c),
+        "burst": lambda o, h, l, c, v: _staged_burst(strategies, o, h, l, c, v),
         "spike": lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c),
         "pump": lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0].clone()),
         "gainer": lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c),
@@ -280,6 +282,14 @@ def test_plan_cache_hits_are_bit_exact(cuda):
         finally:
             F._PLAN_CACHE_ON = True
         _assert_same_tree(hot, cold, name)
+
+
+def _staged_burst(strategies, o, h, l, c, v):
+    strategies._BURST_FUSED = False
+    try:
+        return strategies.activity_burst_features(o, h, l, c, v, v * c)
+    finally:
+        strategies._BURST_FUSED = True
 
 
 def _assert_same_tree(a, b, path):
