@@ -207,6 +207,8 @@ SIGNATURES: dict[str, tuple] = {
     "bq_pump_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _PP, _I32, _I32, _I32, _PP, _I64, _P]),
     "bq_burst_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _P, _PP, _PP, _P, _I64, _P]),
     "bq_burst_qualify": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P, _P]),
+    "bq_spike_base": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _I32, _PP, _PP, _I64, _P]),
+    "bq_spike_flags": (ctypes.c_int, [_PP, _P, _P, _I64, _I64, _I64, _P, _PP, _PP, _I64, _P]),
     "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_hlc": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_panel": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
@@ -298,6 +300,17 @@ class BqBurstParams(ctypes.Structure):
                 ("min_range_frac", ctypes.c_double), ("min_body_frac", ctypes.c_double),
                 ("max_close_to_high", ctypes.c_double), ("min_recent_up_closes", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
+
+
+class BqSpikeParams(ctypes.Structure):
+    """bq_spike_params (include/binquant_amd.h)"""
+
+    _fields_ = [("volume_cluster_window", ctypes.c_int32), ("volume_cluster_min_count", ctypes.c_int32),
+                ("cumulative_price_window", ctypes.c_int32), ("accel_volume_deriv_window", ctypes.c_int32),
+                ("label_mode", ctypes.c_int32), ("require_both_patterns", ctypes.c_int32),
+                ("require_bullish_spike", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("cumulative_price_threshold", ctypes.c_double), ("accel_volume_deriv_min", ctypes.c_double),
+                ("accel_price_change_min", ctypes.c_double), ("body_size_pct_min", ctypes.c_double)]
 
 
 def ptr_array(ptrs) -> ctypes.Array:

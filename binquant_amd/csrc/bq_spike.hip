@@ -1,0 +1,576 @@
+// Fused failed-spike stages (gfx950): FailedSpikeFade.detect
+// (strategies/failed_spike_fade.py:260-544) on an [S][T] panel in two passes
+// per row around the whole-series calibration:
+//
+//   bq_spike_base   compute_base_features (:260-322) and the early-feature
+//                   operands (:324-357): the candle geometry, pct changes of
+//                   the pad-filled close, the rolling means / sums / integer
+//                   counts (base window, 2 / 3 / 5-bar sums, 10-bar body
+//                   stats, the streak counts) formed in the kernel, the
+//                   z-scores / ratios / momentum against the rolling std
+//                   columns (inputs: the bit-exact Welford replays of
+//                   bq_rolling_batch), the streak flags;
+//   bq_spike_flags  after auto_calibrate (:229-257: per-row thresholds from
+//                   bq_row_quantile) — the volume-cluster, price-break (the
+//                   dynamic threshold: maximum(base, rolling quantile),
+//                   ffilled), cumulative and acceleration flags and the
+//                   preliminary labels (:360-488).
+//
+// Staged, the pipeline ran ~10 element-wise / window launches that wrote and
+// re-read every intermediate (~2.4x its algorithmic bytes). Every expression
+// is the staged programs' (the reference's operation order); the rolling
+// means / sums are direct window sums in time order with pandas' rules
+// (min_periods = window, the same-value and sign rules), equal to the staged
+// panel-mode sums to rounding; integer counts and every flag downstream of
+// them are exact.
+//
+// Mapping (as bq_pump): one 256-thread workgroup per row, tiles of 1024
+// candles (4 per lane), an LDS ring with a 32-candle halo for the series the
+// windows read.
+#include "bq_device.h"
+#include "binquant_amd.h"
+
+#include <stdint.h>
+#include <string.h>
+
+namespace bq {
+
+constexpr int SP_NT = 256;
+constexpr int SP_NW = SP_NT / WAVE;
+constexpr int SP_K = 4;
+constexpr int SP_TT = SP_NT * SP_K;   // 1024
+constexpr int SP_H = 32;
+constexpr int SP_R = SP_H + SP_TT;
+constexpr int SP_Q = SP_R / SP_K;
+__device__ __forceinline__ int sp_slot(int p) { return (p & (SP_K - 1)) * SP_Q + (p >> 2); }
+constexpr double SP_EPS = 1e-6;
+
+typedef double sp_dbl2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void sp_load(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[SP_K]) {
+  if (vec && tb + SP_K <= T) {
+    const sp_dbl2* p = reinterpret_cast<const sp_dbl2*>(row + tb);
+    const sp_dbl2 a = p[0], b = p[1];
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = b.x;
+    x[3] = b.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) x[k] = tb + k < T ? row[tb + k] : qnan();
+  }
+}
+
+__device__ __forceinline__ void sp_put_bytes(uint8_t* __restrict__ row, int tb, int T, bool vec4, const bool (&b)[SP_K]) {
+  if (vec4 && tb + SP_K <= T) {
+    const uint32_t w = (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16) | ((uint32_t)b[3] << 24);
+    *reinterpret_cast<uint32_t*>(row + tb) = w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k)
+      if (tb + k < T) row[tb + k] = b[k] ? 1 : 0;
+  }
+}
+
+// x.rolling(w).sum() / .mean() at candle t over values f(j), j = -w+1 .. 0
+// (time order), min_periods = w: pandas' NaN skip, same-value rule (every
+// observed value equal: the value, times nobs for a sum) and calc_mean's
+// sign rule
+template <bool MEAN, typename F>
+__device__ __forceinline__ double sp_window(int t, int w, F f) {
+  if (t < w - 1) return qnan();
+  double s = 0.0, first = qnan();
+  int n = 0, neg = 0;
+  bool same = true;
+  for (int j = -w + 1; j <= 0; ++j) {
+    const double v = f(j);
+    if (v != v) continue;
+    s += v;
+    ++n;
+    neg += signbit(v) ? 1 : 0;
+    if (first != first) first = v;
+    else same = same && v == first;
+  }
+  if (n < w || n <= 0) return qnan();
+  if (!MEAN) return same ? first * (double)n : s;
+  double r = s / (double)n;
+  if (same) r = first;
+  else if (neg == 0 && r < 0.0) r = 0.0;
+  else if (neg == n && r > 0.0) r = 0.0;
+  return r;
+}
+
+// ---- pass 1: base features ------------------------------------------------------------
+enum { SB_O = 0, SB_H, SB_L, SB_C, SB_V, SB_Q, SB_CF, SB_PSTD, SB_VSTD, SB_S8, SB_S20, SB_BSD, SB_NIN };
+
+struct SpikeBaseArgs {
+  const double* in[SB_NIN];
+  double* out[BQ_NUM_SPIKE_BASE_F];
+  uint8_t* flag[BQ_NUM_SPIKE_BASE_B];
+  int64_t S, ld_in, ld_out;
+  int T, w, n, pad;
+};
+
+__global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A, int vin, int vout, int vb) {
+  __shared__ double sO[SP_R], sC[SP_R], sF[SP_R], sV[SP_R], sQ[SP_R];
+  const int tid = threadIdx.x;
+  const int64_t sym = blockIdx.x;
+  const int T = A.T, W = A.w, N = A.n;
+  const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
+  if (tid < SP_H) sO[sp_slot(tid)] = sC[sp_slot(tid)] = sF[sp_slot(tid)] = sV[sp_slot(tid)] = sQ[sp_slot(tid)] = qnan();
+  for (int t0 = 0; t0 < T; t0 += SP_TT) {
+    const int tb = t0 + SP_K * tid, pb = SP_H + SP_K * tid;
+    double o[SP_K], h[SP_K], l[SP_K], c[SP_K], v[SP_K], q[SP_K], cf[SP_K];
+    sp_load(A.in[SB_O] + irow, tb, T, vin, o);
+    sp_load(A.in[SB_H] + irow, tb, T, vin, h);
+    sp_load(A.in[SB_L] + irow, tb, T, vin, l);
+    sp_load(A.in[SB_C] + irow, tb, T, vin, c);
+    sp_load(A.in[SB_V] + irow, tb, T, vin, v);
+    sp_load(A.in[SB_Q] + irow, tb, T, vin, q);
+    sp_load(A.in[SB_CF] + irow, tb, T, vin, cf);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      sO[sp_slot(pb + k)] = o[k];
+      sC[sp_slot(pb + k)] = c[k];
+      sF[sp_slot(pb + k)] = cf[k];
+      sV[sp_slot(pb + k)] = v[k];
+      sQ[sp_slot(pb + k)] = q[k];
+    }
+    __syncthreads();
+    const bool whole = t0 + SP_TT <= T, vo = vout != 0, v4 = vb != 0;
+    auto put = [&](int col, const double (&r)[SP_K]) {
+      if (A.out[col]) store_lines<SP_K>(A.out[col] + orow, tb, T, vo, r, whole);
+    };
+    auto putb = [&](int col, const bool (&b)[SP_K]) {
+      if (A.flag[col]) sp_put_bytes(A.flag[col] + orow, tb, T, v4, b);
+    };
+    // ring readers (p = ring position of the candle)
+    auto pc_at = [&](int p) { return sF[sp_slot(p)] / sF[sp_slot(p - 1)] - 1.0; };   // pct_change of the ffilled close
+    auto bsp_at = [&](int p) {
+      const double oo = sO[sp_slot(p)];
+      return fabs(sC[sp_slot(p)] - oo) / (oo + SP_EPS);
+    };
+    double r[SP_K], pc[SP_K], body[SP_K], bsp[SP_K];
+    bool b[SP_K];
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      pc[k] = pc_at(pb + k);
+      body[k] = fabs(c[k] - o[k]);
+      bsp[k] = body[k] / (o[k] + SP_EPS);
+    }
+    put(BQ_SPIKE_PRICE_CHANGE, pc);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = fabs(pc[k]);
+    put(BQ_SPIKE_PRICE_CHANGE_ABS, r);
+    put(BQ_SPIKE_BODY_SIZE, body);
+    put(BQ_SPIKE_BODY_SIZE_PCT, bsp);
+    double uw[SP_K], lw[SP_K];
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      uw[k] = h[k] - fmax(c[k], o[k]);
+      lw[k] = fmin(c[k], o[k]) - l[k];
+    }
+    put(BQ_SPIKE_UPPER_WICK, uw);
+    put(BQ_SPIKE_LOWER_WICK, lw);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = uw[k] / (body[k] + SP_EPS);
+    put(BQ_SPIKE_UPPER_WICK_RATIO, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = lw[k] / (body[k] + SP_EPS);
+    put(BQ_SPIKE_LOWER_WICK_RATIO, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = h[k] - l[k];
+    put(BQ_SPIKE_TOTAL_RANGE, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (h[k] - l[k]) / (o[k] + SP_EPS);
+    put(BQ_SPIKE_RANGE_PCT, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) b[k] = c[k] > o[k];
+    putb(BQ_SPIKE_IS_BULLISH, b);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (c[k] - o[k]) / (o[k] + SP_EPS);
+    put(BQ_SPIKE_CLOSE_OPEN_RATIO, r);
+    // price: mean over the base window, z-score against the replayed std
+    double ma[SP_K], sd[SP_K];
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sC[sp_slot(pb + k + j)]; });
+    put(BQ_SPIKE_PRICE_MA, ma);
+    sp_load(A.in[SB_PSTD] + irow, tb, T, vin, sd);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (c[k] - ma[k]) / (sd[k] + SP_EPS);
+    put(BQ_SPIKE_PRICE_ZSCORE, r);
+    // volume
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sV[sp_slot(pb + k + j)]; });
+    put(BQ_SPIKE_VOLUME_MA, ma);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = v[k] / (ma[k] + SP_EPS);
+    put(BQ_SPIKE_VOLUME_RATIO, r);
+    sp_load(A.in[SB_VSTD] + irow, tb, T, vin, sd);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (v[k] - ma[k]) / (sd[k] + SP_EPS);
+    put(BQ_SPIKE_VOLUME_ZSCORE, r);
+    // quote volume
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sQ[sp_slot(pb + k + j)]; });
+    put(BQ_SPIKE_QUOTE_VOLUME_MA, ma);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = q[k] / (ma[k] + SP_EPS);
+    put(BQ_SPIKE_QUOTE_VOLUME_RATIO, r);
+    // momentum of the ffilled close
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = cf[k] / sF[sp_slot(pb + k - 3)] - 1.0;
+    put(BQ_SPIKE_MOMENTUM_3, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = cf[k] / sF[sp_slot(pb + k - 5)] - 1.0;
+    put(BQ_SPIKE_MOMENTUM_5, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (h[k] - c[k]) / (h[k] + SP_EPS);
+    put(BQ_SPIKE_CLOSE_TO_HIGH, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (c[k] - l[k] + SP_EPS) / (c[k] + SP_EPS);
+    put(BQ_SPIKE_CLOSE_TO_LOW, r);
+    // the 8 / 20-bar std ratio and the compression flag
+    {
+      double s8[SP_K], s20[SP_K];
+      sp_load(A.in[SB_S8] + irow, tb, T, vin, s8);
+      sp_load(A.in[SB_S20] + irow, tb, T, vin, s20);
+#pragma unroll
+      for (int k = 0; k < SP_K; ++k) {
+        r[k] = s8[k] / (s20[k] + SP_EPS);
+        b[k] = s8[k] < s20[k] * 0.6;
+      }
+      put(BQ_SPIKE_STD_RATIO_8_20, r);
+      putb(BQ_SPIKE_VOL_COMPRESSION_FLAG, b);
+    }
+    // pct-change sums, positive count, absolute sum
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 2, [&](int j) { return pc_at(pb + k + j); });
+    put(BQ_SPIKE_PC_2C, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 3, [&](int j) { return pc_at(pb + k + j); });
+    put(BQ_SPIKE_PC_3C, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k)
+      r[k] = sp_window<false>(tb + k, 5, [&](int j) { return pc_at(pb + k + j) > 0.0 ? 1.0 : 0.0; });
+    put(BQ_SPIKE_PC_POS_COUNT_5, r);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 5, [&](int j) { return fabs(pc_at(pb + k + j)); });
+    put(BQ_SPIKE_PC_ABS_SUM_5, r);
+    // body size: 10-bar mean, z-score against the replayed std
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, 10, [&](int j) { return bsp_at(pb + k + j); });
+    put(BQ_SPIKE_BODY_SIZE_PCT_MA_10, ma);
+    sp_load(A.in[SB_BSD] + irow, tb, T, vin, sd);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) r[k] = (bsp[k] - ma[k]) / (sd[k] + SP_EPS);
+    put(BQ_SPIKE_BODY_SIZE_PCT_Z, r);
+    // detect_streaks: green / red counts over the streak length
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const double g = sp_window<false>(tb + k, N, [&](int j) {
+        return sC[sp_slot(pb + k + j)] > sO[sp_slot(pb + k + j)] ? 1.0 : 0.0;
+      });
+      b[k] = g >= (double)N;
+    }
+    putb(BQ_SPIKE_UPWARD, b);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const double g = sp_window<false>(tb + k, N, [&](int j) {
+        return sC[sp_slot(pb + k + j)] < sO[sp_slot(pb + k + j)] ? 1.0 : 0.0;
+      });
+      b[k] = g >= (double)N;
+    }
+    putb(BQ_SPIKE_DOWNWARD, b);
+
+    if (t0 + SP_TT >= T) break;
+    __syncthreads();
+    if (pb >= SP_TT) {
+#pragma unroll
+      for (int k = 0; k < SP_K; ++k) {
+        const int a = sp_slot(pb + k), d = sp_slot(pb + k - SP_TT);
+        sO[d] = sO[a];
+        sC[d] = sC[a];
+        sF[d] = sF[a];
+        sV[d] = sV[a];
+        sQ[d] = sQ[a];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- pass 2: flags and labels ---------------------------------------------------------
+enum { SF_O = 0, SF_C, SF_CF, SF_VR, SF_DYN, SF_NIN };
+
+struct SpikeFlagArgs {
+  const double* in[SF_NIN];           // open, close, ffilled close, volume_ratio, rolling quantile of |pc|
+  const double *vcmr, *pbbt;          // [S] calibrated volume-cluster ratio / price-break base
+  double* out[BQ_NUM_SPIKE_FLAG_F];
+  uint8_t* flag[BQ_NUM_SPIKE_FLAG_B];
+  int64_t S, ld_in, ld_out;
+  int T, cluster_w, cluster_min, cw, accel_w, mode, both, bullish;
+  double cum_thr, accel_vd, accel_pc, body_min;
+};
+
+__global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs A, int vin, int vout, int vb) {
+  __shared__ double sO[SP_R], sC[SP_R], sF[SP_R], sVR[SP_R], sTP[SP_R];
+  __shared__ int sW[SP_NW];
+  __shared__ int sCar;
+  __shared__ double sTV;   // threshold carried across tiles (the ffill)
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const int64_t sym = blockIdx.x;
+  const int T = A.T;
+  const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
+  const double VC = A.vcmr[sym], PB = A.pbbt[sym];
+  if (tid < SP_H) sO[sp_slot(tid)] = sC[sp_slot(tid)] = sF[sp_slot(tid)] = sVR[sp_slot(tid)] = sTP[sp_slot(tid)] = qnan();
+  if (tid == 0) {
+    sCar = -1;
+    sTV = qnan();
+  }
+  for (int t0 = 0; t0 < T; t0 += SP_TT) {
+    const int tb = t0 + SP_K * tid, pb = SP_H + SP_K * tid;
+    double o[SP_K], c[SP_K], cf[SP_K], vr[SP_K], dy[SP_K];
+    sp_load(A.in[SF_O] + irow, tb, T, vin, o);
+    sp_load(A.in[SF_C] + irow, tb, T, vin, c);
+    sp_load(A.in[SF_CF] + irow, tb, T, vin, cf);
+    sp_load(A.in[SF_VR] + irow, tb, T, vin, vr);
+    sp_load(A.in[SF_DYN] + irow, tb, T, vin, dy);
+    // the volume ratio one candle past the tile (shift(base, -1) of the last candle)
+    const double vr_next = tb + SP_K < T ? A.in[SF_VR][irow + tb + SP_K] : qnan();
+    int lv[SP_K];
+    int last = -1;
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const int t = tb + k;
+      // where(isnan(D), D, maximum(PB, D)): NaN stays, else the larger
+      const double d = dy[k];
+      const double tp = d != d ? d : (PB != PB ? qnan() : (PB > d ? PB : d));
+      if (tp == tp && t < T) last = t;
+      lv[k] = last;
+      sO[sp_slot(pb + k)] = o[k];
+      sC[sp_slot(pb + k)] = c[k];
+      sF[sp_slot(pb + k)] = cf[k];
+      sVR[sp_slot(pb + k)] = vr[k];
+      sTP[sp_slot(pb + k)] = tp;
+    }
+    {
+      const int inc = wave_scan_max_dpp(lv[SP_K - 1] + 1, lane);
+      if (lane == WAVE - 1) sW[w] = inc - 1;
+      const int ex = dpp_i32<DPP_WAVE_SHR1>(inc) - 1;
+      __syncthreads();
+      int cc = max(sCar, ex);
+      for (int u = 0; u < w; ++u) cc = max(cc, sW[u]);
+#pragma unroll
+      for (int k = 0; k < SP_K; ++k) lv[k] = max(lv[k], cc);
+    }
+    const bool whole = t0 + SP_TT <= T, vo = vout != 0, v4 = vb != 0;
+    auto put = [&](int col, const double (&r)[SP_K]) {
+      if (A.out[col]) store_lines<SP_K>(A.out[col] + orow, tb, T, vo, r, whole);
+    };
+    auto putb = [&](int col, const bool (&b)[SP_K]) {
+      if (A.flag[col]) sp_put_bytes(A.flag[col] + orow, tb, T, v4, b);
+    };
+    auto vr_at = [&](int p, int k, int j) {   // volume ratio of candle tb + k + j (j <= 1)
+      return (k + j >= SP_K) ? vr_next : sVR[sp_slot(p + j)];
+    };
+    auto pc_at = [&](int p) { return sF[sp_slot(p)] / sF[sp_slot(p - 1)] - 1.0; };
+    double r[SP_K], thr[SP_K];
+    bool b[SP_K], vcf[SP_K], pbf[SP_K], cumf[SP_K], cums[SP_K], accl[SP_K], accs[SP_K];
+    const int AW = A.accel_w;
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const int t = tb + k, p = pb + k;
+      // diff(VR, 3) and its first difference (t - 3 < 0: NaN)
+      const double d3 = vr[k] - (t >= 3 ? sVR[sp_slot(p - 3)] : qnan());
+      const double d3p = (t >= 1 ? sVR[sp_slot(p - 1)] : qnan()) - (t >= 4 ? sVR[sp_slot(p - 4)] : qnan());
+      r[k] = d3;
+      thr[k] = d3 - (t >= 1 ? d3p : qnan());
+    }
+    put(BQ_SPIKE_VOL_RATIO_SLOPE_3, r);
+    put(BQ_SPIKE_VOL_RATIO_ACCEL, thr);
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const int t = tb + k, p = pb + k;
+      // volume_cluster_flag: count of (VR >= VC) over the cluster window
+      // (min_periods 1), base = count >= min & cond; "last": base & ~base[t+1]
+      auto cond = [&](int j) { return vr_at(p, k, j) >= VC; };
+      auto base_at = [&](int j) {   // j = 0 or 1
+        if (t + j >= T) return false;
+        int cnt = 0;
+        for (int u = -A.cluster_w + 1; u <= 0; ++u)
+          cnt += (t + j + u >= 0) && cond(j + u);
+        return cnt >= A.cluster_min && cond(j);
+      };
+      const bool b0 = base_at(0);
+      vcf[k] = A.mode == 0 ? (b0 && !base_at(1))
+                           : (A.mode == 1 ? (b0 && !(t >= 1 && [&] {
+                                int cnt = 0;
+                                for (int u = -A.cluster_w + 1; u <= 0; ++u) cnt += (t - 1 + u >= 0) && cond(u - 1);
+                                return cnt >= A.cluster_min && cond(-1);
+                              }()))
+                                            : b0);
+      // price break against the ffilled dynamic threshold
+      const int i = lv[k];
+      const double th = i < 0 ? qnan() : (i >= t0 - SP_H ? sTP[sp_slot(i - t0 + SP_H)] : sTV);
+      thr[k] = th;
+      const double pc = pc_at(p), pca = fabs(pc);
+      pbf[k] = pca >= th;
+      // cumulative break: 3-bar sums of the positive / negative moves while
+      // the 8/10-scaled cluster condition held in the window (NaN max -> True)
+      const double cp = sp_window<false>(t, A.cw, [&](int j) {
+        const double x = pc_at(p + j);
+        return x < 0.0 ? 0.0 : x;
+      });
+      const double cn = sp_window<false>(t, A.cw, [&](int j) {
+        const double x = pc_at(p + j);
+        return fabs(x > 0.0 ? 0.0 : x);
+      });
+      double vm;   // max(VR >= VC * 0.8) over the window, min_periods = window
+      {
+        bool any = false;
+        for (int j = -A.cw + 1; j <= 0; ++j) any = any || (vr_at(p, k, j) >= VC * 0.8);
+        vm = t < A.cw - 1 ? qnan() : (any ? 1.0 : 0.0);
+      }
+      const bool vol_cond = vm != vm || vm != 0.0;
+      cumf[k] = (cp >= A.cum_thr) && vol_cond;
+      cums[k] = (cn >= A.cum_thr) && vol_cond;
+      // acceleration
+      const double vd = vr[k] - (t >= AW ? sVR[sp_slot(p - AW)] : qnan());
+      const bool acc = (vd >= A.accel_vd) && (pca >= A.accel_pc);
+      accl[k] = acc && (pc > 0.0);
+      accs[k] = acc && (pc < 0.0);
+    }
+    putb(BQ_SPIKE_VOLUME_CLUSTER_FLAG, vcf);
+    putb(BQ_SPIKE_PRICE_BREAK_FLAG, pbf);
+    put(BQ_SPIKE_PRICE_BREAK_THRESHOLD, thr);
+    putb(BQ_SPIKE_CUM_BREAK_FLAG, cumf);
+    putb(BQ_SPIKE_CUM_BREAK_SHORT_FLAG, cums);
+    putb(BQ_SPIKE_ACCEL_FLAG, accl);
+    putb(BQ_SPIKE_ACCEL_SHORT_FLAG, accs);
+    const double th_last = thr[SP_K - 1];   // the ffilled threshold at the lane's last candle
+    bool lp[SP_K], ls[SP_K];
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      const double bsp = fabs(c[k] - o[k]) / (o[k] + SP_EPS);
+      const bool combo = A.both ? (vcf[k] && pbf[k]) : (vcf[k] || pbf[k]);
+      bool a = combo || cumf[k] || accl[k];
+      if (A.bullish) a = a && (c[k] > o[k]);
+      if (A.body_min > 0.0) a = a && (bsp >= A.body_min);
+      lp[k] = a;
+      bool s = (combo || cums[k] || accs[k]) && (c[k] < o[k]);
+      if (A.body_min > 0.0) s = s && (bsp >= A.body_min);
+      ls[k] = s;
+      r[k] = qnan();
+      b[k] = false;
+    }
+    putb(BQ_SPIKE_LABEL_PRE, lp);
+    putb(BQ_SPIKE_LABEL_SHORT_PRE, ls);
+    put(BQ_SPIKE_EARLY_PROBA, r);
+    putb(BQ_SPIKE_EARLY_AUG_FLAG, b);
+
+    if (t0 + SP_TT >= T) break;
+    __syncthreads();
+    if (pb >= SP_TT) {
+#pragma unroll
+      for (int k = 0; k < SP_K; ++k) {
+        const int a = sp_slot(pb + k), d = sp_slot(pb + k - SP_TT);
+        sO[d] = sO[a];
+        sC[d] = sC[a];
+        sF[d] = sF[a];
+        sVR[d] = sVR[a];
+        sTP[d] = sTP[a];
+      }
+    }
+    if (tid == SP_NT - 1) {
+      sCar = lv[SP_K - 1];
+      sTV = th_last;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace bq
+
+namespace {
+bool sp_aligned(const void* p, unsigned a) { return (((uintptr_t)p) & (a - 1)) == 0; }
+}
+
+extern "C" int bq_spike_base(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
+                             int32_t streak_length, double* const* out_f, uint8_t* const* out_b, int64_t ld_out,
+                             void* stream) {
+  using namespace bq;
+  if (!in || !out_f || !out_b || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff - SP_TT ||
+      S > 0x7fffffff || base_window < 1 || base_window > SP_H - 2 || streak_length < 1 || streak_length > SP_H - 2)
+    return BQ_EINVAL;
+  SpikeBaseArgs A;
+  memset(&A, 0, sizeof(A));
+  for (int f = 0; f < SB_NIN; ++f) {
+    if (!in[f]) return BQ_EINVAL;
+    A.in[f] = in[f];
+  }
+  for (int c = 0; c < BQ_NUM_SPIKE_BASE_F; ++c) A.out[c] = out_f[c];
+  for (int c = 0; c < BQ_NUM_SPIKE_BASE_B; ++c) A.flag[c] = out_b[c];
+  if (S == 0 || T == 0) return BQ_OK;
+  A.S = S;
+  A.T = (int)T;
+  A.ld_in = ld_in;
+  A.ld_out = ld_out;
+  A.w = base_window;
+  A.n = streak_length;
+  int vin = (ld_in % 2) == 0, vout = (ld_out % 2) == 0, vb = (ld_out % 4) == 0;
+  for (int f = 0; f < SB_NIN; ++f) vin &= sp_aligned(in[f], 16);
+  for (int c = 0; c < BQ_NUM_SPIKE_BASE_F; ++c)
+    if (out_f[c]) vout &= sp_aligned(out_f[c], 16);
+  for (int c = 0; c < BQ_NUM_SPIKE_BASE_B; ++c)
+    if (out_b[c]) vb &= sp_aligned(out_b[c], 4);
+  hipLaunchKernelGGL(spike_base_kernel, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout, vb);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+extern "C" int bq_spike_flags(const double* const* in, const double* vcmr, const double* pbbt, int64_t S, int64_t T,
+                              int64_t ld_in, const bq_spike_params* p, double* const* out_f, uint8_t* const* out_b,
+                              int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!in || !vcmr || !pbbt || !p || !out_f || !out_b || S < 0 || T < 0 || ld_in < T || ld_out < T ||
+      T > 0x7fffffff - SP_TT || S > 0x7fffffff)
+    return BQ_EINVAL;
+  if (p->volume_cluster_window < 1 || p->volume_cluster_window > SP_H - 2 || p->cumulative_price_window < 2 ||
+      p->cumulative_price_window > SP_H - 2 || p->accel_volume_deriv_window < 0 ||
+      p->accel_volume_deriv_window > SP_H - 2 || p->label_mode < 0 || p->label_mode > 2)
+    return BQ_EINVAL;
+  SpikeFlagArgs A;
+  memset(&A, 0, sizeof(A));
+  for (int f = 0; f < SF_NIN; ++f) {
+    if (!in[f]) return BQ_EINVAL;
+    A.in[f] = in[f];
+  }
+  A.vcmr = vcmr;
+  A.pbbt = pbbt;
+  for (int c = 0; c < BQ_NUM_SPIKE_FLAG_F; ++c) A.out[c] = out_f[c];
+  for (int c = 0; c < BQ_NUM_SPIKE_FLAG_B; ++c) A.flag[c] = out_b[c];
+  if (S == 0 || T == 0) return BQ_OK;
+  A.S = S;
+  A.T = (int)T;
+  A.ld_in = ld_in;
+  A.ld_out = ld_out;
+  A.cluster_w = p->volume_cluster_window;
+  A.cluster_min = p->volume_cluster_min_count;
+  A.cw = p->cumulative_price_window;
+  A.accel_w = p->accel_volume_deriv_window;
+  A.mode = p->label_mode;
+  A.both = p->require_both_patterns;
+  A.bullish = p->require_bullish_spike;
+  A.cum_thr = p->cumulative_price_threshold;
+  A.accel_vd = p->accel_volume_deriv_min;
+  A.accel_pc = p->accel_price_change_min;
+  A.body_min = p->body_size_pct_min;
+  int vin = (ld_in % 2) == 0, vout = (ld_out % 2) == 0, vb = (ld_out % 4) == 0;
+  for (int f = 0; f < SF_NIN; ++f) vin &= sp_aligned(in[f], 16);
+  for (int c = 0; c < BQ_NUM_SPIKE_FLAG_F; ++c)
+    if (out_f[c]) vout &= sp_aligned(out_f[c], 16);
+  for (int c = 0; c < BQ_NUM_SPIKE_FLAG_B; ++c)
+    if (out_b[c]) vb &= sp_aligned(out_b[c], 4);
+  hipLaunchKernelGGL(spike_flags_kernel, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout, vb);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}

@@ -406,6 +406,85 @@ def burst_qualify(score: torch.Tensor, threshold: torch.Tensor, all_flags: torch
     return q
 
 
+SPIKE_BASE_FLOAT = ("price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
+                    "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "close_open_ratio", "price_ma",
+                    "price_zscore", "volume_ma", "volume_ratio", "volume_zscore", "quote_volume_ma",
+                    "quote_volume_ratio", "momentum_3", "momentum_5", "close_to_high", "close_to_low",
+                    "std_ratio_8_20", "pc_2c", "pc_3c", "pc_pos_count_5", "pc_abs_sum_5", "body_size_pct_ma_10",
+                    "body_size_pct_z")
+SPIKE_BASE_BOOL = ("is_bullish", "vol_compression_flag", "upward", "downward")
+SPIKE_FLAG_FLOAT = ("vol_ratio_slope_3", "vol_ratio_accel", "price_break_threshold_series", "early_spike_proba")
+SPIKE_FLAG_BOOL = ("volume_cluster_flag", "price_break_flag", "cumulative_price_break_flag",
+                   "cumulative_price_break_short_flag", "accel_spike_flag", "accel_spike_short_flag", "label_pre",
+                   "label_short_pre", "early_proba_aug_flag")
+
+
+def _cols(S, T, dev, names, dtype, given=None):
+    given = given or {}
+    return {n: given[n] if n in given else torch.empty((S, T), dtype=dtype, device=dev) for n in names}
+
+
+@device_entry
+def spike_base(o, h, l, c, v, qv, close_ffill, price_std, volume_std, std8, std20, body_pct_std, base_window: int = 12,
+               streak_length: int = 3, body_size_pct: torch.Tensor | None = None,
+               stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
+    """FailedSpikeFade's base and early-feature columns
+    (strategies/failed_spike_fade.py:260-357) in one pass per row
+    (bq_spike_base), given the ffilled close and the rolling std columns;
+    body_size_pct: an existing column with the kernel's values (not rewritten)."""
+    c = _check_panel(c, "c")
+    S, T = c.shape
+    ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip(
+        (o, h, l, c, v, qv, close_ffill, price_std, volume_std, std8, std20, body_pct_std),
+        ("o", "h", "l", "c", "v", "qv", "close_ffill", "price_std", "volume_std", "std8", "std20", "body_pct_std"))]
+    out = _cols(S, T, c.device, SPIKE_BASE_FLOAT, torch.float64,
+                {"body_size_pct": body_size_pct} if body_size_pct is not None else None)
+    flags = _cols(S, T, c.device, SPIKE_BASE_BOOL, torch.bool)
+    st = _lib.load().bq_spike_base(
+        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, int(base_window), int(streak_length),
+        _lib.ptr_array([0 if (n == "body_size_pct" and body_size_pct is not None) else out[n].data_ptr()
+                        for n in SPIKE_BASE_FLOAT]),
+        _lib.ptr_array([flags[n].data_ptr() for n in SPIKE_BASE_BOOL]), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_spike_base")
+    out.update(flags)
+    return out
+
+
+_SPIKE_MODES = {"last": 0, "first": 1, "all": 2}
+
+
+@device_entry
+def spike_flags(o, c, close_ffill, volume_ratio, dyn_threshold, vcmr, pbbt, params,
+                stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
+    """FailedSpikeFade's flag columns and preliminary labels
+    (strategies/failed_spike_fade.py:360-488) in one pass per row
+    (bq_spike_flags): vcmr / pbbt [S] the calibrated thresholds, dyn_threshold
+    the |pct change| rolling quantile."""
+    c = _check_panel(c, "c")
+    S, T = c.shape
+    ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip(
+        (o, c, close_ffill, volume_ratio, dyn_threshold), ("o", "c", "close_ffill", "volume_ratio", "dyn_threshold"))]
+    vc = vcmr.reshape(S).contiguous().to(torch.float64)
+    pb = pbbt.reshape(S).contiguous().to(torch.float64)
+    pr = _lib.BqSpikeParams(int(params.volume_cluster_window), int(params.volume_cluster_min_count),
+                            int(params.cumulative_price_window), int(params.accel_volume_deriv_window),
+                            _SPIKE_MODES[params.volume_cluster_label_mode], int(bool(params.require_both_patterns)),
+                            int(bool(params.require_bullish_spike)), 0, float(params.cumulative_price_threshold),
+                            float(params.accel_volume_deriv_min), float(params.accel_price_change_min),
+                            float(params.body_size_pct_min))
+    out = _cols(S, T, c.device, SPIKE_FLAG_FLOAT, torch.float64)
+    flags = _cols(S, T, c.device, SPIKE_FLAG_BOOL, torch.bool)
+    st = _lib.load().bq_spike_flags(
+        _lib.ptr_array([t.data_ptr() for t in ins]), ctypes.c_void_p(vc.data_ptr()), ctypes.c_void_p(pb.data_ptr()),
+        S, T, T, ctypes.byref(pr), _lib.ptr_array([out[n].data_ptr() for n in SPIKE_FLAG_FLOAT]),
+        _lib.ptr_array([flags[n].data_ptr() for n in SPIKE_FLAG_BOOL]), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_spike_flags")
+    out.update(flags)
+    return out
+
+
 @device_entry
 def breadth_partial(
     close: torch.Tensor,

@@ -167,6 +167,79 @@ def _activity_burst_fused(o, h, l, c, v, qv, p: BurstParams) -> dict[str, torch.
 # pipeline; tests compare the two)
 _BURST_FUSED = True
 
+def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Tensor]:
+    """failed_spike_features (panel mode) through bq_spike_base / bq_spike_flags:
+    the ffill and the five rolling std columns (the bit-exact Welford replays)
+    in ONE bq_rolling_batch call, the base / early features in one pass, the
+    |pct change| quantile and the whole-series calibration, the flags and
+    labels in a second pass, then the cooldowns."""
+    eps = 1e-6
+    w, n = p.base_window, p.streak_length
+    O, C = F.inp(o), F.inp(c)
+    bsp = F.run({"bsp": (C - O).abs() / (O + eps)})["bsp"]
+    cf, price_std, volume_std, s8, s20, bsp_sd = engine.rolling_many(
+        FF(c), R(c, w, "std"), R(v, w, "std"), R(c, 8, "std"), R(c, 20, "std"), R(bsp, 10, "std"))
+    b = engine.spike_base(o, h, l, c, v, qv, cf, price_std, volume_std, s8, s20, bsp_sd, w, n, body_size_pct=bsp)
+    pca = b["price_change_abs"]
+    dyn = engine.rolling(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20)
+    vr = b["volume_ratio"]
+    qv_thr = engine.row_quantile(vr, p.volume_quantile).unsqueeze(1)
+    qp_thr = engine.row_quantile(pca, p.price_base_floor_quantile).unsqueeze(1)
+    skip = torch.isnan(qv_thr) | torch.isnan(qp_thr)
+    new_vol = torch.where(qv_thr > p.min_volume_ratio, qv_thr, torch.full_like(qv_thr, p.min_volume_ratio))
+    new_floor = torch.where(qp_thr > p.min_price_abs_floor, qp_thr, torch.full_like(qp_thr, p.min_price_abs_floor))
+    base0 = p.price_break_base_threshold
+    new_base = torch.where(new_floor > base0, new_floor, torch.full_like(new_floor, base0))
+    vcmr = torch.where(skip, torch.full_like(new_vol, p.volume_cluster_min_ratio), new_vol).contiguous()
+    pbbt = torch.where(skip, torch.full_like(new_base, base0), new_base).contiguous()
+    f = engine.spike_flags(o, c, cf, vr, dyn, vcmr, pbbt, p)
+    out: dict[str, torch.Tensor] = {}
+    for key in ("price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
+                "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "is_bullish", "close_open_ratio"):
+        out[key] = b[key]
+    out["price_ma"] = b["price_ma"]
+    out["price_std"] = price_std
+    out["price_zscore"] = b["price_zscore"]
+    out["volume_ma"] = b["volume_ma"]
+    out["volume_ratio"] = vr
+    out["volume_zscore"] = b["volume_zscore"]
+    out["quote_volume_ma"] = b["quote_volume_ma"]
+    for key in ("quote_volume_ratio", "momentum_3", "momentum_5", "close_to_high", "close_to_low"):
+        out[key] = b[key]
+    out["volume_cluster_min_ratio"] = vcmr.squeeze(1)
+    out["price_break_base_threshold"] = pbbt.squeeze(1)
+    out["rolling_price_std_8"] = s8
+    out["rolling_price_std_20"] = s20
+    out["std_ratio_8_20"] = b["std_ratio_8_20"]
+    out["vol_ratio_slope_3"] = f["vol_ratio_slope_3"]
+    out["vol_ratio_accel"] = f["vol_ratio_accel"]
+    out["pc_1"] = b["price_change"]
+    for key in ("pc_2c", "pc_3c", "pc_pos_count_5", "pc_abs_sum_5", "body_size_pct_ma_10"):
+        out[key] = b[key]
+    out["body_size_pct_std_10"] = bsp_sd
+    out["body_size_pct_z"] = b["body_size_pct_z"]
+    out["vol_compression_flag"] = b["vol_compression_flag"]
+    for key in ("volume_cluster_flag", "price_break_flag", "price_break_threshold_series",
+                "cumulative_price_break_flag", "cumulative_price_break_short_flag", "accel_spike_flag",
+                "accel_spike_short_flag", "label_pre", "label_short_pre", "early_spike_proba",
+                "early_proba_aug_flag"):
+        out[key] = f[key]
+    label_pre_t, label_short_t = f["label_pre"], f["label_short_pre"]
+    if p.post_spike_cooldown_bars <= 0:
+        out["label"], out["suppressed_label"] = label_pre_t.clone(), torch.zeros_like(label_pre_t)
+        out["label_short"], out["suppressed_label_short"] = label_short_t.clone(), torch.zeros_like(label_pre_t)
+    else:
+        out["label"], out["suppressed_label"] = engine.cooldown(label_pre_t, p.post_spike_cooldown_bars)
+        out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_t, p.post_spike_cooldown_bars)
+    out["upward"] = b["upward"]
+    out["downward"] = b["downward"]
+    return out
+
+
+# failed_spike_features (panel mode) through bq_spike_base / bq_spike_flags
+# (False: the staged pipeline; tests compare the two)
+_SPIKE_FUSED = True
+
 # panel mode of pump_score_features through bq_pump_features (False: the staged
 # panel pipeline; tests compare the two)
 _PUMP_FUSED = True
@@ -313,6 +386,10 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None,
     eps = 1e-6
     S, T = c.shape
     w = p.base_window
+    if (_SPIKE_FUSED and not exact and p.price_break_use_dynamic and 2 <= p.cumulative_price_window <= 30
+            and max(w, p.streak_length, p.volume_cluster_window, p.accel_volume_deriv_window) <= 30
+            and p.volume_cluster_label_mode in ("last", "first", "all")):
+        return _failed_spike_fused(o, h, l, c, v, qv, p)
     O, H, L, C, V, Q = (F.inp(t) for t in (o, h, l, c, v, qv))
     # ---- compute_base_features (:260-322) ----
     (cf,) = engine.rolling_many(FF(c))

@@ -385,6 +385,53 @@ int bq_burst_features(const double* const* in, int64_t S, int64_t T, int64_t ld_
 int bq_burst_qualify(const double* score, const double* threshold, const uint8_t* all_flags, int64_t S, int64_t T,
                      int64_t ld_in, int64_t ld_b, int32_t cooldown_bars, uint8_t* qualified, void* stream);
 
+/*
+ * FailedSpikeFade.detect (strategies/failed_spike_fade.py:260-544) in two
+ * passes per row around auto_calibrate. bq_spike_base: in = {open, high, low,
+ * close, volume, quote_volume, ffilled close, price_std (close, base window),
+ * volume_std (base window), close std 8, close std 20, body_size_pct std 10}
+ * [S][ld_in] fp64 (the std columns: bq_rolling_batch's bit-exact replays) ->
+ * compute_base_features' and the early features' columns (out_f
+ * [BQ_NUM_SPIKE_BASE_F] fp64, out_b [BQ_NUM_SPIKE_BASE_B] uint8, NULL = skip),
+ * the rolling means / sums (min_periods = window) formed in the kernel;
+ * base_window, streak_length <= 30. bq_spike_flags: in = {open, close, ffilled
+ * close, volume_ratio, |pct change| rolling quantile} [S][ld_in], vcmr / pbbt
+ * [S] (the calibrated volume-cluster ratio and price-break base) -> the flag
+ * columns and preliminary labels of :360-488 (cooldown: bq_cooldown).
+ */
+typedef struct bq_spike_params {
+  int32_t volume_cluster_window, volume_cluster_min_count, cumulative_price_window, accel_volume_deriv_window;
+  int32_t label_mode;   /* 0 last, 1 first, 2 all */
+  int32_t require_both_patterns, require_bullish_spike, reserved;
+  double cumulative_price_threshold, accel_volume_deriv_min, accel_price_change_min, body_size_pct_min;
+} bq_spike_params;
+enum bq_spike_base_fcol {
+  BQ_SPIKE_PRICE_CHANGE = 0, BQ_SPIKE_PRICE_CHANGE_ABS, BQ_SPIKE_BODY_SIZE, BQ_SPIKE_BODY_SIZE_PCT,
+  BQ_SPIKE_UPPER_WICK, BQ_SPIKE_LOWER_WICK, BQ_SPIKE_UPPER_WICK_RATIO, BQ_SPIKE_LOWER_WICK_RATIO,
+  BQ_SPIKE_TOTAL_RANGE, BQ_SPIKE_RANGE_PCT, BQ_SPIKE_CLOSE_OPEN_RATIO, BQ_SPIKE_PRICE_MA, BQ_SPIKE_PRICE_ZSCORE,
+  BQ_SPIKE_VOLUME_MA, BQ_SPIKE_VOLUME_RATIO, BQ_SPIKE_VOLUME_ZSCORE, BQ_SPIKE_QUOTE_VOLUME_MA,
+  BQ_SPIKE_QUOTE_VOLUME_RATIO, BQ_SPIKE_MOMENTUM_3, BQ_SPIKE_MOMENTUM_5, BQ_SPIKE_CLOSE_TO_HIGH,
+  BQ_SPIKE_CLOSE_TO_LOW, BQ_SPIKE_STD_RATIO_8_20, BQ_SPIKE_PC_2C, BQ_SPIKE_PC_3C, BQ_SPIKE_PC_POS_COUNT_5,
+  BQ_SPIKE_PC_ABS_SUM_5, BQ_SPIKE_BODY_SIZE_PCT_MA_10, BQ_SPIKE_BODY_SIZE_PCT_Z, BQ_NUM_SPIKE_BASE_F
+};
+enum bq_spike_base_bcol {
+  BQ_SPIKE_IS_BULLISH = 0, BQ_SPIKE_VOL_COMPRESSION_FLAG, BQ_SPIKE_UPWARD, BQ_SPIKE_DOWNWARD, BQ_NUM_SPIKE_BASE_B
+};
+enum bq_spike_flag_fcol {
+  BQ_SPIKE_VOL_RATIO_SLOPE_3 = 0, BQ_SPIKE_VOL_RATIO_ACCEL, BQ_SPIKE_PRICE_BREAK_THRESHOLD, BQ_SPIKE_EARLY_PROBA,
+  BQ_NUM_SPIKE_FLAG_F
+};
+enum bq_spike_flag_bcol {
+  BQ_SPIKE_VOLUME_CLUSTER_FLAG = 0, BQ_SPIKE_PRICE_BREAK_FLAG, BQ_SPIKE_CUM_BREAK_FLAG, BQ_SPIKE_CUM_BREAK_SHORT_FLAG,
+  BQ_SPIKE_ACCEL_FLAG, BQ_SPIKE_ACCEL_SHORT_FLAG, BQ_SPIKE_LABEL_PRE, BQ_SPIKE_LABEL_SHORT_PRE,
+  BQ_SPIKE_EARLY_AUG_FLAG, BQ_NUM_SPIKE_FLAG_B
+};
+int bq_spike_base(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
+                  int32_t streak_length, double* const* out_f, uint8_t* const* out_b, int64_t ld_out, void* stream);
+int bq_spike_flags(const double* const* in, const double* vcmr, const double* pbbt, int64_t S, int64_t T,
+                   int64_t ld_in, const bq_spike_params* p, double* const* out_f, uint8_t* const* out_b,
+                   int64_t ld_out, void* stream);
+
 /* ---- sequential state machines (lane = symbol) ----------------------------- */
 /*
  * Supertrend trend flag and final bands (pybinbot Indicators.set_supertrend,

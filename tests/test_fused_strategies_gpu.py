@@ -90,3 +90,72 @@ def test_burst_fused_equals_staged(cuda, with_q):
         assert x.dtype == y.dtype, k
         np.testing.assert_array_equal(x, y, err_msg=k)
     assert staged["qualified_signal"].sum().item() > 0
+
+
+def test_spike_fused_equals_staged(cuda):
+    """bq_spike_base / bq_spike_flags against the staged failed-spike pipeline
+    (panel mode): the rolling std columns and everything computed from raw
+    values (geometry, pct changes, momentum, integer counts, streak flags)
+    equal bit for bit; the rolling means / sums (direct window sums here,
+    sliding in the staged panel kernel) and their dependants within 1e-12 of
+    each row's magnitude; flags equal away from near-ties of their
+    thresholds (a handful at most)."""
+    from binquant_amd import strategies
+    from binquant_amd.synth import numpy_panel
+
+    S, T = 160, 2200
+    p = numpy_panel(S, T, seed0=91, edges=True)
+    p["volume"][3, 700:760] = 0.0
+    p["close"][4, 900:905] = np.nan
+    rng = np.random.default_rng(8)
+    spikes = rng.random((S, T)) < 0.02
+    p["volume"][spikes] *= 6.0
+    p["close"][spikes] *= 1.04
+    p["high"] = np.fmax(p["high"], p["close"])
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    qv = d["volume"] * d["close"]
+    run = lambda: strategies.failed_spike_features(d["open"], d["high"], d["low"], d["close"], d["volume"], qv)
+    fused = run()
+    strategies._SPIKE_FUSED = False
+    try:
+        staged = run()
+    finally:
+        strategies._SPIKE_FUSED = True
+    assert list(fused) == list(staged)
+    exact = {"price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
+             "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "is_bullish", "close_open_ratio",
+             "price_std", "momentum_3", "momentum_5", "close_to_high", "close_to_low", "rolling_price_std_8",
+             "rolling_price_std_20", "std_ratio_8_20", "pc_1", "pc_pos_count_5", "body_size_pct_std_10",
+             "vol_compression_flag", "upward", "downward", "early_spike_proba", "early_proba_aug_flag"}
+    # z-scores: (x - mean) / (std + eps) cancels where x ~ its mean, so the
+    # means' rounding difference (~1e-16 of x) is amplified by |x| / std
+    from binquant_amd import engine
+
+    vstd = engine.rolling(d["volume"], 12, "std").cpu().numpy()
+    zbase = {"price_zscore": (staged["price_std"].cpu().numpy(), p["close"]), "volume_zscore": (vstd, p["volume"]),
+             "body_size_pct_z": (staged["body_size_pct_std_10"].cpu().numpy(), staged["body_size_pct"].cpu().numpy())}
+    flips = 0
+    for k in staged:
+        x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
+        assert x.dtype == y.dtype and x.shape == y.shape, k
+        if k in exact:
+            np.testing.assert_array_equal(x, y, err_msg=k)
+        elif k in zbase:
+            sd, base = zbase[k]
+            np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=k)
+            with np.errstate(all="ignore"):
+                lim = 1e-12 * np.abs(y) + 1e-13 * np.abs(base) / (sd + 1e-6)
+                ok = np.isnan(y) | (np.abs(x - y) <= lim)
+            assert ok.all(), (k, int((~ok).sum()))
+        elif y.dtype == bool:
+            flips += int((x != y).sum())
+        else:
+            x2, y2 = (x[:, None], y[:, None]) if y.ndim == 1 else (x, y)
+            with np.errstate(all="ignore"):
+                fin = np.where(np.isfinite(y2), np.abs(y2), np.nan)
+                sc = np.nan_to_num(np.nanmax(fin, axis=1, initial=0.0), nan=1.0)
+            sc = np.where(sc > 0, sc, 1.0)
+            assert_close(x2, y2, f"fused.{k}", rtol=1e-12, scale=np.broadcast_to(sc[:, None], y2.shape),
+                         atol_rel=1e-13)
+    assert flips <= 10, flips
+    assert staged["label"].sum().item() > 0
