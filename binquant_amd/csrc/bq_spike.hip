@@ -112,12 +112,19 @@ struct SpikeBaseArgs {
 };
 
 __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A, int vin, int vout, int vb) {
-  __shared__ double sO[SP_R], sC[SP_R], sF[SP_R], sV[SP_R], sQ[SP_R];
+  // rings: close, ffilled close, volume, quote volume, body size pct, pct
+  // change (formed once per candle, read by every window), candle colour
+  __shared__ double sC[SP_R], sF[SP_R], sV[SP_R], sQ[SP_R], sB[SP_R], sP[SP_R];
+  __shared__ signed char sG[SP_R];   // +1 close > open, -1 close < open, 0 otherwise
   const int tid = threadIdx.x;
   const int64_t sym = blockIdx.x;
   const int T = A.T, W = A.w, N = A.n;
   const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
-  if (tid < SP_H) sO[sp_slot(tid)] = sC[sp_slot(tid)] = sF[sp_slot(tid)] = sV[sp_slot(tid)] = sQ[sp_slot(tid)] = qnan();
+  if (tid < SP_H) {
+    sC[sp_slot(tid)] = sF[sp_slot(tid)] = sV[sp_slot(tid)] = sQ[sp_slot(tid)] = qnan();
+    sB[sp_slot(tid)] = sP[sp_slot(tid)] = qnan();
+    sG[sp_slot(tid)] = 0;
+  }
   for (int t0 = 0; t0 < T; t0 += SP_TT) {
     const int tb = t0 + SP_K * tid, pb = SP_H + SP_K * tid;
     double o[SP_K], h[SP_K], l[SP_K], c[SP_K], v[SP_K], q[SP_K], cf[SP_K];
@@ -130,12 +137,16 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
     sp_load(A.in[SB_CF] + irow, tb, T, vin, cf);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
-      sO[sp_slot(pb + k)] = o[k];
       sC[sp_slot(pb + k)] = c[k];
       sF[sp_slot(pb + k)] = cf[k];
       sV[sp_slot(pb + k)] = v[k];
       sQ[sp_slot(pb + k)] = q[k];
+      sB[sp_slot(pb + k)] = fabs(c[k] - o[k]) / (o[k] + SP_EPS);
+      sG[sp_slot(pb + k)] = c[k] > o[k] ? 1 : (c[k] < o[k] ? -1 : 0);
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) sP[sp_slot(pb + k)] = cf[k] / sF[sp_slot(pb + k - 1)] - 1.0;
     __syncthreads();
     const bool whole = t0 + SP_TT <= T, vo = vout != 0, v4 = vb != 0;
     auto put = [&](int col, const double (&r)[SP_K]) {
@@ -145,18 +156,15 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
       if (A.flag[col]) sp_put_bytes(A.flag[col] + orow, tb, T, v4, b);
     };
     // ring readers (p = ring position of the candle)
-    auto pc_at = [&](int p) { return sF[sp_slot(p)] / sF[sp_slot(p - 1)] - 1.0; };   // pct_change of the ffilled close
-    auto bsp_at = [&](int p) {
-      const double oo = sO[sp_slot(p)];
-      return fabs(sC[sp_slot(p)] - oo) / (oo + SP_EPS);
-    };
+    auto pc_at = [&](int p) { return sP[sp_slot(p)]; };   // pct_change of the ffilled close
+    auto bsp_at = [&](int p) { return sB[sp_slot(p)]; };
     double r[SP_K], pc[SP_K], body[SP_K], bsp[SP_K];
     bool b[SP_K];
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
       pc[k] = pc_at(pb + k);
       body[k] = fabs(c[k] - o[k]);
-      bsp[k] = body[k] / (o[k] + SP_EPS);
+      bsp[k] = bsp_at(pb + k);
     }
     put(BQ_SPIKE_PRICE_CHANGE, pc);
 #pragma unroll
@@ -269,7 +277,7 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
       const double g = sp_window<false>(tb + k, N, [&](int j) {
-        return sC[sp_slot(pb + k + j)] > sO[sp_slot(pb + k + j)] ? 1.0 : 0.0;
+        return sG[sp_slot(pb + k + j)] > 0 ? 1.0 : 0.0;
       });
       b[k] = g >= (double)N;
     }
@@ -277,7 +285,7 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
       const double g = sp_window<false>(tb + k, N, [&](int j) {
-        return sC[sp_slot(pb + k + j)] < sO[sp_slot(pb + k + j)] ? 1.0 : 0.0;
+        return sG[sp_slot(pb + k + j)] < 0 ? 1.0 : 0.0;
       });
       b[k] = g >= (double)N;
     }
@@ -289,11 +297,13 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
 #pragma unroll
       for (int k = 0; k < SP_K; ++k) {
         const int a = sp_slot(pb + k), d = sp_slot(pb + k - SP_TT);
-        sO[d] = sO[a];
         sC[d] = sC[a];
         sF[d] = sF[a];
         sV[d] = sV[a];
         sQ[d] = sQ[a];
+        sB[d] = sB[a];
+        sP[d] = sP[a];
+        sG[d] = sG[a];
       }
     }
     __syncthreads();
@@ -314,7 +324,7 @@ struct SpikeFlagArgs {
 };
 
 __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs A, int vin, int vout, int vb) {
-  __shared__ double sO[SP_R], sC[SP_R], sF[SP_R], sVR[SP_R], sTP[SP_R];
+  __shared__ double sF[SP_R], sP[SP_R], sVR[SP_R], sTP[SP_R];
   __shared__ int sW[SP_NW];
   __shared__ int sCar;
   __shared__ double sTV;   // threshold carried across tiles (the ffill)
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
   const int T = A.T;
   const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
   const double VC = A.vcmr[sym], PB = A.pbbt[sym];
-  if (tid < SP_H) sO[sp_slot(tid)] = sC[sp_slot(tid)] = sF[sp_slot(tid)] = sVR[sp_slot(tid)] = sTP[sp_slot(tid)] = qnan();
+  if (tid < SP_H) sF[sp_slot(tid)] = sP[sp_slot(tid)] = sVR[sp_slot(tid)] = sTP[sp_slot(tid)] = qnan();
   if (tid == 0) {
     sCar = -1;
     sTV = qnan();
@@ -348,8 +358,6 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
       const double tp = d != d ? d : (PB != PB ? qnan() : (PB > d ? PB : d));
       if (tp == tp && t < T) last = t;
       lv[k] = last;
-      sO[sp_slot(pb + k)] = o[k];
-      sC[sp_slot(pb + k)] = c[k];
       sF[sp_slot(pb + k)] = cf[k];
       sVR[sp_slot(pb + k)] = vr[k];
       sTP[sp_slot(pb + k)] = tp;
@@ -362,7 +370,11 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
       int cc = max(sCar, ex);
       for (int u = 0; u < w; ++u) cc = max(cc, sW[u]);
 #pragma unroll
-      for (int k = 0; k < SP_K; ++k) lv[k] = max(lv[k], cc);
+      for (int k = 0; k < SP_K; ++k) {
+        lv[k] = max(lv[k], cc);
+        sP[sp_slot(pb + k)] = cf[k] / sF[sp_slot(pb + k - 1)] - 1.0;   // the ring is complete (barrier above)
+      }
+      __syncthreads();
     }
     const bool whole = t0 + SP_TT <= T, vo = vout != 0, v4 = vb != 0;
     auto put = [&](int col, const double (&r)[SP_K]) {
@@ -374,7 +386,7 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
     auto vr_at = [&](int p, int k, int j) {   // volume ratio of candle tb + k + j (j <= 1)
       return (k + j >= SP_K) ? vr_next : sVR[sp_slot(p + j)];
     };
-    auto pc_at = [&](int p) { return sF[sp_slot(p)] / sF[sp_slot(p - 1)] - 1.0; };
+    auto pc_at = [&](int p) { return sP[sp_slot(p)]; };
     double r[SP_K], thr[SP_K];
     bool b[SP_K], vcf[SP_K], pbf[SP_K], cumf[SP_K], cums[SP_K], accl[SP_K], accs[SP_K];
     const int AW = A.accel_w;
@@ -475,9 +487,8 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
 #pragma unroll
       for (int k = 0; k < SP_K; ++k) {
         const int a = sp_slot(pb + k), d = sp_slot(pb + k - SP_TT);
-        sO[d] = sO[a];
-        sC[d] = sC[a];
         sF[d] = sF[a];
+        sP[d] = sP[a];
         sVR[d] = sVR[a];
         sTP[d] = sTP[a];
       }
