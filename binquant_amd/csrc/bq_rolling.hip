@@ -752,15 +752,26 @@ __device__ __forceinline__ int select_bit(const unsigned (&M)[NW], int r) {
 #ifndef BQ_TR_WPB
 #define BQ_TR_WPB 1   // waves per block of the tile rank kernel
 #endif
-template <int EPL, int OPL, bool SEL>
+// PACK (panel-mode jobs, bq_roll_job.panel = 1): the union slot rides in the
+// key's low log2(N) bits instead of a separate payload — one 64-bit key per
+// element through the sort (two cross-lane moves and two selects per element
+// and stage instead of three), the slot read back from the key, the value
+// from an LDS copy of the union. Keys that differ only in those low bits
+// (values within 2^-(52 - log2 N) relative of each other) may swap order, so
+// a selected order statistic is the exact value of an element within that of
+// the true one (N = 128: 2^-45) — within rounding, not bit for bit (exact
+// mode keeps the full keys).
+template <int EPL, int OPL, bool SEL, bool PACK>
 __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBatch B) {
   constexpr int N = WAVE * EPL;          // sorted slots (power of two)
+  constexpr unsigned long long PMASK = (unsigned long long)(N - 1);
   constexpr int TILE = WAVE * OPL;       // outputs per wave
   constexpr int NWORD = N / 32;          // words of a union-slot mask
   // one wave per block (BQ_TR_WPB = 1): the waves share no LDS, so a block
   // barrier would only make independent tiles wait for each other
   __shared__ unsigned long long s_key[BQ_TR_WPB][N];
-  __shared__ unsigned short s_pos[BQ_TR_WPB][N];
+  __shared__ unsigned short s_pos[BQ_TR_WPB][PACK ? 1 : N];
+  __shared__ double s_val[BQ_TR_WPB][PACK ? N : 1];   // PACK: the union's values by slot
   __shared__ unsigned short s_cnt[BQ_TR_WPB][N + 1];   // non-NaN values before union slot u
   __shared__ unsigned char s_idx[BQ_TR_WPB][SEL ? N : 1];              // union slot -> sorted index
   __shared__ unsigned s_X[BQ_TR_WPB][SEL ? N : 1][SEL ? NWORD : 1];    // XOR prefix of the one-hot masks
@@ -778,6 +789,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
 
   unsigned long long key[EPL];
   unsigned pos[EPL];
+  bool num[EPL];
   int c = 0;
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
@@ -785,8 +797,13 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
     const int i = ubase + u;
     const double v = (live && u < U && t0 - w + 1 + u >= A.shift && i < T) ? x[i] : qnan();
     key[e] = okey_nan_last(v);
+    num[e] = v == v;
+    if constexpr (PACK) {
+      key[e] = (key[e] & ~PMASK) | (unsigned long long)u;   // NaN keys stay above every number
+      s_val[wv][u] = v;
+    }
     pos[e] = (unsigned)u;
-    c += v == v ? 1 : 0;
+    c += num[e] ? 1 : 0;
   }
   // exclusive prefix of the non-NaN counts in union order
   int incl = c;
@@ -800,7 +817,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       s_cnt[wv][lane * EPL + e] = (unsigned short)run;
-      run += key[e] != ~0ull ? 1 : 0;
+      run += num[e] ? 1 : 0;
     }
     if (lane == WAVE - 1) s_cnt[wv][N] = (unsigned short)run;
   }
@@ -820,9 +837,11 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
           const bool swap = (up & (b < a)) | (!up & (a < b));   // selects, not branches
           key[e] = swap ? b : a;
           key[e + d] = swap ? a : b;
-          const unsigned pa = pos[e], pb = pos[e + d];
-          pos[e] = swap ? pb : pa;
-          pos[e + d] = swap ? pa : pb;
+          if constexpr (!PACK) {
+            const unsigned pa = pos[e], pb = pos[e + d];
+            pos[e] = swap ? pb : pa;
+            pos[e + d] = swap ? pa : pb;
+          }
         }
       } else {
         const int ld = d / EPL;   // partner lane distance
@@ -831,24 +850,32 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
           const int i = lane * EPL + e;
           const unsigned lo32 = lane_xor((unsigned)key[e], ld);
           const unsigned hi32 = lane_xor((unsigned)(key[e] >> 32), ld);
-          const unsigned pp = lane_xor(pos[e], ld);
           const unsigned long long pk = ((unsigned long long)hi32 << 32) | lo32;
           const bool lower = (i & d) == 0, up = (i & k) == 0;
           // the lower slot of an ascending pair keeps the minimum
           const bool keep_min = lower == up;
           const bool take = (keep_min & (pk < key[e])) | (!keep_min & (key[e] < pk));
           key[e] = take ? pk : key[e];
-          pos[e] = take ? pp : pos[e];
+          if constexpr (!PACK) {
+            const unsigned pp = lane_xor(pos[e], ld);
+            pos[e] = take ? pp : pos[e];
+          }
         }
       }
     }
   }
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
+    if constexpr (PACK) pos[e] = (unsigned)(key[e] & PMASK);
     s_key[wv][lane * EPL + e] = key[e];
-    s_pos[wv][lane * EPL + e] = (unsigned short)pos[e];
+    if constexpr (!PACK) s_pos[wv][lane * EPL + e] = (unsigned short)pos[e];
     if constexpr (SEL) s_idx[wv][pos[e]] = (unsigned char)(lane * EPL + e);
   }
+  // value of a sorted key: the key itself, or (PACK) the union slot's value
+  auto kval = [&](unsigned long long kk) -> double {
+    if constexpr (PACK) return s_val[wv][kk & PMASK];
+    else return okey_value(kk);
+  };
   __syncthreads();
   if constexpr (SEL) {
     // one-hot masks of this lane's union slots, their XOR prefix in slot order
@@ -896,10 +923,10 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
           two = n > 1 && (double)a != idxf && !A.lower;
           frac = idxf - (double)a;
         }
-        const double lo = okey_value(s_key[wv][select_bit<NWORD>(M, a)]);
+        const double lo = kval(s_key[wv][select_bit<NWORD>(M, a)]);
         if (!two) r = lo;
         else {
-          const double hi = okey_value(s_key[wv][select_bit<NWORD>(M, a + 1)]);
+          const double hi = kval(s_key[wv][select_bit<NWORD>(M, a + 1)]);
           if (A.mode == BQ_ROLL_MEDIAN) r = (lo + hi) / 2.0;
           else r = lo + (hi - lo) * frac;
         }
@@ -955,7 +982,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
       if (s >= n_num) break;
       const int si = desc ? n_num - 1 - s : s;
       const unsigned long long kk = s_key[wv][si];
-      const int p = s_pos[wv][si];
+      const int p = PACK ? (int)(kk & PMASK) : (int)s_pos[wv][si];
 #pragma unroll
       for (int o = 0; o < OPL; ++o) {
         const bool mem = (unsigned)(p - m[o]) < (unsigned)w;
@@ -972,10 +999,10 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
     if (!live || t >= T) continue;
     double r = qnan();
     if (act[o]) {
-      const double lo = okey_value(klo[o]);
+      const double lo = kval(klo[o]);
       if (!need2[o]) r = lo;
       else {
-        const double hi = okey_value(khi[o]);
+        const double hi = kval(khi[o]);
         if (A.mode == BQ_ROLL_MEDIAN) r = (lo + hi) / 2.0;
         else r = lo + (hi - lo) * (idxf[o] - (double)(int)idxf[o]);
       }
@@ -1150,12 +1177,22 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
   hipLaunchKernelGGL(bq::rank_kernel<W>, dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
-template <int EPL, int OPL, bool SEL>
+template <int EPL, int OPL, bool SEL, bool PACK>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   const int64_t nt = (B.T + bq::WAVE * OPL - 1) / (bq::WAVE * OPL);
   const unsigned blocks = (unsigned)((B.S * nt + BQ_TR_WPB - 1) / BQ_TR_WPB);
-  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL, SEL>), dim3(blocks, (unsigned)n), dim3(64 * BQ_TR_WPB), 0, st,
-                     B);
+  hipLaunchKernelGGL((bq::tile_rank_kernel<EPL, OPL, SEL, PACK>), dim3(blocks, (unsigned)n), dim3(64 * BQ_TR_WPB), 0,
+                     st, B);
+}
+
+// panel-mode order statistics with packed keys (tile_rank_kernel PACK);
+// BQ_RANK_PACK=0 keeps the full keys for them too (measurement)
+bool rank_pack() {
+  static const bool on = [] {
+    const char* e = getenv("BQ_RANK_PACK");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // tile group of a job: 0 = 64-output tiles (w <= 65: union fits 128 slots),
@@ -1364,18 +1401,23 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     nrank[b] = 0;
     rank_items[b] = 0;
   };
-  RollBatch tile[3];
-  int ntile[3] = {0, 0, 0};
-  for (int g = 0; g < 3; ++g) {
+  RollBatch tile[6];   // tile group + 3 for panel-mode (packed-key) jobs
+  int ntile[6] = {0, 0, 0, 0, 0, 0};
+  for (int g = 0; g < 6; ++g) {
     memset(&tile[g], 0, sizeof(RollBatch));
     tile[g].S = S;
     tile[g].T = (int)T;
   }
   auto flush_tile = [&](int g) {
     if (!ntile[g]) return;
-    if (g == 0) launch_tile_rank<2, 1, BQ_RANK_SEL != 0>(tile[g], ntile[g], st);
-    else if (g == 1) launch_tile_rank<4, 2, true>(tile[g], ntile[g], st);
-    else launch_tile_rank<4, 2, false>(tile[g], ntile[g], st);
+    switch (g) {
+      case 0: launch_tile_rank<2, 1, BQ_RANK_SEL != 0, false>(tile[g], ntile[g], st); break;
+      case 1: launch_tile_rank<4, 2, true, false>(tile[g], ntile[g], st); break;
+      case 2: launch_tile_rank<4, 2, false, false>(tile[g], ntile[g], st); break;
+      case 3: launch_tile_rank<2, 1, BQ_RANK_SEL != 0, true>(tile[g], ntile[g], st); break;
+      case 4: launch_tile_rank<4, 2, true, true>(tile[g], ntile[g], st); break;
+      default: launch_tile_rank<4, 2, false, true>(tile[g], ntile[g], st);
+    }
     ntile[g] = 0;
   };
   RollBatch ff;
@@ -1468,7 +1510,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       sten[b].j[nsten[b]++] = J;
       if (nsten[b] == RW_MAXJOBS) flush_sten(b);
     } else if (rank_impl(in.window, S, T) >= 1) {
-      const int g = tile_group(in.window, in.mode, in.q);
+      const int g = tile_group(in.window, in.mode, in.q) + (in.panel && rank_pack() ? 3 : 0);
       tile[g].j[ntile[g]++] = J;
       if (ntile[g] == RW_MAXJOBS) flush_tile(g);
     } else {
@@ -1499,7 +1541,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   flush_rep();
   flush_ff();
   for (int b = 0; b < 6; ++b) flush_rank(b);
-  for (int g = 0; g < 3; ++g) flush_tile(g);
+  for (int g = 0; g < 6; ++g) flush_tile(g);
   for (int b = 0; b < 6; ++b) flush_sten(b);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }

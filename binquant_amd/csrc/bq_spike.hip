@@ -383,13 +383,24 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
     auto putb = [&](int col, const bool (&b)[SP_K]) {
       if (A.flag[col]) sp_put_bytes(A.flag[col] + orow, tb, T, v4, b);
     };
-    auto vr_at = [&](int p, int k, int j) {   // volume ratio of candle tb + k + j (j <= 1)
-      return (k + j >= SP_K) ? vr_next : sVR[sp_slot(p + j)];
-    };
     auto pc_at = [&](int p) { return sP[sp_slot(p)]; };
     double r[SP_K], thr[SP_K];
     bool b[SP_K], vcf[SP_K], pbf[SP_K], cumf[SP_K], cums[SP_K], accl[SP_K], accs[SP_K];
     const int AW = A.accel_w;
+    // condition bits of candles tb - 31 .. tb + 4 (bit u <-> candle tb - 31 + u;
+    // before the row and missing ratios: 0): VR >= VC and VR >= 0.8 VC
+    uint64_t m1 = 0, m8 = 0;
+    {
+      const double vc8 = VC * 0.8;
+#pragma unroll 4
+      for (int u = 0; u < 36; ++u) {
+        const double x = u < 35 ? sVR[sp_slot(pb - 31 + u)] : vr_next;
+        m1 |= (uint64_t)(x >= VC) << u;
+        m8 |= (uint64_t)(x >= vc8) << u;
+      }
+    }
+    // bits of the window of w candles ending at candle tb + e (e <= 4)
+    auto win_bits = [&](uint64_t m, int e, int w) { return (m >> (31 + e - w + 1)) & ((1ull << w) - 1ull); };
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
       const int t = tb + k, p = pb + k;
@@ -406,22 +417,13 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
       const int t = tb + k, p = pb + k;
       // volume_cluster_flag: count of (VR >= VC) over the cluster window
       // (min_periods 1), base = count >= min & cond; "last": base & ~base[t+1]
-      auto cond = [&](int j) { return vr_at(p, k, j) >= VC; };
-      auto base_at = [&](int j) {   // j = 0 or 1
-        if (t + j >= T) return false;
-        int cnt = 0;
-        for (int u = -A.cluster_w + 1; u <= 0; ++u)
-          cnt += (t + j + u >= 0) && cond(j + u);
-        return cnt >= A.cluster_min && cond(j);
+      auto base_at = [&](int j) {   // candle t + j, j in -1 .. 1
+        if (t + j >= T || t + j < 0) return false;
+        const int cnt = __popcll(win_bits(m1, k + j, A.cluster_w));
+        return cnt >= A.cluster_min && ((m1 >> (31 + k + j)) & 1ull);
       };
       const bool b0 = base_at(0);
-      vcf[k] = A.mode == 0 ? (b0 && !base_at(1))
-                           : (A.mode == 1 ? (b0 && !(t >= 1 && [&] {
-                                int cnt = 0;
-                                for (int u = -A.cluster_w + 1; u <= 0; ++u) cnt += (t - 1 + u >= 0) && cond(u - 1);
-                                return cnt >= A.cluster_min && cond(-1);
-                              }()))
-                                            : b0);
+      vcf[k] = A.mode == 0 ? (b0 && !base_at(1)) : (A.mode == 1 ? (b0 && !base_at(-1)) : b0);
       // price break against the ffilled dynamic threshold
       const int i = lv[k];
       const double th = i < 0 ? qnan() : (i >= t0 - SP_H ? sTP[sp_slot(i - t0 + SP_H)] : sTV);
@@ -438,12 +440,8 @@ __global__ __launch_bounds__(SP_NT) void spike_flags_kernel(const SpikeFlagArgs 
         const double x = pc_at(p + j);
         return fabs(x > 0.0 ? 0.0 : x);
       });
-      double vm;   // max(VR >= VC * 0.8) over the window, min_periods = window
-      {
-        bool any = false;
-        for (int j = -A.cw + 1; j <= 0; ++j) any = any || (vr_at(p, k, j) >= VC * 0.8);
-        vm = t < A.cw - 1 ? qnan() : (any ? 1.0 : 0.0);
-      }
+      // max(VR >= VC * 0.8) over the window, min_periods = window
+      const double vm = t < A.cw - 1 ? qnan() : (win_bits(m8, k, A.cw) != 0 ? 1.0 : 0.0);
       const bool vol_cond = vm != vm || vm != 0.0;
       cumf[k] = (cp >= A.cum_thr) && vol_cond;
       cums[k] = (cn >= A.cum_thr) && vol_cond;

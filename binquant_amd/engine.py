@@ -799,8 +799,10 @@ def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = 
     the same launch (bq_roll_job.rows) instead of paying a replay walk of
     its own. exact=False: sums / means (window + shift <= 128) and ewm run
     time-parallel (bq_panel.hip, panel mode), within rounding of pandas
-    (1e-9) instead of the bit-exact sequential replay; var / std, order
-    statistics and the rest are unchanged."""
+    (1e-9) instead of the bit-exact sequential replay; order statistics on
+    the tile kernels sort packed keys (the union slot in the key's low bits:
+    the selected value is an element within 2^-45 relative of the exact
+    order statistic); var / std and the rest are unchanged."""
     if not specs:
         return []
     xs = [_check_panel(sp.x, "x") for sp in specs]

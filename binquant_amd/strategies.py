@@ -181,7 +181,7 @@ def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Te
         FF(c), R(c, w, "std"), R(v, w, "std"), R(c, 8, "std"), R(c, 20, "std"), R(bsp, 10, "std"))
     b = engine.spike_base(o, h, l, c, v, qv, cf, price_std, volume_std, s8, s20, bsp_sd, w, n, body_size_pct=bsp)
     pca = b["price_change_abs"]
-    dyn = engine.rolling(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20)
+    (dyn,) = engine.rolling_many(R(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20), exact=False)
     vr = b["volume_ratio"]
     qv_thr = engine.row_quantile(vr, p.volume_quantile).unsqueeze(1)
     qp_thr = engine.row_quantile(pca, p.price_base_floor_quantile).unsqueeze(1)
@@ -328,9 +328,9 @@ def _pump_score_fused(h, l, c, v, tr, bench, p: PumpParams) -> dict[str, torch.T
     )
     st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
                               p.volume_lookback, p.compression_bars)
-    thr_s, thr_v = engine.rolling_many(
+    thr_s, thr_v = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)
         R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
-        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
+        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1), exact=False,
     )
     PS, TS = F.inp(st["pump_score"]), F.inp(thr_s)
     cross = F.run({"score_cross": (PS >= TS) & (F.shift(PS, 1) < F.shift(TS, 1))})["score_cross"]
