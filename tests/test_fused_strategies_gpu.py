@@ -159,3 +159,58 @@ def test_spike_fused_equals_staged(cuda):
                          atol_rel=1e-13)
     assert flips <= 10, flips
     assert staged["label"].sum().item() > 0
+
+
+@pytest.mark.parametrize("S,T", [(7, 1001), (3, 5), (1, 1025), (5, 2)])
+def test_fused_odd_shapes_equal_staged(cuda, S, T):
+    """Odd T (rows not 16-byte aligned: the scalar load / store paths, byte
+    flags unaligned), tiny rows and a partial second tile: the three fused
+    paths against their staged pipelines — burst bit for bit, pump / spike to
+    1e-12 / the z-score bound as above, flags equal."""
+    from binquant_amd import engine, strategies
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(S, T, seed0=S * 100 + T, edges=T > 50)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    qv = d["volume"] * d["close"]
+    btc = d["close"][0].clone()
+    calls = {
+        "burst": (lambda: strategies.activity_burst_features(d["open"], d["high"], d["low"], d["close"], d["volume"],
+                                                             qv), "_BURST_FUSED"),
+        "pump": (lambda: strategies.pump_score_features(d["open"], d["high"], d["low"], d["close"], d["volume"], btc),
+                 "_PUMP_FUSED"),
+        "spike": (lambda: strategies.failed_spike_features(d["open"], d["high"], d["low"], d["close"], d["volume"], qv),
+                  "_SPIKE_FUSED"),
+    }
+    for name, (fn, flag) in calls.items():
+        fused = fn()
+        setattr(strategies, flag, False)
+        try:
+            staged = fn()
+        finally:
+            setattr(strategies, flag, True)
+        assert list(fused) == list(staged), name
+        if name == "spike":
+            vstd = engine.rolling(d["volume"], 12, "std").cpu().numpy()
+            zb = {"price_zscore": (staged["price_std"].cpu().numpy(), p["close"]),
+                  "volume_zscore": (vstd, p["volume"]),
+                  "body_size_pct_z": (staged["body_size_pct_std_10"].cpu().numpy(),
+                                      staged["body_size_pct"].cpu().numpy())}
+        for k in staged:
+            x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
+            assert x.dtype == y.dtype and x.shape == y.shape, (name, k)
+            if y.dtype == bool or name == "burst":
+                np.testing.assert_array_equal(x, y, err_msg=f"{name}.{k}")
+                continue
+            np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=f"{name}.{k}")
+            with np.errstate(all="ignore"):
+                y2 = y if y.ndim == 2 else y[:, None]
+                fin = np.where(np.isfinite(y2), np.abs(y2), np.nan)
+                sc = np.nan_to_num(np.nanmax(fin, axis=1, initial=0.0), nan=1.0)
+                sc = np.where(sc > 0, sc, 1.0)
+                lim = 1e-12 * np.abs(y) + 1e-13 * (sc[:, None] if y.ndim == 2 else sc)
+                if name == "spike" and k in zb:   # the cancellation bound of test_spike_fused_equals_staged
+                    sd, base = zb[k]
+                    lim = lim + 1e-13 * np.abs(base) / (sd + 1e-6)
+                ok = np.isnan(y) | (np.abs(x - y) <= lim)
+            assert ok.all(), (name, k, int((~ok).sum()))
