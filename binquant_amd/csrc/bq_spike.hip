@@ -74,30 +74,44 @@ __device__ __forceinline__ void sp_put_bytes(uint8_t* __restrict__ row, int tb, 
 
 // x.rolling(w).sum() / .mean() at candle t over values f(j), j = -w+1 .. 0
 // (time order), min_periods = w: pandas' NaN skip, same-value rule (every
-// observed value equal: the value, times nobs for a sum) and calc_mean's
-// sign rule
+// observed value equal: the newest one, times nobs for a sum) and calc_mean's
+// sign rule. Branch-free (selects): the observed values' min / max decide
+// "all equal", sign-bit OR / AND decide "none / all negative".
 template <bool MEAN, typename F>
 __device__ __forceinline__ double sp_window(int t, int w, F f) {
   if (t < w - 1) return qnan();
-  double s = 0.0, first = qnan();
-  int n = 0, neg = 0;
-  bool same = true;
+  double s = 0.0, mn = __builtin_inf(), mx = -__builtin_inf(), last = qnan();
+  int n = 0;
+  unsigned sor = 0u, sand = 1u;
   for (int j = -w + 1; j <= 0; ++j) {
     const double v = f(j);
-    if (v != v) continue;
-    s += v;
-    ++n;
-    neg += signbit(v) ? 1 : 0;
-    if (first != first) first = v;
-    else same = same && v == first;
+    const bool ok = v == v;
+    const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
+    s += ok ? v : 0.0;
+    n += ok;
+    sor |= ok ? sg : 0u;
+    sand &= ok ? sg : 1u;
+    mn = ok ? fmin(mn, v) : mn;
+    mx = ok ? fmax(mx, v) : mx;
+    last = ok ? v : last;
   }
   if (n < w || n <= 0) return qnan();
-  if (!MEAN) return same ? first * (double)n : s;
+  const bool same = mn == mx;
+  if (!MEAN) return same ? last * (double)n : s;
   double r = s / (double)n;
-  if (same) r = first;
-  else if (neg == 0 && r < 0.0) r = 0.0;
-  else if (neg == n && r > 0.0) r = 0.0;
+  if (same) r = last;
+  else if (sor == 0u && r < 0.0) r = 0.0;
+  else if (sand == 1u && r > 0.0) r = 0.0;
   return r;
+}
+
+// an integer count over the window (values 0 / 1, never missing): the sum
+template <typename F>
+__device__ __forceinline__ double sp_count(int t, int w, F f) {
+  if (t < w - 1) return qnan();
+  int c = 0;
+  for (int j = -w + 1; j <= 0; ++j) c += f(j);
+  return (double)c;
 }
 
 // ---- pass 1: base features ------------------------------------------------------------
@@ -259,8 +273,7 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
     for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 3, [&](int j) { return pc_at(pb + k + j); });
     put(BQ_SPIKE_PC_3C, r);
 #pragma unroll
-    for (int k = 0; k < SP_K; ++k)
-      r[k] = sp_window<false>(tb + k, 5, [&](int j) { return pc_at(pb + k + j) > 0.0 ? 1.0 : 0.0; });
+    for (int k = 0; k < SP_K; ++k) r[k] = sp_count(tb + k, 5, [&](int j) { return pc_at(pb + k + j) > 0.0 ? 1 : 0; });
     put(BQ_SPIKE_PC_POS_COUNT_5, r);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 5, [&](int j) { return fabs(pc_at(pb + k + j)); });
@@ -276,17 +289,13 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
     // detect_streaks: green / red counts over the streak length
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
-      const double g = sp_window<false>(tb + k, N, [&](int j) {
-        return sG[sp_slot(pb + k + j)] > 0 ? 1.0 : 0.0;
-      });
+      const double g = sp_count(tb + k, N, [&](int j) { return sG[sp_slot(pb + k + j)] > 0 ? 1 : 0; });
       b[k] = g >= (double)N;
     }
     putb(BQ_SPIKE_UPWARD, b);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
-      const double g = sp_window<false>(tb + k, N, [&](int j) {
-        return sG[sp_slot(pb + k + j)] < 0 ? 1.0 : 0.0;
-      });
+      const double g = sp_count(tb + k, N, [&](int j) { return sG[sp_slot(pb + k + j)] < 0 ? 1 : 0; });
       b[k] = g >= (double)N;
     }
     putb(BQ_SPIKE_DOWNWARD, b);
