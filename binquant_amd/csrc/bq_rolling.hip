@@ -651,6 +651,169 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
   }
 }
 
+// ---- slide rank kernel (lane = symbol segment, window sorted in W registers) --------
+// The window of a compile-time length W is kept SORTED in W registers, NaNs
+// (and the slots not yet filled) as +inf placeholders at the top, with the
+// non-NaN count n beside it. One step replaces the leaving value `o` (a
+// placeholder while the window fills) by the entering value `v` with no
+// search and no index arithmetic: the array with one copy of o removed is
+//   b[i] = s[i] < o ? s[i] : s[i+1]        (s[W] = +inf)
+// and inserting v into a sorted b is a clamp per slot,
+//   s'[i] = max(b[i-1], min(v, b[i]))      (b[-1] = -inf),
+// i.e. 1 compare, 2 selects, 1 min, 1 max per slot (5 VALU; ~5 W per output
+// against the tile kernel's ~1 100 per 64-output sort for w <= 65). Zeros enter as +0 (x + 0.0), so the
+// multiset's values are the exact-mode keys' values; order statistics are a
+// pure function of the multiset, so the outputs equal the other kernels' bit
+// for bit. The quantile's rank K = int(q (w - 1)) of a full window is a
+// template constant (the host has an instantiation per (W, K) where this
+// kernel wins and sends any other (w, q) to the tile / stencil kernels), so the
+// full-window output reads two fixed registers; a partial window (warm-up,
+// NaNs) picks its ranks with the masked-OR reads of SortedWin::get.
+// Parallelism: lanes = (symbol, segment); a segment first replays the W - 1
+// values before it (the warm-up, bounded by the host's segment length).
+// Measured at 12.5k x 2k (tools/slide_probe.py, identical outputs): median(19)
+// 0.28 (stencil) -> 0.22 ms, quantile(0.80, 48) 0.61 (tile) -> 0.38 ms; at
+// w = 60 / 80 / 96 the W-register window leaves 1-2 waves per SIMD and the
+// kernel ties or loses (0.53 / 0.73 / 1.15 ms against the tile kernel's
+// 0.62 / 0.74 / 0.83), so those stay on the tile kernel. The VALU count
+// matches the 5-per-slot model (PMC: 129.5 M wave instructions for w = 48);
+// the VALU is busy ~56 % of the time at 2 waves per SIMD.
+//
+// v_min_f64 / v_max_f64 without the compiler's IEEE-mode canonicalisation of
+// operands it cannot prove canonical (a third max per slot on the loop-carried
+// registers); no NaN ever reaches them here (placeholders are +inf)
+__device__ __forceinline__ double min_f64_nn(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double max_f64_nn(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// 8-byte-aligned pairs of doubles: one 16-byte access (rows are 8-byte aligned)
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
+
+template <int W, int K, bool MED>
+__global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
+  // steps per chunk: each lane reads / writes 8 * SL_C contiguous bytes
+  // (16 for short windows: 0.27 -> 0.22 ms at w = 19; 8 where registers bind)
+  constexpr int SL_C = W <= 24 ? 16 : 8;
+  const RollJob& A = B.j[blockIdx.y];
+  const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t sym = item % B.S;
+  const int seg = (int)(item / B.S);
+  if (seg >= A.nseg) return;   // no barriers below
+  const double* __restrict__ x = A.x + sym * A.ld_in;
+  double* __restrict__ out = A.out + sym * A.ld_out;
+  const int T = B.T, sh = A.shift;
+  const int t_begin = seg * A.seg, t_end = min(T, t_begin + A.seg);
+  const int t_start = max(0, t_begin - W + 1);
+  const double inf = __builtin_inf();
+  // values of steps ts .. ts + SL_C - 1 (x[t - shift], NaN outside the row):
+  // a lane's whole span at once, so every line it touches is used up
+  // by this lane's back-to-back accesses (a value per step per lane would
+  // keep S * nseg partially read lines live in L2)
+  auto load_chunk = [&](int ts, double (&v)[SL_C]) {
+    const int i0 = ts - sh;
+    if (i0 >= 0 && i0 + SL_C <= T) {
+#pragma unroll
+      for (int j = 0; j < SL_C; j += 2) {
+        const dbl2u p = *reinterpret_cast<const dbl2u*>(x + i0 + j);
+        v[j] = p.x;
+        v[j + 1] = p.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
+    }
+  };
+  // full-window rank constants (uniform)
+  bool full_two;
+  double full_frac = 0.0;
+  if constexpr (MED) {
+    full_two = (W & 1) == 0;
+  } else {
+    const double idxf = A.q * (double)(W - 1);
+    full_two = W > 1 && (double)K != idxf && !A.lower;
+    full_frac = idxf - (double)K;
+  }
+  double s[W];
+#pragma unroll
+  for (int i = 0; i < W; ++i) s[i] = inf;
+  int n = 0;
+  for (int tc = t_start; tc < t_end; tc += SL_C) {
+    double vin[SL_C], vout[SL_C], r[SL_C];
+    load_chunk(tc, vin);
+    if (tc + SL_C - 1 - W >= t_start) load_chunk(tc - W, vout);   // else: placeholders below
+#pragma unroll
+    for (int j = 0; j < SL_C; ++j) {
+      const int t = tc + j;
+      const bool has_out = t - W >= t_start;   // else a placeholder leaves
+      const bool in_num = t < t_end && vin[j] == vin[j];
+      const bool out_num = t < t_end && has_out && vout[j] == vout[j];
+      n += (in_num ? 1 : 0) - (out_num ? 1 : 0);
+      const double v = in_num ? vin[j] + 0.0 : inf;
+      const double o = out_num ? vout[j] + 0.0 : inf;
+      double bp = -inf;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        const double nxt = i + 1 < W ? s[i + 1] : inf;
+        const double b = s[i] < o ? s[i] : nxt;
+        s[i] = max_f64_nn(bp, min_f64_nn(v, b));
+        bp = b;
+      }
+      r[j] = qnan();
+      if (n >= A.minp && n > 0) {
+        if (n == W) {
+          constexpr int K1 = K + 1 < W ? K + 1 : K;
+          const double lo = s[K];
+          if (!full_two) r[j] = lo;
+          else if (MED) r[j] = (lo + s[K1]) / 2.0;
+          else r[j] = lo + (s[K1] - lo) * full_frac;
+        } else {   // partial window: run-time ranks among the n numbers
+          auto get = [&](int k) -> double {
+            unsigned long long m = 0;
+#pragma unroll
+            for (int i = 0; i < W; ++i)
+              m |= (0ull - (unsigned long long)(i == k)) & (unsigned long long)__double_as_longlong(s[i]);
+            return __longlong_as_double((long long)m);
+          };
+          if (MED) {
+            const int h = n >> 1;
+            r[j] = (n & 1) ? get(h) : (get(h - 1) + get(h)) / 2.0;
+          } else if (n == 1) {
+            r[j] = s[0];
+          } else {
+            const double idxf = A.q * (double)(n - 1);
+            const int idx = (int)idxf;
+            if ((double)idx == idxf || A.lower) r[j] = get(idx);
+            else {
+              const double lo = get(idx), hi = get(idx + 1);
+              r[j] = lo + (hi - lo) * (idxf - (double)idx);
+            }
+          }
+        }
+      }
+    }
+    if (tc >= t_begin && tc + SL_C <= t_end) {
+#pragma unroll
+      for (int j = 0; j < SL_C; j += 2) {
+        dbl2u p;
+        p.x = r[j];
+        p.y = r[j + 1];
+        *reinterpret_cast<dbl2u*>(out + tc + j) = p;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j)
+        if (tc + j >= t_begin && tc + j < t_end) out[tc + j] = r[j];
+    }
+  }
+}
+
 // ---- tile rank kernel (wave = 64*OPL consecutive outputs of one symbol) --------------
 // The windows of TILE consecutive outputs all lie in one union of
 // U = w + TILE - 1 consecutive values. The wave loads the union (coalesced:
@@ -1177,6 +1340,60 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
   hipLaunchKernelGGL(bq::rank_kernel<W>, dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
+// slide kernel instantiations: (window, full-window rank K, median) of the
+// strategies' defaults where it wins — ActivityBurstPump's 19-candle medians
+// and LiquidationSweepPump's quantile(0.80, 48). Other (w, q) go to the tile /
+// stencil kernels (w = 60 / 80 / 96 measured no faster, slide_rank_kernel).
+struct SlideCfg {
+  int w, k, med;
+};
+constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}};
+constexpr int kNSlide = (int)(sizeof(kSlide) / sizeof(kSlide[0]));
+
+int slide_variant(int w, int mode, double q) {
+  for (int i = 0; i < kNSlide; ++i) {
+    if (kSlide[i].w != w) continue;
+    if (mode == BQ_ROLL_MEDIAN) {
+      if (kSlide[i].med && kSlide[i].k == ((w & 1) ? w / 2 : w / 2 - 1)) return i;
+    } else if (mode == BQ_ROLL_QUANTILE && !kSlide[i].med && q > 0.0 && q < 1.0 &&
+               kSlide[i].k == (int)(q * (double)(w - 1))) {
+      return i;
+    }
+  }
+  return -1;
+}
+
+// segment length of a slide job: lanes = (symbol, segment), about
+// BQ_SLIDE_WAVES waves per SIMD over 1024 SIMDs (the kernel is VALU-bound and
+// every slot update is independent, so a few waves hide its loads); each
+// segment replays W - 1 warm-up values, so segments stay >= 2 W
+int slide_segment(int w, int64_t S, int64_t T) {
+  static const int waves = [] {
+    const char* e = getenv("BQ_SLIDE_WAVES");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2;
+  }();
+  const int64_t lanes = (int64_t)1024 * waves * 64;
+  const int64_t nseg = lanes / (S > 0 ? S : 1) > 1 ? lanes / (S > 0 ? S : 1) : 1;
+  int64_t seg = (T + nseg - 1) / nseg;
+  if (seg < 2 * w) seg = 2 * w;
+  return (int)(seg < T ? seg : (T > 0 ? T : 1));
+}
+
+template <int W, int K, bool MED>
+void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
+  const unsigned blocks = (unsigned)((items + 255) / 256);
+  hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+}
+
+void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
+  switch (v) {
+    case 0: launch_slide1<19, 9, true>(B, n, items, st); break;
+    default: launch_slide1<48, 37, false>(B, n, items, st);
+  }
+}
+static_assert(kNSlide == 2, "launch_slide covers every kSlide entry");
+
 template <int EPL, int OPL, bool SEL, bool PACK>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
   const int64_t nt = (B.T + bq::WAVE * OPL - 1) / (bq::WAVE * OPL);
@@ -1293,18 +1510,31 @@ void launch_restage_any(int cls, const bq::RollBatch& B, int n, hipStream_t st) 
 // (sorted union per wave), 2 = stencil (sorting network per output, w <= 32).
 // BQ_RANK_IMPL=lane|tile|stencil forces one (measurement; stencil falls back
 // to tile above w = 32).
-int rank_impl(int w, int64_t S, int64_t T) {
+// BQ_RANK_SLIDE=0 keeps large panels on the tile kernel (measurement)
+bool slide_on() {
+  static const bool on = [] {
+    const char* e = getenv("BQ_RANK_SLIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int rank_impl(int w, int64_t S, int64_t T, bool slide) {
   static const int forced = [] {
     const char* e = getenv("BQ_RANK_IMPL");
     return !e ? -1
               : (strcmp(e, "lane") == 0      ? 0
                  : strcmp(e, "tile") == 0    ? 1
                  : strcmp(e, "stencil") == 0 ? 2
+                 : strcmp(e, "slide") == 0   ? 3
                                              : -1);
   }();
-  (void)S;
-  (void)T;
+  if (forced == 3) return slide ? 3 : (w <= 32 ? 2 : 1);
   if (forced >= 0) return forced == 2 && w > 32 ? 1 : forced;
+  // large panels with a slide instantiation: the sorted-register window
+  // (5 VALU per slot and step, against the tile kernel's sort per 64
+  // outputs); live shapes keep the tile / stencil kernels (no warm-up)
+  if (slide && S * T >= (int64_t)(1 << 22) && T >= 4 * (int64_t)w && slide_on()) return 3;
   // short windows: the stencil kernel (coalesced, no warm-up, no per-lane row
   // walk); longer ones: the tile kernel, whose sort is shared by 64 / 128
   // outputs (the lane kernel stays selectable for measurement)
@@ -1420,6 +1650,20 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     }
     ntile[g] = 0;
   };
+  RollBatch slide[kNSlide];
+  int nslide[kNSlide] = {};
+  int64_t slide_items[kNSlide] = {};
+  for (int v = 0; v < kNSlide; ++v) {
+    memset(&slide[v], 0, sizeof(RollBatch));
+    slide[v].S = S;
+    slide[v].T = (int)T;
+  }
+  auto flush_slide = [&](int v) {
+    if (!nslide[v]) return;
+    launch_slide(v, slide[v], nslide[v], slide_items[v], st);
+    nslide[v] = 0;
+    slide_items[v] = 0;
+  };
   RollBatch ff;
   memset(&ff, 0, sizeof(ff));
   ff.S = S;
@@ -1505,11 +1749,19 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       max_back = back > max_back ? back : max_back;
       rep.j[nrep++] = J;
       if (nrep == RW_MAXJOBS) flush_rep();
-    } else if (rank_impl(in.window, S, T) == 2 && S * ((T + SR_NT - 1) / SR_NT) <= 0x7fffffff) {
+    } else if (const int sv = slide_variant(in.window, J.mode, J.q);
+               rank_impl(in.window, S, T, sv >= 0) == 3) {
+      J.seg = slide_segment(in.window, S, T);
+      J.nseg = (int)((T + J.seg - 1) / J.seg);
+      slide[sv].j[nslide[sv]++] = J;
+      const int64_t items = S * (int64_t)J.nseg;
+      slide_items[sv] = items > slide_items[sv] ? items : slide_items[sv];
+      if (nslide[sv] == RW_MAXJOBS) flush_slide(sv);
+    } else if (rank_impl(in.window, S, T, false) == 2 && S * ((T + SR_NT - 1) / SR_NT) <= 0x7fffffff) {
       const int b = stencil_bucket(in.window);
       sten[b].j[nsten[b]++] = J;
       if (nsten[b] == RW_MAXJOBS) flush_sten(b);
-    } else if (rank_impl(in.window, S, T) >= 1) {
+    } else if (rank_impl(in.window, S, T, false) >= 1) {
       const int g = tile_group(in.window, in.mode, in.q) + (in.panel && rank_pack() ? 3 : 0);
       tile[g].j[ntile[g]++] = J;
       if (ntile[g] == RW_MAXJOBS) flush_tile(g);
@@ -1542,6 +1794,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   flush_ff();
   for (int b = 0; b < 6; ++b) flush_rank(b);
   for (int g = 0; g < 6; ++g) flush_tile(g);
+  for (int v = 0; v < kNSlide; ++v) flush_slide(v);
   for (int b = 0; b < 6; ++b) flush_sten(b);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }

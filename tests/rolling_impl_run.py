@@ -12,7 +12,8 @@ from binquant_amd.engine import Ewm, Ffill, Roll
 RANK_JOBS = [(3, "max", 1.0, 1, 1), (6, "min", 0.0, 6, 1), (8, "quantile", 0.3, 4, 0), (12, "median", 0.5, 12, 0),
              (19, "median", 0.5, 19, 2), (24, "quantile", 0.75, 5, 0), (48, "quantile", 0.8, 48, 1),
              (65, "quantile", 0.92, 20, 1), (66, "median", 0.5, 1, 3), (80, "quantile", 0.92, 20, 1),
-             (96, "quantile", 0.05, 30, 0)]
+             (96, "quantile", 0.05, 30, 0), (60, "quantile", 0.85, 20, 1), (96, "qlower", 0.8, 20, 0),
+             (96, "qlower", 0.8, 96, 2)]
 
 
 def panel(S, T):

@@ -1,6 +1,7 @@
 """Both kernel families behind each rolling statistic give the same bits:
-the per-lane sorted window vs the per-wave sorted union vs the per-output
-sorting network (order statistics),
+the per-lane sorted window (a run-time and a register-resident compile-time
+window) vs the per-wave sorted union vs the per-output sorting network
+(order statistics),
 the LDS-ring replay vs the class-specialised re-staging replay (moments, ewm,
 ffill). Each implementation is forced in its own child process
 (BQ_RANK_IMPL / BQ_REPLAY_IMPL) over the same battery — NaN gaps, constant
@@ -32,6 +33,7 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
         "lane_ring": _run(tmp_path, "lane_ring", {"BQ_RANK_IMPL": "lane", "BQ_REPLAY_IMPL": "ring"}),
         "tile_restage": _run(tmp_path, "tile_restage", {"BQ_RANK_IMPL": "tile", "BQ_REPLAY_IMPL": "restage"}),
         "stencil_mixed": _run(tmp_path, "stencil_mixed", {"BQ_RANK_IMPL": "stencil", "BQ_REPLAY_IMPL": "mixed"}),
+        "slide": _run(tmp_path, "slide", {"BQ_RANK_IMPL": "slide"}),
         "restage64": _run(tmp_path, "restage64", {"BQ_REPLAY_IMPL": "restage", "BQ_REPLAY_SPW": "64"}),
         "mixed32": _run(tmp_path, "mixed32", {"BQ_REPLAY_IMPL": "mixed", "BQ_REPLAY_SPW": "32"}),
         "auto": _run(tmp_path, "auto", {}),
@@ -56,6 +58,6 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
     for w, st, q, mp, sh in RANK_JOBS:
         roll = df.shift(sh).rolling(w, min_periods=mp)
         want = (roll.median() if st == "median" else roll.max() if st == "max" else roll.min() if st == "min"
-                else roll.quantile(q)).to_numpy().T
+                else roll.quantile(q, interpolation="lower") if st == "qlower" else roll.quantile(q)).to_numpy().T
         got = ref[f"rank_{w}_{st}_{q}_{mp}_{sh}"]
         np.testing.assert_array_equal(got, want, err_msg=f"w={w} {st} q={q}")

@@ -16,7 +16,7 @@ from binquant_amd.synth import device_panel
 # the pipelines' order-statistic jobs (window, stat, q, min_periods, shift)
 JOBS = [(19, "median", 0.5, 19, 2), (80, "quantile", 0.92, 20, 1), (48, "quantile", 0.80, 48, 1),
         (60, "quantile", 0.85, 20, 1), (3, "max", 1.0, 1, 1), (6, "max", 1.0, 6, 1), (6, "min", 0.0, 6, 1),
-        (96, "median", 0.5, 1, 0), (24, "quantile", 0.3, 5, 0)]
+        (96, "median", 0.5, 1, 0), (24, "quantile", 0.3, 5, 0), (96, "qlower", 0.8, 20, 0)]
 impl = os.environ.get("BQ_RANK_IMPL", "auto")
 for S, T, reps in ((1000, 400, 50), (12_500, 2_000, 10)):
     p = device_panel(S, T, seed=5)
