@@ -669,8 +669,8 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
 // kernel wins and sends any other (w, q) to the tile / stencil kernels), so the
 // full-window output reads two fixed registers; a partial window (warm-up,
 // NaNs) picks its ranks with the masked-OR reads of SortedWin::get.
-// Parallelism: lanes = (symbol, segment); a segment first replays the W - 1
-// values before it (the warm-up, bounded by the host's segment length).
+// Parallelism: lanes = (symbol, segment); a segment first inserts the W - 1
+// values before it (the warm-up, insert-only passes).
 // Measured at 12.5k x 2k (tools/slide_probe.py, identical outputs): median(19)
 // 0.28 (stencil) -> 0.22 ms, quantile(0.80, 48) 0.61 (tile) -> 0.38 ms; at
 // w = 60 / 80 / 96 the W-register window leaves 1-2 waves per SIMD and the
@@ -740,11 +740,34 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
     full_two = W > 1 && (double)K != idxf && !A.lower;
     full_frac = idxf - (double)K;
   }
+  // the window before the segment's first output (the W - 1 values of steps
+  // t_start .. t_begin - 1; NaNs and steps before the row stay +inf): only
+  // insertions while it fills (no value leaves yet), each a clamp pass
+  // s'[i] = max(s[i-1], min(v, s[i])) from the top down — 2 VALU per slot
+  // instead of a full step's 5; the +inf pad in the top slot is what drops.
   double s[W];
 #pragma unroll
   for (int i = 0; i < W; ++i) s[i] = inf;
   int n = 0;
-  for (int tc = t_start; tc < t_end; tc += SL_C) {
+  {
+    constexpr int NCH = (W + SL_C - 1) / SL_C;
+    const int t0 = t_begin - NCH * SL_C;   // step of chunk slot 0
+    for (int c = 0; c < NCH; ++c) {
+      if (t0 + (c + 1) * SL_C <= t_start) continue;   // chunk wholly before the window
+      double v[SL_C];
+      load_chunk(t0 + c * SL_C, v);
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j) {
+        const bool num = t0 + c * SL_C + j >= t_start && v[j] == v[j];
+        n += num ? 1 : 0;
+        const double a = num ? v[j] + 0.0 : inf;
+#pragma unroll
+        for (int i = W - 1; i > 0; --i) s[i] = max_f64_nn(s[i - 1], min_f64_nn(a, s[i]));
+        s[0] = min_f64_nn(a, s[0]);
+      }
+    }
+  }
+  for (int tc = t_begin; tc < t_end; tc += SL_C) {
     double vin[SL_C], vout[SL_C], r[SL_C];
     load_chunk(tc, vin);
     if (tc + SL_C - 1 - W >= t_start) load_chunk(tc - W, vout);   // else: placeholders below
@@ -1341,13 +1364,14 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
 }
 
 // slide kernel instantiations: (window, full-window rank K, median) of the
-// strategies' defaults where it wins — ActivityBurstPump's 19-candle medians
-// and LiquidationSweepPump's quantile(0.80, 48). Other (w, q) go to the tile /
-// stencil kernels (w = 60 / 80 / 96 measured no faster, slide_rank_kernel).
+// strategies' defaults where it wins — ActivityBurstPump's 19-candle medians,
+// LiquidationSweepPump's quantile(0.80, 48), FailedSpikeFade's quantile(0.85,
+// 60) (0.53 vs 0.64 ms on NaN-free rows). Other (w, q) go to the tile /
+// stencil kernels (w = 80 / 96 measured no faster, slide_rank_kernel).
 struct SlideCfg {
   int w, k, med;
 };
-constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}};
+constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}, {60, 50, 0}};
 constexpr int kNSlide = (int)(sizeof(kSlide) / sizeof(kSlide[0]));
 
 int slide_variant(int w, int mode, double q) {
@@ -1389,10 +1413,11 @@ void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st)
 void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
   switch (v) {
     case 0: launch_slide1<19, 9, true>(B, n, items, st); break;
-    default: launch_slide1<48, 37, false>(B, n, items, st);
+    case 1: launch_slide1<48, 37, false>(B, n, items, st); break;
+    default: launch_slide1<60, 50, false>(B, n, items, st);
   }
 }
-static_assert(kNSlide == 2, "launch_slide covers every kSlide entry");
+static_assert(kNSlide == 3, "launch_slide covers every kSlide entry");
 
 template <int EPL, int OPL, bool SEL, bool PACK>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
