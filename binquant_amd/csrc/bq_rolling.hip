@@ -1364,14 +1364,23 @@ void launch_rank(const bq::RollBatch& B, int n, int64_t max_items, hipStream_t s
 }
 
 // slide kernel instantiations: (window, full-window rank K, median) of the
-// strategies' defaults where it wins — ActivityBurstPump's 19-candle medians,
-// LiquidationSweepPump's quantile(0.80, 48), FailedSpikeFade's quantile(0.85,
-// 60) (0.53 vs 0.64 ms on NaN-free rows). Other (w, q) go to the tile /
-// stencil kernels (w = 80 / 96 measured no faster, slide_rank_kernel).
+// strategies' defaults — ActivityBurstPump's 19-candle medians and
+// quantile(0.92, 80), LiquidationSweepPump's quantile(0.80, 48),
+// FailedSpikeFade's quantile(0.85, 60), the leadership's lower quantile
+// (0.80, 96). At 12.5k x 2k on NaN-free rows (tools/slide_probe.py):
+// 0.20 / 0.70 / 0.34 / 0.41 / 0.78 ms against the stencil / tile kernels'
+// 0.28 / 0.73 / 0.60 / 0.60 / 0.82. Other (w, q) go to those kernels.
 struct SlideCfg {
   int w, k, med;
 };
-constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}, {60, 50, 0}};
+#ifndef BQ_SLIDE_BIG
+#define BQ_SLIDE_BIG 1   // 0: w = 80 / 96 on the tile kernel (measurement)
+#endif
+constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}, {60, 50, 0}
+#if BQ_SLIDE_BIG
+                               , {80, 72, 0}, {96, 76, 0}
+#endif
+};
 constexpr int kNSlide = (int)(sizeof(kSlide) / sizeof(kSlide[0]));
 
 int slide_variant(int w, int mode, double q) {
@@ -1414,10 +1423,14 @@ void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream
   switch (v) {
     case 0: launch_slide1<19, 9, true>(B, n, items, st); break;
     case 1: launch_slide1<48, 37, false>(B, n, items, st); break;
+#if BQ_SLIDE_BIG
+    case 3: launch_slide1<80, 72, false>(B, n, items, st); break;
+    case 4: launch_slide1<96, 76, false>(B, n, items, st); break;
+#endif
     default: launch_slide1<60, 50, false>(B, n, items, st);
   }
 }
-static_assert(kNSlide == 3, "launch_slide covers every kSlide entry");
+static_assert(kNSlide == 3 + 2 * BQ_SLIDE_BIG, "launch_slide covers every kSlide entry");
 
 template <int EPL, int OPL, bool SEL, bool PACK>
 void launch_tile_rank(const bq::RollBatch& B, int n, hipStream_t st) {
