@@ -306,7 +306,7 @@ def bench_breadth(args, panel, world, dev):
     }
 
 
-def _time_call(fn, reps=3):
+def _time_call(fn, reps=10):
     fn()
     torch.cuda.synchronize()
     s = torch.cuda.current_stream()
