@@ -666,9 +666,10 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
 // pure function of the multiset, so the outputs equal the other kernels' bit
 // for bit. The quantile's rank K = int(q (w - 1)) of a full window is a
 // template constant (the host has an instantiation per (W, K) where this
-// kernel wins and sends any other (w, q) to the tile / stencil kernels), so the
-// full-window output reads two fixed registers; a partial window (warm-up,
-// NaNs) picks its ranks with the masked-OR reads of SortedWin::get.
+// kernel wins and sends any other (w, q) to the tile / stencil kernels), and
+// the placeholders are split between -inf at the bottom and +inf at the top
+// so that the wanted rank of ANY window count n sits in slot K: every output
+// reads two fixed registers.
 // Parallelism: lanes = (symbol, segment); a segment first inserts the W - 1
 // values before it (the warm-up, insert-only passes).
 // Measured at 12.5k x 2k (tools/slide_probe.py, identical outputs): median(19)
@@ -730,16 +731,20 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
     }
   };
-  // full-window rank constants (uniform)
-  bool full_two;
-  double full_frac = 0.0;
-  if constexpr (MED) {
-    full_two = (W & 1) == 0;
-  } else {
-    const double idxf = A.q * (double)(W - 1);
-    full_two = W > 1 && (double)K != idxf && !A.lower;
-    full_frac = idxf - (double)K;
-  }
+  // Placeholders split so the wanted rank sits in a FIXED slot: with n
+  // numbers in the window, a(n) = int(q (n - 1)) (median: (n - 1) / 2) and
+  // B(n) = K - a(n) placeholders at the bottom (-inf), the rest at the top
+  // (+inf), the a-th smallest number is s[K] and the next one s[K + 1] for any
+  // n (B(n) + n <= W since q < 1). n changes by at most 1 per step and B by
+  // at most 1 with it, so a step keeps the split by choosing which kind of
+  // placeholder leaves or enters (a NaN leaving or entering is a placeholder
+  // leaving or entering). No run-time register index anywhere: partial
+  // windows (warm-up, NaN gaps, min_periods < w) cost what full ones do.
+  auto a_of = [&](int nn) -> int {
+    if constexpr (MED) return (nn - 1) >> 1;
+    else return (int)(A.q * (double)(nn - 1));
+  };
+  auto b_of = [&](int nn) -> int { return nn >= 1 ? K - a_of(nn) : K + 1; };
   // the window before the segment's first output (the W - 1 values of steps
   // t_start .. t_begin - 1; NaNs and steps before the row stay +inf): only
   // insertions while it fills (no value leaves yet), each a clamp pass
@@ -767,6 +772,16 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       }
     }
   }
+  // then B(n) of the W - n top placeholders move to the bottom: the array
+  // shifted up by B (a log-step barrel shift, -inf filling; the B slots that
+  // drop off the top are +inf)
+  int nb = b_of(n);
+#pragma unroll
+  for (int bit = 1; bit < W; bit <<= 1) {
+    const bool sh_on = (nb & bit) != 0;
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) s[i] = sh_on ? (i >= bit ? s[i - bit] : -inf) : s[i];
+  }
   for (int tc = t_begin; tc < t_end; tc += SL_C) {
     double vin[SL_C], vout[SL_C], r[SL_C];
     load_chunk(tc, vin);
@@ -777,9 +792,15 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       const bool has_out = t - W >= t_start;   // else a placeholder leaves
       const bool in_num = t < t_end && vin[j] == vin[j];
       const bool out_num = t < t_end && has_out && vout[j] == vout[j];
-      n += (in_num ? 1 : 0) - (out_num ? 1 : 0);
-      const double v = in_num ? vin[j] + 0.0 : inf;
-      const double o = out_num ? vout[j] + 0.0 : inf;
+      const int n2 = n + (in_num ? 1 : 0) - (out_num ? 1 : 0);
+      const int nb2 = b_of(n2);
+      // a leaving placeholder is a bottom one when B drops, an entering one a
+      // bottom one when B grows (otherwise top; both top when nothing changes:
+      // removing an absent +inf and inserting +inf leaves the array as is)
+      const double o = out_num ? vout[j] + 0.0 : (nb2 < nb ? -inf : inf);
+      const double v = in_num ? vin[j] + 0.0 : (nb2 > nb ? -inf : inf);
+      n = n2;
+      nb = nb2;
       double bp = -inf;
 #pragma unroll
       for (int i = 0; i < W; ++i) {
@@ -790,34 +811,14 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       }
       r[j] = qnan();
       if (n >= A.minp && n > 0) {
-        if (n == W) {
-          constexpr int K1 = K + 1 < W ? K + 1 : K;
-          const double lo = s[K];
-          if (!full_two) r[j] = lo;
-          else if (MED) r[j] = (lo + s[K1]) / 2.0;
-          else r[j] = lo + (s[K1] - lo) * full_frac;
-        } else {   // partial window: run-time ranks among the n numbers
-          auto get = [&](int k) -> double {
-            unsigned long long m = 0;
-#pragma unroll
-            for (int i = 0; i < W; ++i)
-              m |= (0ull - (unsigned long long)(i == k)) & (unsigned long long)__double_as_longlong(s[i]);
-            return __longlong_as_double((long long)m);
-          };
-          if (MED) {
-            const int h = n >> 1;
-            r[j] = (n & 1) ? get(h) : (get(h - 1) + get(h)) / 2.0;
-          } else if (n == 1) {
-            r[j] = s[0];
-          } else {
-            const double idxf = A.q * (double)(n - 1);
-            const int idx = (int)idxf;
-            if ((double)idx == idxf || A.lower) r[j] = get(idx);
-            else {
-              const double lo = get(idx), hi = get(idx + 1);
-              r[j] = lo + (hi - lo) * (idxf - (double)idx);
-            }
-          }
+        constexpr int K1 = K + 1 < W ? K + 1 : K;
+        const double lo = s[K];
+        if constexpr (MED) {
+          r[j] = (n & 1) ? lo : (lo + s[K1]) / 2.0;
+        } else {
+          const double idxf = A.q * (double)(n - 1);
+          const int idx = (int)idxf;
+          r[j] = ((double)idx == idxf || A.lower) ? lo : lo + (s[K1] - lo) * (idxf - (double)idx);
         }
       }
     }
