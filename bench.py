@@ -22,10 +22,13 @@ Also reported (same JSON line):
                  time-bounded sample;
   tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
                  latency p50/p99;
-  breadth      — C5 leg: the fused panel context build (bq_context_partials:
-                 features reduced straight into the [T x 10] partials) + ONE
-                 all-reduce of the partials (tracked count folded in), with its
-                 roofline on 24 B/candle and the unfused pair timed beside it;
+  breadth      — C5 (configs[4]) end to end: market_context_batch = the fused
+                 panel context build (bq_context_partials: features reduced
+                 straight into the [T x 10] partials) + ONE all-reduce of the
+                 partials (tracked count folded in) + host scoring and regime
+                 annotation of all T contexts; the kernel's roofline on
+                 24 B/candle, the reduction and scoring times, the unfused pair
+                 timed beside it;
   rows         — every other SURVEY §8 row on the device at 12 500 x 2 000
                  (HIP-event time per call, algorithmic bytes -> GB/s and
                  fraction of HBM peak) with a bounded CPU timing of the
@@ -173,12 +176,26 @@ def host_cores() -> dict:
             "omp_num_threads": int(omp) if omp.isdigit() else None, "share": max(1, share)}
 
 
+def cpu_model() -> str | None:
+    """The host CPU's model name (/proc/cpuinfo), e.g. for BASELINE.md's plan."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args):
     import multiprocessing as mp
 
     cores = host_cores()
     workers = args.cpu_workers if args.cpu_workers > 0 else cores["share"]
     T = args.cpu_candles
+    # single core, alone on the host (before the pool): the same call pattern in this process
+    sc_done, sc_spent, sc_syms = _cpu_worker((999, T, min(4.0, args.cpu_seconds)))
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
@@ -192,6 +209,9 @@ def cpu_baseline(args):
         "unit": "symbol-candles/s",
         "cores": workers,
         "kind": "port",
+        "cpu_model": cpu_model(),
+        "single_core": {"value": sc_done / sc_spent, "unit": "symbol-candles/s", "cores": 1,
+                        "sample": f"{sc_syms} symbols x {T}-candle frames, one process alone on the host"},
         "host": cores,
         "sample": f"C1: {syms} symbols x {T}-candle frames, per symbol pandas indicators_enrichment (14 columns) "
         f"+ _compute_symbol_features on the last 400 bars (oracle restatement of the reference call pattern), "
@@ -260,30 +280,59 @@ CONTEXT_BYTES_PER_CANDLE = 3 * 8   # C5: high, low, close read once; the [T x 10
 
 
 def bench_breadth(args, panel, world, dev):
-    """C5 leg: the fused panel context build (bq_context_partials: features
-    reduced straight into the [T x 10] partials, the feature columns never
-    written) -> ONE all-reduce(sum) of the partials (tracked-symbol count
-    folded into the spare column; market_regime.batch.reduce_partials, RCCL
-    over xGMI at N > 1). Roofline on the algorithmic bytes: 3 fp64 inputs
-    per candle (the group records the kernels exchange are intermediate);
-    the unfused features + breadth_partial pair is timed beside it."""
+    """C5 (BASELINE configs[4]): breadth / context SCORING at every timestamp
+    of the shard, end to end through the product API
+    market_regime.batch.market_context_batch(keep_features=False):
+    bq_context_partials (features reduced straight into the [T x 10]
+    partials, the feature columns never written) -> ONE all-reduce(sum) of
+    the partials (tracked-symbol count folded into the spare column;
+    reduce_partials, RCCL over xGMI at N > 1) -> the benchmark's feature row
+    -> D2H of the partials -> host scoring (score_contexts) and market-regime
+    annotation (annotate_market) of all T contexts. Roofline on the kernel's
+    algorithmic bytes: 3 fp64 inputs per candle (the group records the
+    kernel's passes exchange are intermediate); the unfused features +
+    breadth_partial pair is timed beside it."""
+    from binquant_amd.market_regime.batch import contexts_from_partials, market_context_batch
+
     h, l, c = panel["high"], panel["low"], panel["close"]
     S, T = c.shape
+    btc_hlc = (h[:1], l[:1], c[:1])   # the benchmark row (replicated on every rank)
+    tss = 1_700_000_000_000 + 900_000 * np.arange(T, dtype=np.int64)
     part, _ = engine.context_partials(h, l, c, max_bars=400)
     steps = max(1, args.breadth_steps)
     stream = torch.cuda.current_stream()
+    # (1) the kernel alone, HIP events on its stream (the roofline)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier(world)
-    t0 = time.perf_counter()
     for i in range(steps):
         evs[i][0].record(stream)
         engine.context_partials(h, l, c, max_bars=400, out=part)
         evs[i][1].record(stream)
-        _, n_total = reduce_partials(part, S)
     barrier(world)
-    dt = max_over_ranks(time.perf_counter() - t0, world) / steps
     kern_ms = max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in evs])), world)
     achieved = S * T * CONTEXT_BYTES_PER_CANDLE / (kern_ms * 1e-3) / 1e9
+    # (2) the whole C5 step: partials + all-reduce + scoring + annotation of T contexts
+    market_context_batch(h, l, c, btc_hlc, timestamps=tss, keep_features=False)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = market_context_batch(h, l, c, btc_hlc, timestamps=tss, keep_features=False)
+    barrier(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world) / steps
+    n_total = int(res.contexts.fields["total_tracked_symbols"][-1]) if res.contexts.valid.any() else S * world
+    # the parts: the reduction alone, and host scoring + annotation (from the reduced partials on the host)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, n_red = reduce_partials(part, S)
+    barrier(world)
+    reduce_ms = max_over_ranks(time.perf_counter() - t0, world) / steps * 1e3
+    ph = res.partial.cpu().numpy()
+    bret = np.zeros(T)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        contexts_from_partials(ph, bret, bret, total_tracked=n_red, timestamps=tss)
+    scoring_ms = (time.perf_counter() - t0) / steps * 1e3
     # the unfused pair (what round 2 ran): features written, re-read by breadth_partial
     feats = engine.market_features(h, l, c, max_bars=400)
     up = engine.breadth_partial(c, feats)
@@ -295,12 +344,19 @@ def bench_breadth(args, panel, world, dev):
         "value": n_total * T / dt,
         "unit": "symbol-candles/s",
         "ms_per_step": dt * 1e3,
+        "kernel_ms": kern_ms,
+        "reduce_ms": reduce_ms,
+        "scoring_ms": scoring_ms,
+        "contexts": T,
+        "valid_contexts": int(res.contexts.valid.sum()),
         "tracked_symbols": n_total,
-        "workload": f"{S} symbols x {T} candles per GPU, max_bars 400, fused features -> partials"
-        + (" + one RCCL all_reduce of [T x 10] fp64" if world > 1 else ""),
+        "workload": f"{S} symbols x {T} candles per GPU, max_bars 400: market_context_batch(keep_features=False) = "
+                    f"fused features -> [T x 10] partials, "
+                    + ("one RCCL all_reduce, " if world > 1 else "")
+                    + "benchmark features, D2H, score_contexts + annotate_market of all T contexts",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "bq_context_partials (3 launches)", "kernel_ms": kern_ms,
+                     "kernel": "bq_context_partials", "kernel_ms": kern_ms,
                      "algorithmic_bytes_per_candle": CONTEXT_BYTES_PER_CANDLE, "candles_per_launch": S * T},
         "unfused_ms": unfused_ms,
     }

@@ -67,13 +67,15 @@ __device__ __forceinline__ void pn_load(const double* __restrict__ row, int tb, 
 
 __device__ __forceinline__ bool pn_aligned(const void* p, int64_t ld) { return (((uintptr_t)p) & 15u) == 0 && (ld % 2) == 0; }
 
-// exclusive block max of a per-lane int >= -1 combined with `carry`
-__device__ __forceinline__ int pn_block_excl_max(int v, int carry, int* sW, int lane, int w) {
+// exclusive block max of a per-lane int >= -1 combined with the tile carry
+// `*carry` — read after the barrier: the previous tile's last thread writes it
+// after that tile's final barrier, so a read before this one would race
+__device__ __forceinline__ int pn_block_excl_max(int v, const int* carry, int* sW, int lane, int w) {
   const int inc = wave_scan_max_dpp(v + 1, lane) - 1;
   if (lane == WAVE - 1) sW[w] = inc;
   const int lpre = dpp_i32<DPP_WAVE_SHR1>(inc + 1) - 1;
   __syncthreads();
-  int c = max(carry, lpre);
+  int c = max(*carry, lpre);
   for (int u = 0; u < w; ++u) c = max(c, sW[u]);
   return c;
 }
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(PN_NT) void panel_window_kernel(const PanelBatch B)
         lcl[k] = run;
         pv = c[k];
       }
-      const int carry = pn_block_excl_max(lcl[PN_K - 1], sCar, sW, lane, w);
+      const int carry = pn_block_excl_max(lcl[PN_K - 1], &sCar, sW, lane, w);
 #pragma unroll
       for (int k = 0; k < PN_K; ++k) lcl[k] = max(lcl[k], carry);
     }

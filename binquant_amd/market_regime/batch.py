@@ -75,15 +75,18 @@ def shard_bounds(n_symbols: int, world: int, rank: int) -> tuple[int, int]:
 TRACKED_COLUMN = 9   # PARTIAL_COLUMNS[9]: symbols tracked by the shard
 
 
-def reduce_partials(part: torch.Tensor, n_local: int, group=None) -> tuple[torch.Tensor, int]:
+def reduce_partials(part: torch.Tensor, n_local: int, group=None, force: bool = False) -> tuple[torch.Tensor, int]:
     """ONE all_reduce(sum) of the [T, 10] partials over the symbol shards (RCCL
     over xGMI on GPUs, gloo on CPU). The shard's tracked-symbol
     count rides in the spare column 9 of every row, so the admission gate's
     total (live_market_context_accumulator.py:96-102) needs no second
     collective. Returns (reduced partials, total tracked symbols); on one
-    rank the partials are returned with column 9 = n_local."""
+    rank the partials are returned with column 9 = n_local.
+
+    force=True runs the collective whenever a process group is initialised,
+    even at world size 1 (the one-GPU RCCL check, tests/test_rccl_gpu.py)."""
     part[:, TRACKED_COLUMN] = float(n_local)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized() and (force or dist.get_world_size(group) > 1):
         # no timestamps (T == 0, the same on every rank): the count alone travels,
         # so every rank still agrees on the admission gate's total
         buf = part if part.shape[0] else torch.full((1, part.shape[1]), float(n_local), dtype=part.dtype,

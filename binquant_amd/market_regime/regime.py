@@ -210,7 +210,13 @@ def market_transition_event(prev: str, cur: str) -> str:
 def annotate_market(batch: ContextBatch, previous: dict | None = None) -> ContextBatch:
     """RegimeTransitionDetector._annotate_market_regime over every valid
     timestamp in order; each context's predecessor is the latest earlier valid
-    one (accumulator._get_previous_context, :86-93), seeded by `previous`."""
+    one (accumulator._get_previous_context, :86-93), seeded by `previous`.
+
+    Vectorised over T: a context depends on its predecessor's regime and four
+    scores only, so the predecessor arrays are the valid contexts shifted by
+    one (the seed first); `regime_stable_since` is the timestamp of the latest
+    run start (a change of regime, or a predecessor without a stable-since)
+    carried forward by a running max of the start indices."""
     f = batch.fields
     sc = market_scores(f)
     regime = classify_market(sc, f["market_stress_score"])
@@ -220,31 +226,49 @@ def annotate_market(batch: ContextBatch, previous: dict | None = None) -> Contex
     strength = np.zeros(T)
     transitioning = regime == "TRANSITIONAL"
     stable_since = np.full(T, None, dtype=object)
-    prev = previous
-    for i in np.flatnonzero(batch.valid):
-        cur = regime[i]
-        if prev is not None:
-            prev_regime[i] = prev["market_regime"]
-            if prev["market_regime"] is not None and prev["market_regime"] != cur:
-                transition[i] = market_transition_event(prev["market_regime"], cur)
-                cur_scores = (sc["long"][i], sc["short"][i], sc["range"][i], sc["stress"][i])
-                prev_scores = (prev["long_regime_score"], prev["short_regime_score"], prev["range_regime_score"],
-                               prev["stress_regime_score"])
-                dominant = max(cur_scores)
-                strength[i] = min(1.0, max(0.0, dominant + max(abs(a - b) for a, b in zip(cur_scores, prev_scores)) - 0.25))
-                transitioning[i] = transitioning[i] or strength[i] >= TRANSITION_STRENGTH_FLOOR
-        if prev is None or prev["market_regime"] != cur or prev.get("regime_stable_since") is None:
-            stable_since[i] = int(batch.timestamp[i])
+    vi = np.flatnonzero(batch.valid)
+    n = len(vi)
+    if n:
+        cur = regime[vi]
+        seed_regime = None if previous is None else previous["market_regime"]
+        pr = np.empty(n, dtype=object)
+        pr[0] = seed_regime
+        pr[1:] = cur[:-1]
+        if previous is not None:
+            prev_regime[vi] = pr
         else:
-            stable_since[i] = prev["regime_stable_since"]
-        prev = dict(
-            market_regime=cur,
-            long_regime_score=sc["long"][i],
-            short_regime_score=sc["short"][i],
-            range_regime_score=sc["range"][i],
-            stress_regime_score=sc["stress"][i],
-            regime_stable_since=stable_since[i],
-        )
+            prev_regime[vi[1:]] = pr[1:]
+        has_prev = np.ones(n, dtype=bool)
+        has_prev[0] = previous is not None
+        changed = has_prev & np.not_equal(pr, None) & (pr != cur)
+        names = ("long", "short", "range", "stress")
+        keys = ("long_regime_score", "short_regime_score", "range_regime_score", "stress_regime_score")
+        cs = np.stack([sc[k][vi] for k in names])          # [4, n]
+        ps = np.empty_like(cs)
+        ps[:, 1:] = cs[:, :-1]
+        ps[:, 0] = [previous[k] for k in keys] if changed[0] else 0.0
+        ci = np.flatnonzero(changed)
+        if len(ci):
+            dominant = cs[:, ci].max(axis=0)
+            delta = np.abs(cs[:, ci] - ps[:, ci]).max(axis=0)
+            st = np.fmin(1.0, np.fmax(0.0, (dominant + delta) - 0.25))   # Python min(1, max(0, x))
+            idx = vi[ci]
+            strength[idx] = st
+            transitioning[idx] = transitioning[idx] | (st >= TRANSITION_STRENGTH_FLOOR)
+            transition[idx] = [market_transition_event(a, b) for a, b in zip(pr[ci], cur[ci])]
+        # run starts: no predecessor, a different regime, or a predecessor without stable-since
+        start = ~has_prev | (pr != cur)
+        carried = None
+        if not start[0]:
+            carried = previous.get("regime_stable_since")
+            start[0] = carried is None
+        ts = batch.timestamp[vi]
+        last = np.maximum.accumulate(np.where(start, np.arange(n), -1))
+        ss = np.empty(n, dtype=object)
+        ok = last >= 0
+        ss[ok] = np.asarray(ts[last[ok]], dtype=np.int64).astype(object)   # Python ints, as int(ts)
+        ss[~ok] = carried   # a seed run continuing from `previous`
+        stable_since[vi] = ss
     f.update(
         market_regime=regime,
         previous_market_regime=prev_regime,

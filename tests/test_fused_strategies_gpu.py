@@ -161,16 +161,26 @@ def test_spike_fused_equals_staged(cuda):
     assert staged["label"].sum().item() > 0
 
 
-@pytest.mark.parametrize("S,T", [(7, 1001), (3, 5), (1, 1025), (5, 2)])
+@pytest.mark.parametrize("S,T", [(7, 1001), (3, 5), (1, 1025), (5, 2), (6, 4500)])
 def test_fused_odd_shapes_equal_staged(cuda, S, T):
     """Odd T (rows not 16-byte aligned: the scalar load / store paths, byte
     flags unaligned), tiny rows and a partial second tile: the three fused
     paths against their staged pipelines — burst bit for bit, pump / spike to
-    1e-12 / the z-score bound as above, flags equal."""
+    1e-12 / the z-score bound as above, flags equal. At T = 4500, halted
+    stretches (constant price, zero volume) and a NaN stretch cross the 1024 /
+    2048 / 4096-candle tile boundaries, so every cross-tile carry (volume run
+    start, ffill index, ring halo) is exercised."""
     from binquant_amd import engine, strategies
     from binquant_amd.synth import numpy_panel
 
     p = numpy_panel(S, T, seed0=S * 100 + T, edges=T > 50)
+    if T > 4150:
+        for s, (a, b) in enumerate(((1010, 1040), (2030, 2100), (4080, 4150))):
+            for f in ("open", "high", "low", "close"):
+                p[f][s, a:b] = p["close"][s, a]
+            p["volume"][s, a:b] = 0.0
+            p["volume"][s + 3, a:b] = 0.0
+        p["close"][5, 2040:2056] = np.nan
     d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
     qv = d["volume"] * d["close"]
     btc = d["close"][0].clone()
@@ -212,5 +222,5 @@ def test_fused_odd_shapes_equal_staged(cuda, S, T):
                 if name == "spike" and k in zb:   # the cancellation bound of test_spike_fused_equals_staged
                     sd, base = zb[k]
                     lim = lim + 1e-13 * np.abs(base) / (sd + 1e-6)
-                ok = np.isnan(y) | (np.abs(x - y) <= lim)
+                ok = np.isnan(y) | (x == y) | (np.abs(x - y) <= lim)   # x == y: equal infinities (v / 0)
             assert ok.all(), (name, k, int((~ok).sum()))

@@ -30,10 +30,16 @@ def _panel(S, T, seed, signed=False):
     x[5] = np.nan                        # all missing
     x[6, 1000:1400] = 3.25               # a long constant run (past the window)
     x[7, 700:760] = 0.0                  # zeros
+    if T > 2100:                         # runs crossing the 2048-candle tile boundary (the run-start carry)
+        x[8, 2030:2100] = x[8, 2030]
+        x[9, 2030:2100] = 0.0
+    if T > 4150:                         # ... and the second one
+        x[10, 4080:4150] = x[10, 4080]
+        x[11, 4080:4150] = 0.0
     return x
 
 
-@pytest.mark.parametrize("T", [700, 2048, 2500])
+@pytest.mark.parametrize("T", [700, 2048, 2500, 4500])
 @pytest.mark.parametrize("signed", [False, True])
 def test_panel_sum_mean_vs_pandas(cuda, T, signed):
     x = _panel(40, T, seed=T + signed, signed=signed)
@@ -52,7 +58,7 @@ def test_panel_sum_mean_vs_pandas(cuda, T, signed):
                 scale = np.nanmax(np.abs(x[s])) * w if np.isfinite(x[s]).any() else 1.0
                 assert_close(g[s], want, f"{st} w={w} mp={mp} sh={sh} row {s}", rtol=1e-9, scale=scale)
                 # constant windows: pandas returns the value exactly (same-value rule)
-                if s in (0, 6):
+                if s in (0, 6, 8, 9, 10, 11):
                     const = pd.Series(x[s]).shift(sh).rolling(w, min_periods=max(mp, 1)).apply(
                         lambda a: float(np.all(a[~np.isnan(a)] == a[~np.isnan(a)][-1])) if (~np.isnan(a)).any()
                         else 0.0, raw=True).to_numpy() > 0

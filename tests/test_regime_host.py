@@ -74,3 +74,41 @@ def test_vectorised_scoring_matches_reference(label):
             wf = want["symbol_features"][s]
             assert ann["micro_regime"][j] == wf["micro_regime"], s
             assert ann["micro_regime_strength"][j] == pytest.approx(wf["micro_regime_strength"], abs=1e-12)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_vectorised_annotation_chain_matches_sequential(seed):
+    """annotate_market over T timestamps at once (predecessor arrays, run
+    starts by a running max) against the oracle's one-context-at-a-time
+    _annotate_market_regime chained through each previous valid context
+    (accumulator._get_previous_context): regimes, transitions, strengths and
+    regime_stable_since equal on random partials with gaps in validity and
+    every kind of seed context."""
+    rng = np.random.default_rng(seed)
+    T, S = 400, 120
+    n = np.where(rng.random(T) < 0.15, rng.integers(0, 60, T), S).astype(float)
+    adv = np.floor(n * rng.random(T))
+    dec = np.floor((n - adv) * rng.random(T))
+    P = np.stack([n, adv, dec, np.floor(n * rng.random(T)), np.floor(n * rng.random(T)),
+                  rng.normal(0, 0.03, T) * n, rng.normal(0, 0.01, T) * n, rng.uniform(0, 0.06, T) * n,
+                  rng.uniform(0, 0.25, T) * n, np.zeros(T)], 1)
+    br, bt, bv = rng.normal(0, 0.03, T), rng.normal(0, 0.02, T), rng.random(T) > 0.1
+    ts = 1_700_000_000_000 + 900_000 * np.arange(T)
+    seeds = [None, {"market_regime": None},
+             {"market_regime": "RANGE", "long_regime_score": 0.3, "short_regime_score": 0.2,
+              "range_regime_score": 0.6, "stress_regime_score": 0.1, "regime_stable_since": 5},
+             {"market_regime": "TRANSITIONAL", "long_regime_score": 0.3, "short_regime_score": 0.3,
+              "range_regime_score": 0.3, "stress_regime_score": 0.3}]
+    for seed_ctx in seeds:
+        batch = annotate_market(score_contexts(P, br, bt, bv, total_tracked=S, timestamps=ts), seed_ctx)
+        prev = seed_ctx
+        for i in range(T):
+            got = batch.context_at(i)
+            if got is None:
+                continue
+            want = market_ref.annotate_market(got, prev)
+            for k in ("market_regime", "previous_market_regime", "market_regime_transition",
+                      "market_regime_transition_strength", "regime_is_transitioning", "regime_stable_since",
+                      "long_regime_score", "short_regime_score", "range_regime_score", "stress_regime_score"):
+                assert got[k] == want[k], (seed_ctx, i, k, got[k], want[k])
+            prev = want
