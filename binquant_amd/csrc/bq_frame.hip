@@ -33,33 +33,6 @@ __device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
   return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
 }
 
-// first index i in [0, n) with ts[i] >= key (n if none)
-__device__ __forceinline__ int lower_bound_i64(const int64_t* __restrict__ ts, int n, int64_t key) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (ts[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// lower_bound with a guess first: on a regular grid (the kline rows) the
-// index of key is (key - ts[0]) / step with step = (ts[n-1] - ts[0]) / (n - 1);
-// the guess is taken only when ts[g-1] < key <= ts[g] holds, so the result is
-// lower_bound's for any row (a gap or an irregular row falls back to the
-// binary search): two loads instead of ~11 dependent ones per search.
-__device__ __forceinline__ int lower_bound_guess(const int64_t* __restrict__ ts, int n, int64_t key, int64_t t0v,
-                                                 int64_t step) {
-  if (step > 0) {
-    int64_t g = key <= t0v ? 0 : (key - t0v + step - 1) / step;
-    g = g > n ? n : g;
-    const bool ok = (g == 0 || ts[g - 1] < key) && (g == n || ts[g] >= key);
-    if (ok) return (int)g;
-  }
-  return lower_bound_i64(ts, n, key);
-}
-
 __device__ __forceinline__ int row_len(const int64_t* lens, int64_t s, int T) {
   if (!lens) return T;
   const int64_t n = lens[s];

@@ -1032,6 +1032,43 @@ def align(ts: torch.Tensor, bench_ts: torch.Tensor, bench_val: torch.Tensor, len
     return out
 
 
+LEADERSHIP_FUSED = dict(lookback=96, rank=76, long_max=31)   # bq_leadership's compiled configuration
+
+
+@device_entry
+def leadership(open_time: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
+               rs_quantile: float = 0.80, lookback: int = 96, min_history: int = 100, min_count: int = 20,
+               short: int = 8, long: int = 24, stream: torch.cuda.Stream | None = None):
+    """GradualGainerRetest._leadership_allows at every prefix t
+    (strategies/gradual_gainer_retest.py:131-196) in two passes (bq_leadership):
+    returns {"leader": bool [S, T], "rs_2h": [S, T], "rs_6h": [S, T]}, or None
+    when the parameters are not the compiled ones (RS_LOOKBACK 96, int(q * 95)
+    == 76, long <= 31): the caller then runs the staged pipeline."""
+    if lookback != LEADERSHIP_FUSED["lookback"] or int(rs_quantile * (lookback - 1)) != LEADERSHIP_FUSED["rank"] \
+            or not 0.0 <= rs_quantile < 1.0 or not 1 <= short <= long <= LEADERSHIP_FUSED["long_max"] \
+            or min_count < 1 or min_history < 0:
+        return None
+    close = _check_panel(close, "close").contiguous()
+    S, T = close.shape
+    ts = _check_ts(open_time)
+    if tuple(ts.shape) != (S, T):
+        raise ValueError(f"open_time: expected shape {(S, T)}, got {tuple(ts.shape)}")
+    bts = _check_ts(bench_ts, "bench_ts").reshape(-1).contiguous()
+    bc = _check_panel(bench_close.reshape(1, -1), "bench_close", (1, bts.numel())).contiguous()
+    dev = close.device
+    leader = torch.empty((S, T), dtype=torch.bool, device=dev)
+    rs2 = torch.empty((S, T), dtype=torch.float64, device=dev)
+    rs6 = torch.empty_like(rs2)
+    lib = _lib.load()
+    nbytes = int(lib.bq_leadership_workspace_bytes(S, T))
+    ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)   # caching allocator: 512-B aligned
+    st = lib.bq_leadership(_ptr(ts), T, _ptr(close), T, S, T, _ptr(bts), _ptr(bc), bts.numel(), float(rs_quantile),
+                           int(lookback), int(min_history), int(min_count), int(short), int(long), _ptr(ws), nbytes,
+                           _ptr(leader), _ptr(rs2), _ptr(rs6), T, _stream_handle(stream))
+    _lib.check(st, "bq_leadership")
+    return {"leader": leader, "rs_2h": rs2, "rs_6h": rs6}
+
+
 @device_entry
 def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
                  lens=None, stream: torch.cuda.Stream | None = None):

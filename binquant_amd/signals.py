@@ -188,6 +188,9 @@ def top_gainer_features(o, h, l, c, v, qv=None, atr=None, min_history: int = 56,
     return out, status_f.to(torch.int8)
 
 
+_LEADERSHIP_FUSED = True   # False: the staged pipeline for every parameter set (tests)
+
+
 def gradual_gainer_leadership(open_time: torch.Tensor, close: torch.Tensor, btc_time: torch.Tensor,
                               btc_close: torch.Tensor, rs_quantile: float = 0.80, rs_lookback: int = 96,
                               min_history: int = 100, min_count: int = 20, short: int = 8, long: int = 24):
@@ -210,7 +213,20 @@ def gradual_gainer_leadership(open_time: torch.Tensor, close: torch.Tensor, btc_
     Returns {"leader": bool [S, T], "rs_2h": [S, T], "rs_6h": [S, T]} with the
     method's fall-backs: (False, 0.0, 0.0) when the strengths are None or the
     frame is shorter than min_history, (False, rs_2h, rs_6h) when fewer than
-    min_count history entries exist."""
+    min_count history entries exist.
+
+    The strategy's own parameters run in two passes (engine.leadership,
+    bq_leadership); any others run the staged pipeline below. A NaN close is
+    not > 0 here, so it never enters the history or the strengths; the
+    reference's Python min(...) skips a NaN unless it is its first argument
+    (:148, :178) and can append NaN strengths, whose place in sorted() is
+    undefined: frames with missing closes are parity-unpinned (the golden
+    frames hold none; pre_process drops such rows before the strategies)."""
+    fused = engine.leadership(open_time, close, btc_time, btc_close, rs_quantile, rs_lookback, min_history,
+                              min_count, short, long) if _LEADERSHIP_FUSED else None
+    if fused is not None:   # the strategy's own parameters: two passes (bq_leadership)
+        return fused
+    # any other parameters: the staged pipeline
     S, T = close.shape
     recent = long + 1
     b = engine.align(open_time, btc_time, btc_close)

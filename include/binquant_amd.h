@@ -224,6 +224,27 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
                         int32_t max_bars, void* workspace, size_t workspace_bytes,
                         double* partial, double* const* last_feat, void* stream);
 
+/*
+ * GradualGainerRetest relative-strength leadership at every prefix t
+ * (GradualGainerRetest._leadership_allows + _relative_strengths,
+ * strategies/gradual_gainer_retest.py:131-196): open_time [S][ld_ts] int64 ms
+ * and close [S][ld_c] of the panel, the benchmark frame bench_ts [nb]
+ * (ascending; a duplicated time keeps the later row) / bench_close [nb].
+ * Outputs [S][ld_out]: leader (0 / 1 bytes) and rs_2h / rs_6h as the method
+ * returns them ((False, 0.0, 0.0) when the strengths are None or the frame
+ * is shorter than min_history). Compiled for the strategy's RS_LOOKBACK 96
+ * and int(rs_quantile * 95) == 76 (RS_QUANTILE 0.80), long_bars <= 31; other
+ * parameters return BQ_EINVAL (the Python layer then runs its staged
+ * pipeline). workspace: bq_leadership_workspace_bytes(S, T) bytes, 256-byte
+ * aligned (the history entries and the strengths gate between the passes).
+ */
+size_t bq_leadership_workspace_bytes(int64_t S, int64_t T);
+int bq_leadership(const int64_t* open_time, int64_t ld_ts, const double* close, int64_t ld_c, int64_t S,
+                  int64_t T, const int64_t* bench_ts, const double* bench_close, int64_t nb,
+                  double rs_quantile, int32_t lookback, int32_t min_history, int32_t min_count,
+                  int32_t short_bars, int32_t long_bars, void* workspace, size_t workspace_bytes,
+                  uint8_t* leader, double* rs_2h, double* rs_6h, int64_t ld_out, void* stream);
+
 /* ---- benchmark-relative statistics ---------------------------------------- */
 /*
  * Rolling beta and correlation of log returns vs the benchmark

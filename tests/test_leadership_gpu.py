@@ -54,3 +54,50 @@ def test_leadership_panel_vs_oracle(cuda):
     assert want[0].sum() > 100
     np.testing.assert_array_equal(out["rs_2h"].cpu().numpy(), want[1])
     np.testing.assert_array_equal(out["rs_6h"].cpu().numpy(), want[2])
+
+
+@pytest.mark.parametrize("S,T", [(300, 1500), (7, 2500), (3, 97)])
+def test_leadership_fused_equals_staged(cuda, S, T):
+    """bq_leadership (two passes) against the staged pipeline (align, fused
+    stages, the order-statistic jobs, the integer rolling sum) bit for bit:
+    BTC gaps and a duplicated BTC time, zero / negative closes, a late
+    listing, symbols on their own time grids; T = 2500 at 7 symbols runs
+    several pass-2 segments per row (the warm-up of each)."""
+    from binquant_amd import signals
+
+    rng = np.random.default_rng(S * 7 + T)
+    t0 = 1_800_000_000_000
+    grid = t0 + 900_000 * np.arange(T + 40, dtype=np.int64)
+    off = rng.integers(0, 40, S)
+    times = np.stack([grid[o:o + T] for o in off])
+    close = 10.0 ** rng.uniform(-3, 3, (S, 1)) * np.exp(np.cumsum(rng.normal(0, 0.006, (S, T)), axis=1))
+    close[0, 500 % T:520 % T] = 0.0
+    close[1 % S, 700 % T] = -1.0
+    close[2 % S, : T // 3] = 0.0   # late listing
+    keep = rng.random(T + 40) > 0.03
+    bt = grid[keep]
+    bt = np.sort(np.concatenate([bt, bt[5:6]]))   # a duplicated time: the later row wins
+    bc = 30_000.0 * np.exp(np.cumsum(rng.normal(0, 0.004, bt.size)))
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    fused = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc))
+    signals._LEADERSHIP_FUSED = False
+    try:
+        staged = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc))
+    finally:
+        signals._LEADERSHIP_FUSED = True
+    for k in ("leader", "rs_2h", "rs_6h"):
+        np.testing.assert_array_equal(fused[k].cpu().numpy(), staged[k].cpu().numpy(), err_msg=k)
+    assert T < 200 or fused["leader"].sum().item() > 0
+
+
+def test_leadership_other_parameters_stage(cuda):
+    """parameters other than the compiled ones (lookback 48) run the staged
+    pipeline: engine.leadership declines them"""
+    from binquant_amd import engine, signals
+
+    z = np.load(G / "leadership.npz")
+    d = lambda k: torch.from_numpy(np.ascontiguousarray(z[f"pan__{k}"])).cuda()  # noqa: E731
+    assert engine.leadership(d("open_time"), d("close"), d("btc_time"), d("btc_close"), lookback=48) is None
+    out = signals.gradual_gainer_leadership(d("open_time"), d("close"), d("btc_time"), d("btc_close"),
+                                            rs_lookback=48)
+    assert out["leader"].dtype == torch.bool and out["rs_2h"].shape == d("close").shape
