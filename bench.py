@@ -34,7 +34,10 @@ Also reported (same JSON line):
                  fraction of HBM peak) with a bounded CPU timing of the
                  oracle's per-symbol path where the oracle restates the row;
   store        — §8f row 1: device MarketStateStore + live context at 10k
-                 symbols x 400-bar histories, per-tick latency p50/p99.
+                 symbols x 400-bar histories, per-tick latency p50/p99;
+  cohort       — one message cohort end to end (process_data for 1000
+                 symbols' 5m + 15m frames + the context refresh), eager and as
+                 one hipGraph, beside the reference's per-symbol cost x S.
 """
 
 from __future__ import annotations
@@ -429,7 +432,7 @@ def bench_rows(args, dev):
         "a20_zscore": (lambda: signals.zscore(c), 8, "strategies/range_bb_rsi_mean_reversion.py:124-138"),
         "a20_leadership": (lambda: signals.gradual_gainer_leadership(ts, c, ts[0], btc), 16,
                            "strategies/gradual_gainer_retest.py:131-196"),
-        "supertrend": (lambda: engine.supertrend(h, l, c), 24, "strategies/coinrule/coinrule.py:143"),
+        "supertrend": (lambda: engine.supertrend(h, l, c, exact=False), 24, "strategies/coinrule/coinrule.py:143"),
         "a9_resample_1h": (lambda: engine.resample(ts, {"open": o, "high": h, "low": l, "close": c, "volume": v},
                                                    agg, 3_600_000), 48, "producers/context_evaluator.py:403-407"),
         "f4_btc_join_returns": (lambda: engine.join_returns(ts, c, ts[0], btc), 16,
@@ -496,6 +499,42 @@ def bench_live(args, dev):
                      "reference_cpu_ms": None if ref_ms is None else ref_ms * S}
         del g
     return out
+
+
+# the reference's single-core pandas cost per symbol of one message (BASELINE.md
+# rows, measured through the real modules): indicators_enrichment on the 5m and
+# 15m frames (5.1 ms each), the store features (2.2), ActivityBurstPump (9.1),
+# LiquidationSweepPump (9.8), FailedSpikeFade (24.3)
+REF_COHORT_MS_PER_SYMBOL = 5.1 * 2 + 2.2 + 9.1 + 9.8 + 24.3
+
+
+def bench_cohort(args, dev):
+    """One message cohort end to end (binquant_amd.cohort.process_cohort:
+    ContextEvaluator.process_data for every symbol of a 15-minute cohort,
+    producers/context_evaluator.py:347-512, with the context refresh of
+    klines_provider.py:181-199): S symbols x 400-bar 5m and 15m frames, eager
+    and replayed as one captured hipGraph, next to the reference's per-symbol
+    pandas cost x S on one core."""
+    from binquant_amd.cohort import process_cohort
+    from binquant_amd.graphs import CapturedPipeline
+
+    S, T = args.live_symbols, 400
+    p5 = device_panel(S, T, device=dev, seed=41)
+    p15 = device_panel(S, T, device=dev, seed=43)
+    ts15 = (1_700_000_000_000 + 900_000 * torch.arange(T, device=dev, dtype=torch.int64)).expand(S, T).contiguous()
+    ins = [p5[k] for k in ("open", "high", "low", "close", "volume")] + \
+          [p15[k] for k in ("open", "high", "low", "close", "volume")] + [ts15, ts15[0].clone(), p15["close"][0].clone()]
+    eager = _time_call(lambda: process_cohort(*ins), reps=3)
+    g = CapturedPipeline(process_cohort, *ins)
+    graph = _time_call(lambda: g(*ins), reps=10)
+    del g
+    ref_ms = REF_COHORT_MS_PER_SYMBOL * S
+    return {"workload": f"{S} symbols x {T}-bar 5m + 15m frames (one message cohort): enrich x2, 1h resample, "
+                        "beta/corr + BTC change, context partials + last features, burst / pump / spike / top gainer "
+                        "/ leadership features (exact replays)",
+            "eager_ms": eager, "graph_ms": graph,
+            "reference_cpu_ms": ref_ms, "reference_cpu_basis": "BASELINE.md per-symbol pandas costs x symbols, 1 core",
+            "speedup_vs_reference_1core": ref_ms / graph}
 
 
 def bench_store(args, dev):
@@ -645,6 +684,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_rows:
         result["rows"] = bench_rows(args, dev)
         result["live"] = bench_live(args, dev)
+        result["cohort"] = bench_cohort(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args)
     else:

@@ -15,16 +15,20 @@
 //           affine maps, the pandas same-value run starts) are wave scans on
 //           DPP with tile carries held in registers — no workgroup barrier;
 //         * the history-capped EMA uses the exact window identity
-//             y_t = Y_t - a^(M-1) (Y_s - c_s),  s = t - M + 1,
-//           with Y_s from a second, lagged EMA chain over c[t - M + 1] (a
-//           re-read that hits L2 / MALL: the row was streamed M - 1 candles
-//           earlier) instead of an LDS ring of M values per symbol;
+//             y_t = Y_t - a^(M-1) (Y_s - c_s),  s = t - M + 1:
+//           long caps (a^(M-1) <= 1e-6: span 50 at M >= 346, the store's
+//           400) read D_s = Y_s - c_s from a per-wave fp32 ring in LDS (the
+//           last 3 tiles' D, written when s was processed; fp32 moves the
+//           term by <= 6e-14 |D|); short caps run a second, lagged EMA chain
+//           over c[t - M + 1] (a re-read of the row);
 //         * the 4 symbols' contributions at each t are summed in the
-//           workgroup in a fixed order, (s0 + s1) + (s2 + s3), through LDS,
-//           and written as one group record per t: 4 fp64 sums + the 5
-//           counts packed in 16 bits (34 B per 4 candles).
+//           workgroup in a fixed order, (s0 + s1) + (s2 + s3), through two
+//           LDS slots (the second pair's sum written back in place), and
+//           written as one group record per t: 4 fp64 sums + the 5 counts
+//           packed in 16 bits (34 B per 4 candles).
 // pass 2  context_group_reduce_kernel: lane = timestamp, the group records
-//         of a chunk of groups summed in a fixed order -> [chunk][T][9];
+//         of a chunk of groups summed in a fixed order -> [chunk][T][9]
+//         (8 groups' loads in flight per lane before their adds);
 // pass 3  context_chunk_reduce_kernel: the chunks in order -> [T][10].
 //
 // No atomics: the result is bitwise reproducible run to run.
@@ -46,12 +50,6 @@ static_assert(CX_HS % CX_K == 0 && CX_RS % CX_K == 0, "ring shape");
 // ring position i -> LDS slot, lane-interleaved (the lanes' k-th candles side
 // by side: conflict-free; qb = CX_HS + 4 lane is a multiple of 4)
 #define CXS(i) ((((i) & (CX_K - 1)) * CX_Q) + ((i) >> 2))
-// D ring: 3 tiles. A read at s = t - M + 1 (M <= BQ_MAX_HISTORY + 1 = 513) is
-// overwritten first by candle s + CX_DR > t0 + CX_TT - 1, i.e. after this tile.
-// fp32 is enough: the ring is used where a^(M-1) <= 1e-6 (span 50: M >= 346; 1.2e-7
-// at M = 400), so D's rounding (6e-8 |D|) moves the EMA by <= 6e-14 |D|.
-constexpr int CX_DR = 3 * CX_TT;
-static_assert(CX_DR >= BQ_MAX_HISTORY + CX_TT, "D ring too short for the history cap");
 constexpr int CX_ATR = 14;   // live_market_context_accumulator.py:268
 constexpr int CX_BB = 20;    // :269-270
 
@@ -104,17 +102,16 @@ __device__ __forceinline__ double cx_div(double a, double b) {
 }
 
 // DIV: pandas' EMA divide by (old_wt + new_wt) is needed (not exactly 1.0)
-#ifndef CX_PF
-#define CX_PF 1   // the next tile's inputs in flight (measurement switch)
-#endif
-// RING: span 50's history-cap term from the D ring (long caps); otherwise the
+// RING: span 50's history term from the D ring (long caps); otherwise the
 // lagged chains for every span whose a^(M-1) >= 1e-15 (short caps)
 template <bool DIV, bool RING>
 __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArgs A) {
   __shared__ double sTr[CX_NW][CX_RS], sC[CX_NW][CX_RS];   // true range / close rings per wave
-  __shared__ float sD[CX_NW][CX_DR];   // D_t = Y50_t - c_t of the last CX_DR candles (fp32: see CX_DR)
   __shared__ double sR[2][4][CX_TT];   // reduction slots: 4 sums, index k * 64 + lane
   __shared__ uint16_t sN[2][CX_TT];
+  // D ring: 3 tiles. A read at s = t - M + 1 (M <= BQ_MAX_HISTORY + 1 = 513) is
+  // overwritten first by candle s + 3 CX_TT > t0 + CX_TT - 1, i.e. after this tile.
+  __shared__ float sD[RING ? CX_NW : 1][RING ? 3 * CX_TT : 1];
 
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const int64_t grp = blockIdx.x;
@@ -127,7 +124,6 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
   const double* __restrict__ rC = A.c + row * A.ld_in;
   double* __restrict__ trr = sTr[w];
   double* __restrict__ cr = sC[w];
-  float* __restrict__ dr = sD[w];
   const bool vin = A.vin != 0;
   const int WB = M < CX_BB ? M : CX_BB;   // Bollinger window under the history cap
 
@@ -148,34 +144,12 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
   }
   wave_sync();
 
-  // the next tile's high / low / close in flight while this one is computed
-  double nh[CX_K], nl[CX_K], nc[CX_K];
-  if (CX_PF) {
-    cx_load(rH, CX_K * lane, T, vin, nh);
-    cx_load(rL, CX_K * lane, T, vin, nl);
-    cx_load(rC, CX_K * lane, T, vin, nc);
-  }
-  int dslot = 0;   // ring slot of this tile's first candle: t0 mod CX_DR
   for (int t0 = 0; t0 < T; t0 += CX_TT) {
     const int tb = t0 + CX_K * lane, qb = CX_HS + CX_K * lane;
     double h[CX_K], l[CX_K], c[CX_K], xl[CX_K];
-    if (CX_PF) {
-#pragma unroll
-      for (int k = 0; k < CX_K; ++k) {
-        h[k] = nh[k];
-        l[k] = nl[k];
-        c[k] = nc[k];
-      }
-      if (t0 + CX_TT < T) {
-        cx_load(rH, tb + CX_TT, T, vin, nh);
-        cx_load(rL, tb + CX_TT, T, vin, nl);
-        cx_load(rC, tb + CX_TT, T, vin, nc);
-      }
-    } else {
-      cx_load(rH, tb, T, vin, h);
-      cx_load(rL, tb, T, vin, l);
-      cx_load(rC, tb, T, vin, c);
-    }
+    cx_load(rH, tb, T, vin, h);
+    cx_load(rL, tb, T, vin, l);
+    cx_load(rC, tb, T, vin, c);
     if (!RING && (A.lag20 || A.lag50)) {
 #pragma unroll
       for (int k = 0; k < CX_K; ++k) {   // lagged closes c[t - M + 1] (0 before the row starts)
@@ -253,9 +227,10 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         }
         ecar[e] = readlane_f64(v, WAVE - 1);
       }
+      const bool lag = !RING && (e == 0 ? A.lag20 : A.lag50);
 #pragma unroll
       for (int k = 0; k < CX_K; ++k) D[e][k] = 0.0;
-      if (!RING && (e == 0 ? A.lag20 : A.lag50)) {   // short caps: the lagged chain
+      if (lag) {
         const int s0 = tb - (M - 1);
         double y = 0.0;
 #pragma unroll
@@ -274,19 +249,21 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         lcar[e] = readlane_f64(v, WAVE - 1);
       }
     }
-    // long caps, span 50: D_t = Y_t - c_t into the ring; D_s at s = t - M + 1 read back below
     if (RING) {
+      float* dr = sD[w];
+      const int dslot = ((t0 / CX_TT) % 3) * CX_TT;
 #pragma unroll
       for (int k = 0; k < CX_K; ++k) dr[dslot + CX_K * lane + k] = (float)(Y[1][k] - c[k]);
     }
-    wave_sync();   // the rings (close, true range, D) of every lane are visible
+    wave_sync();   // the rings (close, true range) of every lane are visible
     if (RING) {
-      int r = dslot + CX_K * lane - (M - 1);
-      r += r < 0 ? CX_DR : 0;
+      const float* dr = sD[w];
+      int r = ((t0 / CX_TT) % 3) * CX_TT + CX_K * lane - (M - 1);
+      r += r < 0 ? 3 * CX_TT : 0;
 #pragma unroll
       for (int k = 0; k < CX_K; ++k) {
-        const int q = r + k >= CX_DR ? r + k - CX_DR : r + k;
-        D[1][k] = (double)dr[q];   // used only where s = t - M + 1 >= 1
+        const int q = r + k >= 3 * CX_TT ? r + k - 3 * CX_TT : r + k;
+        D[1][k] = (double)dr[q];
       }
     }
 
@@ -296,62 +273,58 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
     // (the BB sums about a lane-local reference, no cancellation); windows
     // still short of their length (the row's first 19 candles) re-sum
     // directly; pandas' constant-window rule from the run starts.
-    // One pass over the lane's candles: the windows, the features and this
-    // symbol's contribution at each t (only the sums and counts stay live).
-    const bool full = tb >= CX_BB - 1 && WB == CX_BB;   // every candle of the lane has full windows
-    double Sx = 0.0, s1 = 0.0, s2 = 0.0;
-    double a0[CX_K - 1], d0[CX_K - 1];   // the values leaving the windows at k = 1 .. 3
-    const double rb = c[0];              // the BB sums' lane-local reference
-    if (full) {
+    double atr[CX_K], mid[CX_K], sd[CX_K];
+    if (tb >= CX_BB - 1 && WB == CX_BB) {   // every candle of the lane has full windows
+      {
+        double a[CX_ATR - 1];
 #pragma unroll
-      for (int i = 0; i < CX_ATR - 1; ++i) {
-        const double a = trr[CXS(qb - (CX_ATR - 1) + i)];
-        if (i < CX_K - 1) a0[i] = a;
-        Sx += a;
-      }
+        for (int i = 0; i < CX_ATR - 1; ++i) a[i] = trr[CXS(qb - (CX_ATR - 1) + i)];
+        double Sx = 0.0;
 #pragma unroll
-      for (int i = 0; i < CX_BB - 1; ++i) {
-        const double d = cr[CXS(qb - (CX_BB - 1) + i)] - rb;
-        if (i < CX_K - 1) d0[i] = d;
-        s1 += d;
-        s2 = fma(d, d, s2);
-      }
-    }
-    // 1 / |close| of the lane's candles: safe_pct's divisor at t + 1 is |close_t|
-    double rc[CX_K];
+        for (int i = 0; i < CX_ATR - 1; ++i) Sx += a[i];
 #pragma unroll
-    for (int k = 0; k < CX_K; ++k) rc[k] = rcp_nr(fabs(c[k]));
-    double rp0 = dpp_f64<DPP_WAVE_SHR1>(rc[CX_K - 1]);
-    if (lane == 0) rp0 = rcp_nr(fabs(p1));
-    double cs[4][CX_K];
-    unsigned cn[CX_K];
-#pragma unroll
-    for (int k = 0; k < CX_K; ++k) {
-      const int t = tb + k;
-      const int n = min(t + 1, M);
-      double atr, mid, sd;
-      if (full) {
-        Sx = k == 0 ? Sx + tr[0] : (Sx + tr[k]) - a0[k - 1];
-        atr = div_count(Sx < 0.0 ? 0.0 : Sx, (double)CX_ATR, 1.0 / CX_ATR);
-        const double dn = c[k] - rb;
-        if (k == 0) {
-          s1 += dn;
-          s2 = fma(dn, dn, s2);
-        } else {
-          const double dol = d0[k - 1];
-          s1 = (s1 + dn) - dol;
-          s2 = fma(-dol, dol, fma(dn, dn, s2));
+        for (int k = 0; k < CX_K; ++k) {
+          Sx = k == 0 ? Sx + tr[0] : (Sx + tr[k]) - a[k - 1];
+          atr[k] = div_count(Sx < 0.0 ? 0.0 : Sx, (double)CX_ATR, 1.0 / CX_ATR);
         }
-        const double m1 = s1 * (1.0 / CX_BB);
-        const double var = fma(-m1, s1, s2) * (1.0 / CX_BB);
-        mid = rb + m1;
-        sd = sqrt_nr(var > 0.0 ? var : 0.0);
-      } else {   // the row's first candles (or a cap below the BB window): direct sums
-        const int q = qb + k;
+      }
+      {
+        const double r = c[0];
+        double d0[CX_K - 1];
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < CX_BB - 1; ++i) {
+          const double d = cr[CXS(qb - (CX_BB - 1) + i)] - r;
+          if (i < CX_K - 1) d0[i] = d;
+          s1 += d;
+          s2 = fma(d, d, s2);
+        }
+#pragma unroll
+        for (int k = 0; k < CX_K; ++k) {
+          const double dn = c[k] - r;
+          if (k == 0) {
+            s1 += dn;
+            s2 = fma(dn, dn, s2);
+          } else {
+            const double dol = d0[k - 1];
+            s1 = (s1 + dn) - dol;
+            s2 = fma(-dol, dol, fma(dn, dn, s2));
+          }
+          const double m1 = s1 * (1.0 / CX_BB);
+          const double var = fma(-m1, s1, s2) * (1.0 / CX_BB);
+          mid[k] = r + m1;
+          sd[k] = sqrt_nr(var > 0.0 ? var : 0.0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        const int t = tb + k, q = qb + k;
+        const int n = min(t + 1, M);
         const int ma = min(CX_ATR, n), mb = min(WB, n);
-        double S = 0.0;
-        for (int i = q - ma + 1; i <= q; ++i) S += trr[CXS(i)];
-        atr = (S < 0.0 ? 0.0 : S) / (double)ma;
+        double Sx = 0.0;
+        for (int i = q - ma + 1; i <= q; ++i) Sx += trr[CXS(i)];
+        atr[k] = (Sx < 0.0 ? 0.0 : Sx) / (double)ma;
         double m = 0.0;
         for (int i = q - mb + 1; i <= q; ++i) m += cr[CXS(i)];
         m = m / (double)mb;
@@ -360,49 +333,66 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
           const double d = cr[CXS(i)] - m;
           acc = fma(d, d, acc);
         }
-        mid = m;
-        sd = sqrt(acc / (double)mb);
+        mid[k] = m;
+        sd[k] = sqrt(acc / (double)mb);
       }
-      // _compute_symbol_features (:244-297); history.empty or len < 2 -> None (:248-249)
+    }
+    double fr[CX_K], fe20[CX_K], fe50[CX_K], ftr[CX_K], fap[CX_K], fbw[CX_K];
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) {
+      const int t = tb + k;
+      const int n = min(t + 1, M);
+      if (n < 2) {   // history.empty or len < 2 -> None (:248-249)
+        fr[k] = fe20[k] = fe50[k] = ftr[k] = fap[k] = fbw[k] = qnan();
+        continue;
+      }
       const double cl = c[k];
       const double prev = k > 0 ? c[k - 1] : p1;
-      const double rprev = k > 0 ? rc[k - 1] : rp0;
       double e20 = Y[0][k], e50 = Y[1][k];
       if (t + 1 > M) {   // the history window starts at s = t - M + 1 > 0
         e20 = e20 - A.corr[0] * D[0][k];
         e50 = e50 - A.corr[1] * D[1][k];
       }
-      const double a = lct[k] <= t - min(CX_ATR, n) + 1 ? tr[k] : atr;
-      double m = mid, s = sd;
+      const double a = lct[k] <= t - min(CX_ATR, n) + 1 ? tr[k] : atr[k];
+      double m = mid[k], s = sd[k];
       if (lcc[k] <= t - min(WB, n) + 1) {
         m = cl;
         s = 0.0;
       }
       const double up = m + (2.0 * s), lo = m - (2.0 * s);
-      const bool has = n >= 2;
-      // safe_pct (shared/utils.py:20-23), as a / b = sign(b) a / |b| through the reciprocal
-      const double q0 = (cl - prev) * rprev;
-      const double fr = !has ? qnan() : (prev == 0.0 ? 0.0 : (prev < 0.0 ? -q0 : q0));
-      const double ftr = e50 != 0.0 ? cx_div(e20 - e50, e50 < 0.0 ? -e50 : e50) : 0.0;
-      const double q1 = a * rc[k];
-      const double fap = cl != 0.0 ? (cl < 0.0 ? -q1 : q1) : 0.0;
-      const double fbw = m != 0.0 ? cx_div(up - lo, m < 0.0 ? -m : m) : 0.0;
-      // the last timestamp's feature row, when asked (the context's symbol_features)
-      if (live && t == T - 1) {
-        const double v[BQ_NUM_FEATURES] = {fr, has ? e20 : qnan(), has ? e50 : qnan(), has ? ftr : qnan(),
-                                           has ? fap : qnan(), has ? fbw : qnan()};
+      fr[k] = prev == 0.0 ? 0.0 : cx_div(cl - prev, prev);   // safe_pct (shared/utils.py:20-23)
+      fe20[k] = e20;
+      fe50[k] = e50;
+      ftr[k] = e50 != 0.0 ? cx_div(e20 - e50, e50 < 0.0 ? -e50 : e50) : 0.0;
+      fap[k] = cl != 0.0 ? cx_div(a, cl) : 0.0;
+      fbw[k] = m != 0.0 ? cx_div(up - lo, m < 0.0 ? -m : m) : 0.0;
+    }
+    // the last timestamp's feature row, when asked (the context's symbol_features)
+    if (live && tb <= T - 1 && T - 1 < tb + CX_K) {
+#pragma unroll
+      for (int k = 0; k < CX_K; ++k) {
+        if (tb + k != T - 1) continue;
+        const double v[BQ_NUM_FEATURES] = {fr[k], fe20[k], fe50[k], ftr[k], fap[k], fbw[k]};
 #pragma unroll
         for (int f = 0; f < BQ_NUM_FEATURES; ++f)
           if (A.last[f]) A.last[f][sym] = v[f];
       }
-      const bool ok = live && t < T && fr == fr;   // no features at t: nothing counted
-      cn[k] = ok ? ((1u << CNT_VALID) | ((fr > 0.0 ? 1u : 0u) << CNT_ADV) | ((fr < 0.0 ? 1u : 0u) << CNT_DEC) |
-                    ((cl > e20 ? 1u : 0u) << CNT_A20) | ((cl > e50 ? 1u : 0u) << CNT_A50))
+    }
+
+    // ---- this symbol's contributions, then the group's (fixed order) --------
+    double cs[4][CX_K];
+    unsigned cn[CX_K];
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) {
+      const double r = fr[k];
+      const bool ok = live && tb + k < T && r == r;   // no features at t: nothing counted
+      cn[k] = ok ? ((1u << CNT_VALID) | ((r > 0.0 ? 1u : 0u) << CNT_ADV) | ((r < 0.0 ? 1u : 0u) << CNT_DEC) |
+                    ((c[k] > fe20[k] ? 1u : 0u) << CNT_A20) | ((c[k] > fe50[k] ? 1u : 0u) << CNT_A50))
                  : 0u;
-      cs[0][k] = ok ? fr : 0.0;
-      cs[1][k] = ok ? ftr : 0.0;
-      cs[2][k] = ok ? fap : 0.0;
-      cs[3][k] = ok ? fbw : 0.0;
+      cs[0][k] = ok ? r : 0.0;
+      cs[1][k] = ok ? ftr[k] : 0.0;
+      cs[2][k] = ok ? fap[k] : 0.0;
+      cs[3][k] = ok ? fbw[k] : 0.0;
     }
     if (w & 1) {   // waves 1, 3 -> slots 0, 1
       const int sl = w >> 1;
@@ -414,7 +404,7 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
       }
     }
     __syncthreads();
-    if (!(w & 1)) {   // wave 0: s0 + s1; wave 2: s2 + s3, back into slot 1 (each lane its own elements)
+    if (!(w & 1)) {   // wave 0: s0 + s1, wave 2: s2 + s3
       const int sl = w >> 1;
 #pragma unroll
       for (int k = 0; k < CX_K; ++k) {
@@ -468,7 +458,6 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
     lc = readlane_f64(l[CX_K - 1], WAVE - 1);
     rcC = __builtin_amdgcn_readlane(lcc[CX_K - 1], WAVE - 1);
     rtC = __builtin_amdgcn_readlane(lct[CX_K - 1], WAVE - 1);
-    dslot = dslot + CX_TT == CX_DR ? 0 : dslot + CX_TT;
   }
 }
 
@@ -659,22 +648,23 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
   A.lag50 = A.corr[1] >= 1e-15;
   if (!A.lag20) A.corr[0] = 0.0;
   if (!A.lag50) A.corr[1] = 0.0;
-  // the D ring (fp32) where span 50's term is small: a^(M-1) <= 1e-6 (M >= 346 at
-  // span 50), so D's fp32 rounding moves the EMA by <= 6e-14 |D|; span 20's term is
-  // then below 1e-15 and skipped
-  const bool ring = A.corr[1] <= 1e-6 && !A.lag20;
   char* ws = (char*)workspace;
   for (int f = 0; f < 4; ++f) A.gsum[f] = (double*)(ws + L.off_sum[f]);
   A.gcnt = (uint16_t*)(ws + L.off_cnt);
   A.ld_g = L.ld_g;
   for (int f = 0; f < BQ_NUM_FEATURES; ++f) A.last[f] = last_feat ? last_feat[f] : nullptr;
   hipStream_t st = (hipStream_t)stream;
-  const bool div = A.den[0] != 1.0 || A.den[1] != 1.0;
-  const dim3 grid((unsigned)L.ngrp), block(CX_NT);
-  if (div && ring) hipLaunchKernelGGL((context_partials_kernel<true, true>), grid, block, 0, st, A);
-  else if (div) hipLaunchKernelGGL((context_partials_kernel<true, false>), grid, block, 0, st, A);
-  else if (ring) hipLaunchKernelGGL((context_partials_kernel<false, true>), grid, block, 0, st, A);
-  else hipLaunchKernelGGL((context_partials_kernel<false, false>), grid, block, 0, st, A);
+  // the D ring (fp32) where span 50's term is small: a^(M-1) <= 1e-6 (M >= 346 at
+  // span 50), so D's fp32 rounding moves the EMA by <= 6e-14 |D|; span 20's term is
+  // then below 1e-15 and skipped
+  const bool ring = A.corr[1] <= 1e-6 && !A.lag20;
+  if (A.den[0] != 1.0 || A.den[1] != 1.0) {
+    if (ring) hipLaunchKernelGGL((context_partials_kernel<true, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    else hipLaunchKernelGGL((context_partials_kernel<true, false>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+  } else {
+    if (ring) hipLaunchKernelGGL((context_partials_kernel<false, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    else hipLaunchKernelGGL((context_partials_kernel<false, false>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+  }
   GroupReduceArgs G;
   for (int f = 0; f < 4; ++f) G.gsum[f] = A.gsum[f];
   G.gcnt = A.gcnt;

@@ -49,7 +49,6 @@
 //       for short windows on large panels.
 #include "bq_device.h"
 #include "bq_panel.h"
-#include "bq_slide.h"
 #include "binquant_amd.h"
 
 #include <stdlib.h>
@@ -673,32 +672,40 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
 // reads two fixed registers.
 // Parallelism: lanes = (symbol, segment); a segment first inserts the W - 1
 // values before it (the warm-up, insert-only passes).
-// Measured at 12.5k x 2k (tools/slide_probe.py, identical outputs): median(19)
-// 0.28 (stencil) -> 0.22 ms, quantile(0.80, 48) 0.61 (tile) -> 0.38 ms; at
-// w = 60 / 80 / 96 the W-register window leaves 1-2 waves per SIMD and the
-// kernel ties or loses (0.53 / 0.73 / 1.15 ms against the tile kernel's
-// 0.62 / 0.74 / 0.83), so those stay on the tile kernel. The VALU count
-// matches the 5-per-slot model (PMC: 129.5 M wave instructions for w = 48);
-// the VALU is busy ~56 % of the time at 2 waves per SIMD.
+// Measured at 12.5k x 2k (tools/slide_probe.py, identical outputs, round 4
+// box): median(19) 0.20 ms, quantile(0.80, 48) 0.35, quantile(0.85, 60) 0.40,
+// quantile(0.92, 80) 0.64, lower quantile(0.80, 96) 0.74 — every strategy
+// window runs here (the tile / stencil kernels took 0.28 / 0.61 / 0.60 / 0.73
+// / 0.82). The VALU count matches the 5-per-slot model (PMC: 129.5 M wave
+// instructions for w = 48). Occupancy is not what binds it: at w = 80 / 96
+// the window takes 305 / 412 registers (one wave per SIMD), and round-4
+// variants at two waves per SIMD (split placeholders from the start instead
+// of the barrel shift below: 291 registers; stepwise loops: 216; 2- or 4-step
+// chunks: 224-274) ran 0-40 % slower — each slot is a dependent compare ->
+// select -> min -> max chain of fp64 operations.
 //
+// v_min_f64 / v_max_f64 without the compiler's IEEE-mode canonicalisation of
+// operands it cannot prove canonical (a third max per slot on the loop-carried
+// registers); no NaN ever reaches them here (placeholders are +inf)
+__device__ __forceinline__ double min_f64_nn(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double max_f64_nn(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // 8-byte-aligned pairs of doubles: one 16-byte access (rows are 8-byte aligned)
 typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
 
-#ifndef BQ_SLIDE_STEP_MIN
-#define BQ_SLIDE_STEP_MIN 60   // windows from this length on run the stepwise loop
-#endif
 template <int W, int K, bool MED>
 __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
   // steps per chunk: each lane reads / writes 8 * SL_C contiguous bytes
   // (16 for short windows: 0.27 -> 0.22 ms at w = 19; 8 where registers bind)
-  // w >= 60: one step per loop iteration, the values read straight from the
-  // row (consecutive steps of a lane hit the same lines). Unrolled over a
-  // chunk, the compiler keeps a second copy of the W-slot window in flight
-  // (412 registers at w = 96: one wave per SIMD, AGPR spills); stepwise the
-  // window and its update fit 2 waves per SIMD (212 at w = 96, 180 at w = 80).
-  constexpr bool STEP = W >= BQ_SLIDE_STEP_MIN;
-  // (stepwise: 4 — the prefetched chunk's registers beside the window: 252 at w = 96)
-  constexpr int SL_C = STEP ? 4 : (W <= 24 ? 16 : 8);
+  constexpr int SL_C = W <= 24 ? 16 : 8;
   const RollJob& A = B.j[blockIdx.y];
   const int64_t item = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t sym = item % B.S;
@@ -728,21 +735,6 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
     }
   };
-  auto store_chunk = [&](int tc, const double (&r)[SL_C]) {   // outputs of steps tc .. tc + SL_C - 1
-    if (tc >= t_begin && tc + SL_C <= t_end) {
-#pragma unroll
-      for (int j = 0; j < SL_C; j += 2) {
-        dbl2u p;
-        p.x = r[j];
-        p.y = r[j + 1];
-        *reinterpret_cast<dbl2u*>(out + tc + j) = p;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < SL_C; ++j)
-        if (tc + j >= t_begin && tc + j < t_end) out[tc + j] = r[j];
-    }
-  };
   // Placeholders split so the wanted rank sits in a FIXED slot: with n
   // numbers in the window, a(n) = int(q (n - 1)) (median: (n - 1) / 2) and
   // B(n) = K - a(n) placeholders at the bottom (-inf), the rest at the top
@@ -766,57 +758,7 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
 #pragma unroll
   for (int i = 0; i < W; ++i) s[i] = inf;
   int n = 0;
-  if constexpr (STEP) {
-    // (bq_slide.h) the split placeholders from the start and the warm-up as
-    // full steps whose leaving value is a placeholder, instead of
-    // insert-only passes and the barrel shift below (3 more VALU per slot
-    // over W - 1 steps; the shift, unrolled over W slots and log W levels,
-    // held a second copy of the window). One step per loop iteration (an
-    // unrolled chunk of steps lets the scheduler overlap consecutive steps'
-    // slot updates, which again holds two copies: 348 registers at w = 96);
-    // the values of a chunk go through a lane-private LDS slice, the next
-    // chunk's loads in flight while this one is stepped.
-    __shared__ double sv[2][SL_C][256];
-    const int tid = threadIdx.x;
-    SlideRank<W, K, MED> R;
-    R.init(A.q);
-    double nin[SL_C], nout[SL_C];
-    auto fetch = [&](int tc) {
-      load_chunk(tc, nin);
-      load_chunk(tc - W, nout);
-    };
-    auto stage = [&]() {
-#pragma unroll
-      for (int j = 0; j < SL_C; ++j) {
-        sv[0][j][tid] = nin[j];
-        sv[1][j][tid] = nout[j];
-      }
-    };
-    // warm-up: steps t_start .. t_begin - 1 enter, placeholders leave
-    int tc = t_start;
-    if (tc < t_begin) fetch(tc);
-    for (; tc < t_begin; tc += SL_C) {
-      stage();
-      if (tc + SL_C < t_begin) fetch(tc + SL_C);
-      else fetch(t_begin);
-      const int nj = min(SL_C, t_begin - tc);
-#pragma unroll 1
-      for (int j = 0; j < nj; ++j) R.step(sv[0][j][tid], qnan());
-    }
-    if (t_start >= t_begin) fetch(t_begin);
-    for (tc = t_begin; tc < t_end; tc += SL_C) {
-      stage();
-      if (tc + SL_C < t_end) fetch(tc + SL_C);
-      const int nj = min(SL_C, t_end - tc);
-#pragma unroll 1
-      for (int j = 0; j < nj; ++j) {
-        const int t = tc + j;
-        R.step(sv[0][j][tid], t - W >= t_start ? sv[1][j][tid] : qnan());   // else a placeholder leaves
-        out[t] = R.value(A.minp, A.lower != 0);
-      }
-    }
-    return;
-  } else {
+  {
     constexpr int NCH = (W + SL_C - 1) / SL_C;
     const int t0 = t_begin - NCH * SL_C;   // step of chunk slot 0
     for (int c = 0; c < NCH; ++c) {
@@ -884,7 +826,19 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
         }
       }
     }
-    store_chunk(tc, r);
+    if (tc >= t_begin && tc + SL_C <= t_end) {
+#pragma unroll
+      for (int j = 0; j < SL_C; j += 2) {
+        dbl2u p;
+        p.x = r[j];
+        p.y = r[j + 1];
+        *reinterpret_cast<dbl2u*>(out + tc + j) = p;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j)
+        if (tc + j >= t_begin && tc + j < t_end) out[tc + j] = r[j];
+    }
   }
 }
 

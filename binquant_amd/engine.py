@@ -903,16 +903,17 @@ def supertrend(
     multiplier: float = 3.0,
     atr: torch.Tensor | None = None,
     stream: torch.cuda.Stream | None = None,
-    exact: bool = False,
+    exact: bool = True,
 ) -> dict[str, torch.Tensor]:
     """pybinbot Indicators.set_supertrend (strategies/coinrule/coinrule.py:143-160)
     on a [S, T] panel: {"supertrend": bool (uptrend), "supertrend_upper",
     "supertrend_lower": final bands}. ATR = TR.rolling(period).mean() unless
-    given: exact=True forms it in the same walk as pandas' roll_mean
-    (bq_supertrend_hlc, bit for bit — the live path, Indicators.set_supertrend);
-    the default panel mode (bq_supertrend_panel) walks chunks of each row in
-    parallel with verified chunk starts (the same recursion) on an ATR equal
-    to pandas' to rounding."""
+    given: the default exact=True forms it in the same walk as pandas'
+    roll_mean (bq_supertrend_hlc, bit for bit — the live path,
+    Indicators.set_supertrend); exact=False is the panel mode
+    (bq_supertrend_panel: chunks of each row walked in parallel with verified
+    chunk starts, the same recursion) on an ATR equal to pandas' to rounding,
+    so bands agree to rounding and flags up to near-ties."""
     high = _check_panel(high, "high")
     S, T = high.shape
     low = _check_panel(low, "low", (S, T))
@@ -977,12 +978,16 @@ def resample(
     aggs: dict[str, str],
     interval_ms: int,
     lens=None,
+    max_bins: int | None = None,
     stream: torch.cuda.Stream | None = None,
 ) -> tuple[torch.Tensor, dict[str, torch.Tensor], torch.Tensor]:
     """Candles.resample (producers/context_evaluator.py:403-407) on a ragged
     [S, T] panel: pandas resample(interval, origin="start_day").agg(aggs) on
     the open_time index. Returns (bin labels int64 [S, B], {field: [S, B]},
-    bins per row int64 [S]); B = the longest row's bin count."""
+    bins per row int64 [S]); B = the longest row's bin count, read back from
+    the device — or, with max_bins (fixed frame geometry, e.g. a captured
+    graph: no host synchronisation), B = max_bins, which must be at least
+    every row's bin count (bins past a row's count are left unwritten)."""
     ts = _check_ts(ts)
     S, T = ts.shape
     names = list(fields)
@@ -1000,7 +1005,12 @@ def resample(
     out_lens = torch.empty(S, dtype=torch.int64, device=ts.device)
     _lib.check(L.bq_resample_count(_ptr(ts), _ptr(lens), S, T, T, int(interval_ms), _ptr(out_lens),
                                    _stream_handle(stream)), "bq_resample_count")
-    B = int(out_lens.max().item()) if S else 0
+    if max_bins is not None:
+        if max_bins < 0:
+            raise ValueError("max_bins must be >= 0")
+        B = int(max_bins)
+    else:
+        B = int(out_lens.max().item()) if S else 0
     out_ts = torch.empty((S, B), dtype=torch.int64, device=ts.device)
     outs = [torch.empty((S, B), dtype=torch.float64, device=ts.device) for _ in names]
     agg_arr = (ctypes.c_int32 * max(1, len(codes)))(*codes)
@@ -1032,7 +1042,7 @@ def align(ts: torch.Tensor, bench_ts: torch.Tensor, bench_val: torch.Tensor, len
     return out
 
 
-LEADERSHIP_FUSED = dict(lookback=96, rank=76, long_max=31)   # bq_leadership's compiled configuration
+LEADERSHIP_FUSED = dict(lookback=96, long_max=31)   # bq_leadership's compiled configuration
 
 
 @device_entry
@@ -1040,13 +1050,13 @@ def leadership(open_time: torch.Tensor, close: torch.Tensor, bench_ts: torch.Ten
                rs_quantile: float = 0.80, lookback: int = 96, min_history: int = 100, min_count: int = 20,
                short: int = 8, long: int = 24, stream: torch.cuda.Stream | None = None):
     """GradualGainerRetest._leadership_allows at every prefix t
-    (strategies/gradual_gainer_retest.py:131-196) in two passes (bq_leadership):
-    returns {"leader": bool [S, T], "rs_2h": [S, T], "rs_6h": [S, T]}, or None
-    when the parameters are not the compiled ones (RS_LOOKBACK 96, int(q * 95)
-    == 76, long <= 31): the caller then runs the staged pipeline."""
-    if lookback != LEADERSHIP_FUSED["lookback"] or int(rs_quantile * (lookback - 1)) != LEADERSHIP_FUSED["rank"] \
-            or not 0.0 <= rs_quantile < 1.0 or not 1 <= short <= long <= LEADERSHIP_FUSED["long_max"] \
-            or min_count < 1 or min_history < 0:
+    (strategies/gradual_gainer_retest.py:131-196) in one pass (bq_leadership:
+    the thresholds are never formed — "rs >= sorted(h)[a]" is a count of the
+    window's entries <= rs): returns {"leader": bool [S, T], "rs_2h": [S, T],
+    "rs_6h": [S, T]}, or None when the parameters are not the compiled ones
+    (RS_LOOKBACK 96, long <= 31): the caller then runs the staged pipeline."""
+    if lookback != LEADERSHIP_FUSED["lookback"] or not 0.0 <= rs_quantile < 1.0 \
+            or not 1 <= short <= long <= LEADERSHIP_FUSED["long_max"] or min_count < 1 or min_history < 0:
         return None
     close = _check_panel(close, "close").contiguous()
     S, T = close.shape

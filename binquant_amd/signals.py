@@ -215,7 +215,7 @@ def gradual_gainer_leadership(open_time: torch.Tensor, close: torch.Tensor, btc_
     frame is shorter than min_history, (False, rs_2h, rs_6h) when fewer than
     min_count history entries exist.
 
-    The strategy's own parameters run in two passes (engine.leadership,
+    The strategy's lookback runs in one pass (engine.leadership,
     bq_leadership); any others run the staged pipeline below. A NaN close is
     not > 0 here, so it never enters the history or the strengths; the
     reference's Python min(...) skips a NaN unless it is its first argument
@@ -224,7 +224,7 @@ def gradual_gainer_leadership(open_time: torch.Tensor, close: torch.Tensor, btc_
     frames hold none; pre_process drops such rows before the strategies)."""
     fused = engine.leadership(open_time, close, btc_time, btc_close, rs_quantile, rs_lookback, min_history,
                               min_count, short, long) if _LEADERSHIP_FUSED else None
-    if fused is not None:   # the strategy's own parameters: two passes (bq_leadership)
+    if fused is not None:   # the strategy's lookback: one pass (bq_leadership)
         return fused
     # any other parameters: the staged pipeline
     S, T = close.shape

@@ -232,11 +232,12 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
  * (ascending; a duplicated time keeps the later row) / bench_close [nb].
  * Outputs [S][ld_out]: leader (0 / 1 bytes) and rs_2h / rs_6h as the method
  * returns them ((False, 0.0, 0.0) when the strengths are None or the frame
- * is shorter than min_history). Compiled for the strategy's RS_LOOKBACK 96
- * and int(rs_quantile * 95) == 76 (RS_QUANTILE 0.80), long_bars <= 31; other
- * parameters return BQ_EINVAL (the Python layer then runs its staged
- * pipeline). workspace: bq_leadership_workspace_bytes(S, T) bytes, 256-byte
- * aligned (the history entries and the strengths gate between the passes).
+ * is shorter than min_history). One pass: "rs >= sorted(history)[int((n - 1)
+ * q)]" is decided by counting the window's entries <= rs (the thresholds are
+ * not outputs of the method). Compiled for the strategy's RS_LOOKBACK 96 and
+ * long_bars <= 31; other parameters return BQ_EINVAL (the Python layer then
+ * runs its staged pipeline). bq_leadership_workspace_bytes returns 0 (the
+ * workspace arguments are kept for callers that size one; NULL is fine).
  */
 size_t bq_leadership_workspace_bytes(int64_t S, int64_t T);
 int bq_leadership(const int64_t* open_time, int64_t ld_ts, const double* close, int64_t ld_c, int64_t S,

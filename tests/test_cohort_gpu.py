@@ -1,0 +1,70 @@
+"""One message cohort on the device (binquant_amd.cohort.process_cohort:
+ContextEvaluator.process_data, producers/context_evaluator.py:347-512, for a
+whole 15-minute cohort): the cohort's outputs equal the stage calls made one
+by one, the 1h resample with a fixed bin count equals the read-back one, and
+the whole cohort captured as one hipGraph replays bit for bit on new inputs
+(no host synchronisation inside, no stale buffers)."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(S, T, seed):
+    from binquant_amd.synth import numpy_panel
+
+    p5 = numpy_panel(S, T, seed0=seed, edges=True)
+    p15 = numpy_panel(S, T, seed0=seed + 1000, edges=True)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    ts = 1_700_000_000_000 + 900_000 * np.arange(T, dtype=np.int64)
+    ins = [d(p5[k]) for k in ("open", "high", "low", "close", "volume")]
+    ins += [d(p15[k]) for k in ("open", "high", "low", "close", "volume")]
+    ins += [d(np.broadcast_to(ts, (S, T))), d(ts), d(p15["close"][0])]
+    return ins
+
+
+def test_cohort_equals_stage_calls(cuda):
+    from binquant_amd import engine, signals, strategies
+    from binquant_amd.cohort import RESAMPLE_AGG, process_cohort
+
+    S, T = 48, 400
+    ins = _inputs(S, T, 5)
+    o5, h5, l5, c5, v5, o15, h15, l15, c15, v15, ts15, bts, bc = ins
+    out = process_cohort(*ins)
+    for k, v in engine.enrich(o15, h15, l15, c15, v15).items():
+        np.testing.assert_array_equal(out[f"e15.{k}"].cpu().numpy(), v.cpu().numpy(), err_msg=k)
+    _, res, nb = engine.resample(ts15, {"open": o15, "high": h15, "low": l15, "close": c15, "volume": v15},
+                                 RESAMPLE_AGG, 3_600_000)
+    assert torch.equal(out["h1.bins"], nb)
+    B = int(nb.max())
+    for k, v in res.items():
+        np.testing.assert_array_equal(out[f"h1.{k}"][:, :B].cpu().numpy(), v.cpu().numpy(), err_msg=k)
+    lead = signals.gradual_gainer_leadership(ts15, c15, bts, bc)
+    for k, v in lead.items():
+        assert torch.equal(out[f"lead.{k}"], v), k
+    spike = strategies.failed_spike_features(o15, h15, l15, c15, v15, v15 * c15, exact=True)
+    for k, v in spike.items():
+        np.testing.assert_array_equal(out[f"spike.{k}"].cpu().numpy(), v.cpu().numpy(), err_msg=k)
+    part, last = engine.context_partials(h15, l15, c15, max_bars=400, last=True)
+    assert torch.equal(out["context.partial"], part)
+
+
+def test_cohort_graph_replays_bit_exact(cuda):
+    from binquant_amd.cohort import process_cohort
+    from binquant_amd.graphs import CapturedPipeline
+
+    S, T = 64, 400
+    a, b = _inputs(S, T, 11), _inputs(S, T, 12)
+    g = CapturedPipeline(process_cohort, *a)
+    got = g(*b)
+    want = process_cohort(*b)
+    torch.cuda.synchronize()
+    assert set(got) == set(want)
+    for k in want:
+        x, y = got[k].cpu().numpy(), want[k].cpu().numpy()
+        if k.startswith("h1."):   # bins past a row's count are unwritten
+            n = int(want["h1.bins"].max())
+            x, y = x[..., :n] if x.ndim == 2 else x, y[..., :n] if y.ndim == 2 else y
+        np.testing.assert_array_equal(x, y, err_msg=k)

@@ -58,11 +58,11 @@ def test_leadership_panel_vs_oracle(cuda):
 
 @pytest.mark.parametrize("S,T", [(300, 1500), (7, 2500), (3, 97)])
 def test_leadership_fused_equals_staged(cuda, S, T):
-    """bq_leadership (two passes) against the staged pipeline (align, fused
+    """bq_leadership (one counting pass) against the staged pipeline (align, fused
     stages, the order-statistic jobs, the integer rolling sum) bit for bit:
     BTC gaps and a duplicated BTC time, zero / negative closes, a late
     listing, symbols on their own time grids; T = 2500 at 7 symbols runs
-    several pass-2 segments per row (the warm-up of each)."""
+    several 256-candle tiles per row (each with its 95-entry history halo)."""
     from binquant_amd import signals
 
     rng = np.random.default_rng(S * 7 + T)
@@ -79,15 +79,16 @@ def test_leadership_fused_equals_staged(cuda, S, T):
     bt = np.sort(np.concatenate([bt, bt[5:6]]))   # a duplicated time: the later row wins
     bc = 30_000.0 * np.exp(np.cumsum(rng.normal(0, 0.004, bt.size)))
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
-    fused = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc))
-    signals._LEADERSHIP_FUSED = False
-    try:
-        staged = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc))
-    finally:
-        signals._LEADERSHIP_FUSED = True
-    for k in ("leader", "rs_2h", "rs_6h"):
-        np.testing.assert_array_equal(fused[k].cpu().numpy(), staged[k].cpu().numpy(), err_msg=k)
-    assert T < 200 or fused["leader"].sum().item() > 0
+    for q in (0.80, 0.55):   # the strategy's RS_QUANTILE and another (the count test holds for any q)
+        fused = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc), rs_quantile=q)
+        signals._LEADERSHIP_FUSED = False
+        try:
+            staged = signals.gradual_gainer_leadership(tt(times), tt(close), tt(bt), tt(bc), rs_quantile=q)
+        finally:
+            signals._LEADERSHIP_FUSED = True
+        for k in ("leader", "rs_2h", "rs_6h"):
+            np.testing.assert_array_equal(fused[k].cpu().numpy(), staged[k].cpu().numpy(), err_msg=f"{k} q={q}")
+        assert T < 200 or fused["leader"].sum().item() > 0
 
 
 def test_leadership_other_parameters_stage(cuda):
