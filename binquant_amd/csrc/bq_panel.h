@@ -14,6 +14,8 @@ struct PanelJob {
   int64_t ld_in, ld_out, rows;
   int win, minp, shift, mode;   // mode: BQ_ROLL_SUM / BQ_ROLL_MEAN / BQ_ROLL_EWM
   double alpha;
+  const double *hi, *lo;        // ewm only: non-null = the series is the true range of
+                                // (hi, lo, x = close), [S][ld_in] like x
 };
 
 constexpr int PN_MAXJOBS = 16;

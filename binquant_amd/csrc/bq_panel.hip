@@ -36,6 +36,8 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <string.h>
+
 namespace bq {
 
 constexpr int PN_NT = 256;
@@ -198,6 +200,11 @@ __global__ __launch_bounds__(PN_NT) void panel_window_kernel(const PanelBatch B)
 }
 
 // ---- ewm ------------------------------------------------------------------------------
+// TR: the series is the true range max(h - l, |h - c[t-1]|, |l - c[t-1]|) of
+// the job's (hi, lo, x = close), formed from the loads (NaN operands skipped,
+// as DataFrame.max(axis=1): the first candle's is h - l) — the ATR of
+// liquidation_sweep_pump.py:206-217 without a true-range column in HBM
+template <bool TR>
 __global__ __launch_bounds__(PN_NT) void panel_ewm_kernel(const PanelBatch B) {
   __shared__ double sA[PN_NW], sB[PN_NW];
   __shared__ double sCarry;
@@ -217,14 +224,33 @@ __global__ __launch_bounds__(PN_NT) void panel_ewm_kernel(const PanelBatch B) {
   bool serial = false;
   double wv = qnan(), owt = 1.0;   // pandas' state (thread 0) once the row turns serial
   int nobs = 0;
-  double nx[PN_K];
-  pn_load(x, PN_K * tid, T, vin, nx);
+  double nx[PN_K], nh[TR ? PN_K : 1], nl[TR ? PN_K : 1];
+  const double* __restrict__ xh = TR ? A.hi + row * A.ld_in : nullptr;
+  const double* __restrict__ xl = TR ? A.lo + row * A.ld_in : nullptr;
+  const bool vhl = TR && pn_aligned(A.hi, A.ld_in) && pn_aligned(A.lo, A.ld_in);
+  auto load_tile = [&](int tb) {
+    pn_load(x, tb, T, vin, nx);
+    if constexpr (TR) {
+      pn_load(xh, tb, T, vhl, nh);
+      pn_load(xl, tb, T, vhl, nl);
+    }
+  };
+  load_tile(PN_K * tid);
   for (int t0 = 0; t0 < T; t0 += PN_TT) {
     const int tb = t0 + PN_K * tid;
     double c[PN_K];
+    if constexpr (TR) {
+      double pc = tb >= 1 && tb <= T ? x[tb - 1] : qnan();
 #pragma unroll
-    for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
-    if (t0 + PN_TT < T) pn_load(x, tb + PN_TT, T, vin, nx);
+      for (int k = 0; k < PN_K; ++k) {
+        c[k] = tb + k < T ? true_range(nh[k], nl[k], pc) : qnan();
+        pc = nx[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
+    }
+    if (t0 + PN_TT < T) load_tile(tb + PN_TT);
     {
       int bad = 0;
 #pragma unroll
@@ -339,13 +365,54 @@ void launch_panel(const PanelBatch& B, int n, hipStream_t st) {
   PanelBatch win, ewm;
   win.S = ewm.S = B.S;
   win.T = ewm.T = B.T;
-  int nw = 0, ne = 0;
+  PanelBatch etr;
+  etr.S = B.S;
+  etr.T = B.T;
+  int nw = 0, ne = 0, nt = 0;
   for (int i = 0; i < n; ++i) {
-    if (B.j[i].mode == BQ_ROLL_EWM) ewm.j[ne++] = B.j[i];
+    if (B.j[i].mode == BQ_ROLL_EWM && B.j[i].hi) etr.j[nt++] = B.j[i];
+    else if (B.j[i].mode == BQ_ROLL_EWM) ewm.j[ne++] = B.j[i];
     else win.j[nw++] = B.j[i];
   }
   if (nw) hipLaunchKernelGGL(panel_window_kernel, dim3((unsigned)B.S, (unsigned)nw), dim3(PN_NT), 0, st, win);
-  if (ne) hipLaunchKernelGGL(panel_ewm_kernel, dim3((unsigned)B.S, (unsigned)ne), dim3(PN_NT), 0, st, ewm);
+  if (ne) hipLaunchKernelGGL(panel_ewm_kernel<false>, dim3((unsigned)B.S, (unsigned)ne), dim3(PN_NT), 0, st, ewm);
+  if (nt) hipLaunchKernelGGL(panel_ewm_kernel<true>, dim3((unsigned)B.S, (unsigned)nt), dim3(PN_NT), 0, st, etr);
 }
 
 }  // namespace bq
+
+// LiquidationSweepPump's per-symbol ewm columns in panel mode
+// (liquidation_sweep_pump.py:206-217, 252-253): candidate_atr =
+// TR.ewm(alpha = 1/14, min_periods = 14), ema20 / ema50 of close — the true
+// range formed from the high / low / close loads (no TR column in HBM).
+extern "C" int bq_pump_ewm(const double* high, const double* low, const double* close, int64_t S, int64_t T,
+                           int64_t ld_in, double* atr, double* ema20, double* ema50, int64_t ld_out, void* stream) {
+  using namespace bq;
+  if (!high || !low || !close || !atr || !ema20 || !ema50 || S < 0 || T < 0 || ld_in < T || ld_out < T ||
+      S > 0x7fffffff || T > 0x7fffffff - 2 * PN_TT)
+    return BQ_EINVAL;
+  if (S == 0 || T == 0) return BQ_OK;
+  PanelBatch B;
+  memset(&B, 0, sizeof(B));
+  B.S = S;
+  B.T = (int)T;
+  // pandas: alpha = 1 / (1 + com), com = 1 / alpha - 1 or (span - 1) / 2
+  const double coms[3] = {1.0 / (1.0 / 14.0) - 1.0, (20.0 - 1.0) / 2.0, (50.0 - 1.0) / 2.0};
+  const int minp[3] = {14, 0, 0};
+  double* outs[3] = {atr, ema20, ema50};
+  for (int i = 0; i < 3; ++i) {
+    PanelJob& J = B.j[i];
+    J.x = close;
+    J.out = outs[i];
+    J.ld_in = ld_in;
+    J.ld_out = ld_out;
+    J.rows = S;
+    J.mode = BQ_ROLL_EWM;
+    J.minp = minp[i];
+    J.alpha = 1.0 / (1.0 + coms[i]);
+    J.hi = i == 0 ? high : nullptr;
+    J.lo = i == 0 ? low : nullptr;
+  }
+  launch_panel(B, 3, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}

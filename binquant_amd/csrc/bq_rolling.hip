@@ -1756,6 +1756,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       P.shift = in.shift;
       P.mode = in.mode;
       P.alpha = in.alpha;
+      P.hi = P.lo = nullptr;
       if (npan == PN_MAXJOBS) flush_pan();
       continue;
     }

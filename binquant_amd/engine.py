@@ -336,6 +336,23 @@ def pump_features(
     return out
 
 
+@device_entry
+def pump_ewm(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor,
+             stream: torch.cuda.Stream | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """LiquidationSweepPump's candidate_atr (TR.ewm(alpha=1/14, min_periods=14))
+    and ema20 / ema50 of close in panel mode (bq_pump_ewm: the true range
+    formed in the kernel; liquidation_sweep_pump.py:206-217, 252-253)."""
+    close = _check_panel(close, "close").contiguous()
+    S, T = close.shape
+    high = _check_panel(high, "high", (S, T)).contiguous()
+    low = _check_panel(low, "low", (S, T)).contiguous()
+    outs = [torch.empty((S, T), dtype=torch.float64, device=close.device) for _ in range(3)]
+    st = _lib.load().bq_pump_ewm(_ptr(high), _ptr(low), _ptr(close), S, T, T, *(_ptr(o) for o in outs), T,
+                                 _stream_handle(stream))
+    _lib.check(st, "bq_pump_ewm")
+    return tuple(outs)
+
+
 BURST_FLOAT_COLUMNS = ("baseline_volume_safe", "volume_ratio", "baseline_quote_volume_safe", "quote_volume_ratio",
                        "price_jump", "range_frac", "body_frac", "close_to_high", "recent_up_closes",
                        "activity_burst_score")

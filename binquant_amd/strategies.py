@@ -265,12 +265,12 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
     exact=True: the ewm / rolling-mean columns by the bit-exact replay (the
     live path); default: time-parallel within rounding of pandas (panel mode)."""
     p = p or PumpParams()
+    bench = btc_close.reshape(1, -1).contiguous()
+    if _PUMP_FUSED and not exact and max(p.volume_lookback, p.compression_bars) < 31 and p.momentum_bars < 32:
+        return _pump_score_fused(h, l, c, v, bench, p)
     H, L, C, V = (F.inp(t) for t in (h, l, c, v))
     prev = F.shift(C, 1)
     tr = F.run({"tr": F.fmax(F.fmax(H - L, (H - prev).abs()), (L - prev).abs())})["tr"]   # max(axis=1) skips NaN
-    bench = btc_close.reshape(1, -1).contiguous()
-    if _PUMP_FUSED and not exact and max(p.volume_lookback, p.compression_bars) < 31 and p.momentum_bars < 32:
-        return _pump_score_fused(h, l, c, v, tr, bench, p)
     # the benchmark's [1, T] series ride in the panel's batch (one launch)
     atr, vmean, hmax, lmin, e20, e50, cf, bf, be20, be50 = engine.rolling_many(
         E(tr, alpha=1 / 14, min_periods=14), R(v, p.volume_lookback, "mean", shift=1),
@@ -316,16 +316,15 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
     return out
 
 
-def _pump_score_fused(h, l, c, v, tr, bench, p: PumpParams) -> dict[str, torch.Tensor]:
-    """Panel mode of pump_score_features: the ewm series by bq_rolling_batch,
-    every other column but the quantiles and score_cross in one pass per row
-    (bq_pump_features: the volume mean, the high / low windows and the
-    pad-filled pct_change inside the kernel), then the two rolling quantiles
-    and score_cross."""
-    atr, e20, e50, bf, be20, be50 = engine.rolling_many(
-        E(tr, alpha=1 / 14, min_periods=14), E(c, span=20), E(c, span=50), FF(bench), E(bench, span=20),
-        E(bench, span=50), exact=False,
-    )
+def _pump_score_fused(h, l, c, v, bench, p: PumpParams) -> dict[str, torch.Tensor]:
+    """Panel mode of pump_score_features: the per-symbol ewm series by
+    bq_pump_ewm (the ATR's true range formed in the kernel), the benchmark's
+    by bq_rolling_batch, every other column but the quantiles and score_cross
+    in one pass per row (bq_pump_features: the volume mean, the high / low
+    windows and the pad-filled pct_change inside the kernel), then the two
+    rolling quantiles and score_cross."""
+    atr, e20, e50 = engine.pump_ewm(h, l, c)
+    bf, be20, be50 = engine.rolling_many(FF(bench), E(bench, span=20), E(bench, span=50), exact=False)
     st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
                               p.volume_lookback, p.compression_bars)
     thr_s, thr_v = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)

@@ -330,6 +330,17 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
 int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, int32_t min_periods, double* out,
            int64_t ld_out, void* stream);
 
+/*
+ * LiquidationSweepPump's per-symbol ewm columns in panel mode (time-parallel,
+ * within rounding of pandas; strategies/liquidation_sweep_pump.py:206-217,
+ * :252-253): atr = TR.ewm(alpha=1/14, adjust=False, min_periods=14).mean() of
+ * the true range of (high, low, close) — formed in the kernel, no TR column —
+ * and ema20 / ema50 = close.ewm(span=20 / 50, adjust=False).mean(). Inputs
+ * [S][ld_in], outputs [S][ld_out] fp64. Feeds bq_pump_features.
+ */
+int bq_pump_ewm(const double* high, const double* low, const double* close, int64_t S, int64_t T, int64_t ld_in,
+                double* atr, double* ema20, double* ema50, int64_t ld_out, void* stream);
+
 /* ---- whole-series order statistics and label cooldown ---------------------- */
 /*
  * out[s] = numpy.quantile(x[s][~isnan], q) (numpy 'linear' method, numpy's
