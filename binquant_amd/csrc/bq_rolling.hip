@@ -94,79 +94,86 @@ struct Moments {
     prev = first;
     nobs = neg = same = 0;
   }
+  // Straight-line updates: every candidate value is formed and the state
+  // takes it by select where v is observed (a missing v leaves the state as
+  // it is, as pandas' `if val == val` does). Branches here split a replay
+  // step into a dozen basic blocks with their exec-mask bookkeeping; the
+  // values are those of the branchy form bit for bit.
   __device__ __forceinline__ void add(double v, bool welford) {
-    if (v != v) return;
-    ++nobs;
+    const bool ok = v == v;
+    nobs += ok ? 1 : 0;
     if (welford) {
-      vn += 1.0;
+      const double vn1 = vn + 1.0;
       const double pm = mean - v_add;
       const double y = v - v_add;
       const double t = y - mean;
-      v_add = t + mean - y;
-      mean = vn != 0.0 ? mean + t / vn : 0.0;
-      ssq = ssq + (v - pm) * (v - mean);
+      const double va = t + mean - y;
+      const double m1 = vn1 != 0.0 ? mean + t / vn1 : 0.0;
+      const double s1 = ssq + (v - pm) * (v - m1);
+      vn = ok ? vn1 : vn;
+      v_add = ok ? va : v_add;
+      mean = ok ? m1 : mean;
+      ssq = ok ? s1 : ssq;
     } else {
       const double y = v - c_add;
       const double t = sum + y;
-      c_add = t - sum - y;
-      sum = t;
-      neg += signbit(v) ? 1 : 0;
+      const double ca = t - sum - y;
+      c_add = ok ? ca : c_add;
+      sum = ok ? t : sum;
+      neg += (ok && signbit(v)) ? 1 : 0;
     }
-    same = (v == prev) ? same + 1 : 1;
-    prev = v;
+    same = ok ? ((v == prev) ? same + 1 : 1) : same;
+    prev = ok ? v : prev;
   }
   __device__ __forceinline__ void remove(double v, bool welford) {
-    if (v != v) return;
-    --nobs;
+    const bool ok = v == v;
+    nobs -= ok ? 1 : 0;
     if (welford) {
-      vn -= 1.0;
-      if (vn != 0.0) {
-        const double pm = mean - v_rem;
-        const double y = v - v_rem;
-        const double t = y - mean;
-        v_rem = t + mean - y;
-        mean = mean - t / vn;
-        ssq = ssq - (v - pm) * (v - mean);
-      } else {
-        mean = ssq = 0.0;
-      }
+      const double vn1 = vn - 1.0;
+      const bool live = vn1 != 0.0;
+      const double pm = mean - v_rem;
+      const double y = v - v_rem;
+      const double t = y - mean;
+      const double vr = t + mean - y;
+      const double m1 = mean - t / vn1;
+      const double s1 = ssq - (v - pm) * (v - m1);
+      vn = ok ? vn1 : vn;
+      v_rem = ok && live ? vr : v_rem;
+      mean = ok ? (live ? m1 : 0.0) : mean;
+      ssq = ok ? (live ? s1 : 0.0) : ssq;
     } else {
       const double y = -v - c_rem;
       const double t = sum + y;
-      c_rem = t - sum - y;
-      sum = t;
-      neg -= signbit(v) ? 1 : 0;
+      const double cr = t - sum - y;
+      c_rem = ok ? cr : c_rem;
+      sum = ok ? t : sum;
+      neg -= (ok && signbit(v)) ? 1 : 0;
     }
   }
-  __device__ __forceinline__ double result(int mode, int minp) const {
-    switch (mode) {
-      case BQ_ROLL_SUM:   // calc_sum
-        if (nobs == 0 && minp == 0) return 0.0;
-        if (nobs < minp) return qnan();
-        return same >= nobs ? prev * (double)nobs : sum;
-      case BQ_ROLL_MEAN: {   // calc_mean
-        if (nobs < minp || nobs <= 0) return qnan();
-        double r = sum / (double)nobs;
-        if (same >= nobs) r = prev;
-        else if (neg == 0 && r < 0.0) r = 0.0;
-        else if (neg == nobs && r > 0.0) r = 0.0;
-        return r;
+  // calc_sum / calc_mean / calc_var as select chains (every candidate formed;
+  // the class is a compile-time constant at the replays' call sites)
+  __device__ __forceinline__ double result(int mode, int minp, bool welford) const {
+    if (!welford) {
+      const double dn = (double)nobs;
+      if (mode == BQ_ROLL_SUM) {   // calc_sum
+        double r = same >= nobs ? prev * dn : sum;
+        r = nobs < minp ? qnan() : r;
+        return (nobs == 0 && minp == 0) ? 0.0 : r;
       }
-      default: {   // calc_var (ddof 1 or 0), std = sqrt
-        const double ddof = (mode == BQ_ROLL_VAR || mode == BQ_ROLL_STD) ? 1.0 : 0.0;
-        double r;
-        if (vn >= (double)minp && vn > ddof) {
-          if (vn == 1.0 || (double)same >= vn) r = 0.0;
-          else {
-            r = ssq / (vn - ddof);
-            r = r < 0.0 ? 0.0 : r;
-          }
-        } else {
-          r = qnan();
-        }
-        return (mode == BQ_ROLL_STD || mode == BQ_ROLL_STD0) ? sqrt(r) : r;
-      }
+      // calc_mean
+      double r = sum / dn;
+      r = (neg == nobs && r > 0.0) ? 0.0 : r;
+      r = (neg == 0 && r < 0.0) ? 0.0 : r;
+      r = same >= nobs ? prev : r;
+      return (nobs < minp || nobs <= 0) ? qnan() : r;
     }
+    // calc_var (ddof 1 or 0), std = sqrt
+    const double ddof = (mode == BQ_ROLL_VAR || mode == BQ_ROLL_STD) ? 1.0 : 0.0;
+    double r = ssq / (vn - ddof);
+    r = r < 0.0 ? 0.0 : r;
+    r = (vn == 1.0 || (double)same >= vn) ? 0.0 : r;
+    r = (vn >= (double)minp && vn > ddof) ? r : qnan();
+    return (mode == BQ_ROLL_STD || mode == BQ_ROLL_STD0) ? sqrt(r) : r;
   }
 };
 
@@ -195,33 +202,24 @@ struct ReplayLane {
       if (v_in == v_in) weighted = v_in;
       return weighted;
     }
-    if (EWM) {
+    if (EWM) {   // straight-line, as Moments (selects, the same values)
       const double alpha = A.alpha, om = 1.0 - alpha;
-      if (!steady && t == 0) {
-        weighted = v_in;
-        nobs = v_in == v_in;
-      } else {
-        const bool obs = v_in == v_in;
-        nobs += obs;
-        if (weighted == weighted) {
-          old_wt *= om;
-          if (obs) {
-            if (weighted != v_in) {
-              weighted = old_wt * weighted + alpha * v_in;
-              weighted /= old_wt + alpha;
-            }
-            old_wt = 1.0;
-          }
-        } else if (obs) {
-          weighted = v_in;
-        }
-      }
+      const bool obs = v_in == v_in;
+      const bool wv = weighted == weighted;
+      const double ow = wv ? old_wt * om : old_wt;
+      const double nw = (ow * weighted + alpha * v_in) / (ow + alpha);
+      double w2 = (wv && obs && weighted != v_in) ? nw : weighted;
+      w2 = (!wv && obs) ? v_in : w2;
+      const bool first = !steady && t == 0;
+      weighted = first ? v_in : w2;
+      old_wt = first ? old_wt : ((wv && obs) ? 1.0 : ow);
+      nobs = first ? (obs ? 1 : 0) : nobs + (obs ? 1 : 0);
       return nobs >= A.minp ? weighted : qnan();
     }
     if (!steady && t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
     if (steady || (t >= A.win && t - A.shift - A.win >= 0)) m.remove(v_out, welford);
     m.add(v_in, welford);
-    return m.result(A.mode, A.minp);
+    return m.result(A.mode, A.minp, welford);
   }
 };
 
@@ -307,7 +305,8 @@ __global__ __launch_bounds__(WAVE) void replay_kernel(const RollBatch B, int rin
 #define BQ_RS_STAGE_OUT 1   // results leave through LDS as coalesced row segments
 #endif
 #ifndef BQ_RS_WPS
-#define BQ_RS_WPS 2   // min waves per SIMD (register cap) of the re-staging replays
+#define BQ_RS_WPS 1   // min waves per SIMD (register cap) of the re-staging replays: 1 wave, no spill (see
+                      // launch_restage: ~1 wave per SIMD at panel sizes; 2 spilled 26 VGPRs of the Welford class)
 #endif
 #ifndef BQ_RS_LPT
 #define BQ_RS_LPT 1   // mixed replay batches ordered longest class first
