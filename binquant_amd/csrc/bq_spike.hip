@@ -105,6 +105,97 @@ __device__ __forceinline__ double sp_window(int t, int w, F f) {
   return r;
 }
 
+// The same statistic at a lane's SP_K consecutive candles tb .. tb + 3 (ring
+// positions pb .. pb + 3): their windows share the W - 3 positions
+// pb + 4 - W .. pb, aggregated once; each candle adds its own older (lead) and
+// newer (trail) extras — W + 3 values read instead of 4 W. The observed
+// count, min / max, sign OR / AND and the newest value combine exactly; the
+// sum is (lead + core) + trail instead of strictly time-ordered (rounding).
+struct SpAgg {
+  double s, mn, mx, last;
+  int n;
+  unsigned sor, sand;
+  __device__ __forceinline__ void init() {
+    s = 0.0;
+    mn = __builtin_inf();
+    mx = -__builtin_inf();
+    last = qnan();
+    n = 0;
+    sor = 0u;
+    sand = 1u;
+  }
+  __device__ __forceinline__ void add(double v) {
+    const bool ok = v == v;
+    const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
+    s += ok ? v : 0.0;
+    n += ok;
+    sor |= ok ? sg : 0u;
+    sand &= ok ? sg : 1u;
+    mn = ok ? fmin(mn, v) : mn;
+    mx = ok ? fmax(mx, v) : mx;
+    last = ok ? v : last;
+  }
+  // this (older) followed by b (newer)
+  __device__ __forceinline__ SpAgg then(const SpAgg& b) const {
+    SpAgg r;
+    r.s = s + b.s;
+    r.n = n + b.n;
+    r.sor = sor | b.sor;
+    r.sand = sand & b.sand;
+    r.mn = fmin(mn, b.mn);
+    r.mx = fmax(mx, b.mx);
+    r.last = b.n > 0 ? b.last : last;
+    return r;
+  }
+};
+
+template <bool MEAN>
+__device__ __forceinline__ double sp_finish(const SpAgg& a, int t, int w) {
+  if (t < w - 1 || a.n < w || a.n <= 0) return qnan();
+  const bool same = a.mn == a.mx;
+  if (!MEAN) return same ? a.last * (double)a.n : a.s;
+  double r = a.s / (double)a.n;
+  if (same) r = a.last;
+  else if (a.sor == 0u && r < 0.0) r = 0.0;
+  else if (a.sand == 1u && r > 0.0) r = 0.0;
+  return r;
+}
+
+// F(p): the value at ring position p (windows shorter than SP_K: one
+// aggregate per candle)
+template <bool MEAN, typename F>
+__device__ __forceinline__ void sp_window4(int tb, int pb, int w, F f, double (&r)[SP_K]) {
+  if (w < SP_K) {
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      SpAgg a;
+      a.init();
+      for (int p = pb + k - w + 1; p <= pb + k; ++p) a.add(f(p));
+      r[k] = sp_finish<MEAN>(a, tb + k, w);
+    }
+    return;
+  }
+  SpAgg core;
+  core.init();
+  for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p));
+  SpAgg trail;
+  trail.init();
+  SpAgg lead[SP_K];
+  lead[SP_K - 1].init();
+#pragma unroll
+  for (int k = SP_K - 2; k >= 0; --k) {   // lead_k = value at pb + k + 1 - w, then lead_{k+1}
+    SpAgg one;
+    one.init();
+    one.add(f(pb + k + 1 - w));
+    lead[k] = one.then(lead[k + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < SP_K; ++k) {
+    if (k > 0) trail.add(f(pb + k));
+    r[k] = sp_finish<MEAN>(lead[k].then(core).then(trail), tb + k, w);
+  }
+}
+
 // an integer count over the window (values 0 / 1, never missing): the sum
 template <typename F>
 __device__ __forceinline__ double sp_count(int t, int w, F f) {
@@ -214,16 +305,14 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
     put(BQ_SPIKE_CLOSE_OPEN_RATIO, r);
     // price: mean over the base window, z-score against the replayed std
     double ma[SP_K], sd[SP_K];
-#pragma unroll
-    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sC[sp_slot(pb + k + j)]; });
+    sp_window4<true>(tb, pb, W, [&](int p) { return sC[sp_slot(p)]; }, ma);
     put(BQ_SPIKE_PRICE_MA, ma);
     sp_load(A.in[SB_PSTD] + irow, tb, T, vin, sd);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = (c[k] - ma[k]) / (sd[k] + SP_EPS);
     put(BQ_SPIKE_PRICE_ZSCORE, r);
     // volume
-#pragma unroll
-    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sV[sp_slot(pb + k + j)]; });
+    sp_window4<true>(tb, pb, W, [&](int p) { return sV[sp_slot(p)]; }, ma);
     put(BQ_SPIKE_VOLUME_MA, ma);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = v[k] / (ma[k] + SP_EPS);
@@ -233,8 +322,7 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
     for (int k = 0; k < SP_K; ++k) r[k] = (v[k] - ma[k]) / (sd[k] + SP_EPS);
     put(BQ_SPIKE_VOLUME_ZSCORE, r);
     // quote volume
-#pragma unroll
-    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, W, [&](int j) { return sQ[sp_slot(pb + k + j)]; });
+    sp_window4<true>(tb, pb, W, [&](int p) { return sQ[sp_slot(p)]; }, ma);
     put(BQ_SPIKE_QUOTE_VOLUME_MA, ma);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = q[k] / (ma[k] + SP_EPS);
@@ -275,12 +363,10 @@ __global__ __launch_bounds__(SP_NT) void spike_base_kernel(const SpikeBaseArgs A
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = sp_count(tb + k, 5, [&](int j) { return pc_at(pb + k + j) > 0.0 ? 1 : 0; });
     put(BQ_SPIKE_PC_POS_COUNT_5, r);
-#pragma unroll
-    for (int k = 0; k < SP_K; ++k) r[k] = sp_window<false>(tb + k, 5, [&](int j) { return fabs(pc_at(pb + k + j)); });
+    sp_window4<false>(tb, pb, 5, [&](int p) { return fabs(pc_at(p)); }, r);
     put(BQ_SPIKE_PC_ABS_SUM_5, r);
     // body size: 10-bar mean, z-score against the replayed std
-#pragma unroll
-    for (int k = 0; k < SP_K; ++k) ma[k] = sp_window<true>(tb + k, 10, [&](int j) { return bsp_at(pb + k + j); });
+    sp_window4<true>(tb, pb, 10, [&](int p) { return bsp_at(p); }, ma);
     put(BQ_SPIKE_BODY_SIZE_PCT_MA_10, ma);
     sp_load(A.in[SB_BSD] + irow, tb, T, vin, sd);
 #pragma unroll
