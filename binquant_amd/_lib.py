@@ -209,6 +209,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_pump_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _PP, _I32, _I32, _I32, _PP, _I64, _P]),
+    "bq_pump_features_ewm": (ctypes.c_int, [_PP, _I64, _I64, _I64, _PP, _I32, _I32, _I32, _PP, _I64, _P]),
     "bq_burst_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _P, _PP, _PP, _P, _I64, _P]),
     "bq_burst_qualify": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P, _P]),
     "bq_spike_base": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _I32, _PP, _PP, _I64, _P]),

@@ -17,6 +17,12 @@ constexpr int WAVE = 64;
 
 __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
 
+// pandas' window operations (rolling *, ewm) see +-inf as missing: they run on
+// np.where(np.isinf(values), np.nan, values) (BaseWindow._prep_values,
+// pandas/core/window/rolling.py). ffill, element-wise ops and np.quantile keep
+// infinities. x - x == 0 is false exactly for NaN and +-inf.
+__device__ __forceinline__ double win_val(double x) { return x - x == 0.0 ? x : qnan(); }
+
 // ---- compensated (double-double) accumulation ------------------------------
 struct dd {
   double hi, lo;

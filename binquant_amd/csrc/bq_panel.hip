@@ -108,8 +108,8 @@ __global__ __launch_bounds__(PN_NT) void panel_window_kernel(const PanelBatch B)
     const int tb = t0 + PN_K * tid, pb = PN_H + PN_K * tid;
     double c[PN_K];
 #pragma unroll
-    for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
-    const double pc0 = tb >= 1 && tb <= T ? x[tb - 1] : qnan();
+    for (int k = 0; k < PN_K; ++k) c[k] = win_val(nx[k]);   // +-inf is missing (pandas' window ops)
+    const double pc0 = tb >= 1 && tb <= T ? win_val(x[tb - 1]) : qnan();
     if (t0 + PN_TT < T) pn_load(x, tb + PN_TT, T, vin, nx);
     // run starts of the values (NaN counts as a change)
     int lcl[PN_K];
@@ -243,12 +243,12 @@ __global__ __launch_bounds__(PN_NT) void panel_ewm_kernel(const PanelBatch B) {
       double pc = tb >= 1 && tb <= T ? x[tb - 1] : qnan();
 #pragma unroll
       for (int k = 0; k < PN_K; ++k) {
-        c[k] = tb + k < T ? true_range(nh[k], nl[k], pc) : qnan();
+        c[k] = tb + k < T ? win_val(true_range(nh[k], nl[k], pc)) : qnan();
         pc = nx[k];
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < PN_K; ++k) c[k] = nx[k];
+      for (int k = 0; k < PN_K; ++k) c[k] = win_val(nx[k]);   // +-inf is missing (pandas' window ops)
     }
     if (t0 + PN_TT < T) load_tile(tb + PN_TT);
     {

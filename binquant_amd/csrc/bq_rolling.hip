@@ -198,10 +198,12 @@ struct ReplayLane {
   // always inside the row) — lets a caller drop the per-step checks
   __device__ __forceinline__ double step(const RollJob& A, bool EWM, bool welford, int t, double v_in, double v_out,
                                          bool FFILL = false, bool steady = false) {
-    if (FFILL) {   // last observation carried forward (weighted holds it)
+    if (FFILL) {   // last observation carried forward (weighted holds it; infinities are values)
       if (v_in == v_in) weighted = v_in;
       return weighted;
     }
+    v_in = win_val(v_in);   // window operations: +-inf is missing
+    v_out = win_val(v_out);
     if (EWM) {   // straight-line, as Moments (selects, the same values)
       const double alpha = A.alpha, om = 1.0 - alpha;
       const bool obs = v_in == v_in;
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(256) void rank_kernel(const RollBatch B) {
   const int t_begin = seg * A.seg, t_end = min(T, t_begin + A.seg);
   auto val = [&](int t) -> double {
     const int i = t - sh;
-    return (i >= 0 && i < T) ? x[i] : qnan();
+    return (i >= 0 && i < T) ? win_val(x[i]) : qnan();
   };
   SortedWin<W> win;
   win.clear();
@@ -726,12 +728,12 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
 #pragma unroll
       for (int j = 0; j < SL_C; j += 2) {
         const dbl2u p = *reinterpret_cast<const dbl2u*>(x + i0 + j);
-        v[j] = p.x;
-        v[j + 1] = p.y;
+        v[j] = win_val(p.x);
+        v[j + 1] = win_val(p.y);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
+      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? win_val(x[i0 + j]) : qnan();
     }
   };
   // Placeholders split so the wanted rank sits in a FIXED slot: with n
@@ -985,7 +987,7 @@ __global__ __launch_bounds__(64 * BQ_TR_WPB) void tile_rank_kernel(const RollBat
   for (int e = 0; e < EPL; ++e) {
     const int u = lane * EPL + e;
     const int i = ubase + u;
-    const double v = (live && u < U && t0 - w + 1 + u >= A.shift && i < T) ? x[i] : qnan();
+    const double v = (live && u < U && t0 - w + 1 + u >= A.shift && i < T) ? win_val(x[i]) : qnan();
     key[e] = okey_nan_last(v);
     num[e] = v == v;
     if constexpr (PACK) {
@@ -1257,7 +1259,7 @@ __global__ __launch_bounds__(SR_NT) void stencil_rank_kernel(const RollBatch B) 
   const int base = t0 - (w - 1) - A.shift;
   for (int i = threadIdx.x; i < SR_NT + w - 1; i += SR_NT) {
     const int xi = base + i;
-    s[i] = (xi >= 0 && xi < T) ? x[xi] : qnan();
+    s[i] = (xi >= 0 && xi < T) ? win_val(x[xi]) : qnan();
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;

@@ -84,7 +84,7 @@ __device__ __forceinline__ double sp_window(int t, int w, F f) {
   int n = 0;
   unsigned sor = 0u, sand = 1u;
   for (int j = -w + 1; j <= 0; ++j) {
-    const double v = f(j);
+    const double v = win_val(f(j));   // +-inf is missing (pandas' window ops)
     const bool ok = v == v;
     const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
     s += ok ? v : 0.0;
@@ -125,6 +125,7 @@ struct SpAgg {
     sand = 1u;
   }
   __device__ __forceinline__ void add(double v) {
+    v = win_val(v);   // +-inf is missing (pandas' window ops)
     const bool ok = v == v;
     const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
     s += ok ? v : 0.0;

@@ -337,6 +337,42 @@ def pump_features(
 
 
 @device_entry
+def pump_features_ewm(
+    high: torch.Tensor,
+    low: torch.Tensor,
+    close: torch.Tensor,
+    volume: torch.Tensor,
+    bench_ffill: torch.Tensor,
+    bench_ema20: torch.Tensor,
+    bench_ema50: torch.Tensor,
+    momentum_bars: int = 3,
+    volume_lookback: int = 20,
+    compression_bars: int = 6,
+    stream: torch.cuda.Stream | None = None,
+) -> dict[str, torch.Tensor]:
+    """pump_features with candidate_atr / ema20 / ema50 formed inside the pass
+    (bq_pump_features_ewm: the three ewm scans on the row's tiles, no ewm
+    column read back; liquidation_sweep_pump.py:206-217, 252-253)."""
+    close = _check_panel(close, "close")
+    S, T = close.shape
+    ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in
+           zip((high, low, close, volume), ("high", "low", "close", "volume"))]
+    bench = []
+    for t, n in zip((bench_ffill, bench_ema20, bench_ema50), ("bench_ffill", "bench_ema20", "bench_ema50")):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float64 or t.numel() != T:
+            raise ValueError(f"{n}: expected a float64 CUDA tensor of {T} values")
+        bench.append(t.reshape(T).contiguous())
+    out = {n: torch.empty((S, T), dtype=torch.float64, device=close.device) for n in PUMP_COLUMNS}
+    st = _lib.load().bq_pump_features_ewm(
+        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, _lib.ptr_array([t.data_ptr() for t in bench]),
+        int(momentum_bars), int(volume_lookback), int(compression_bars),
+        _lib.ptr_array([out[n].data_ptr() for n in PUMP_COLUMNS]), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_pump_features_ewm")
+    return out
+
+
+@device_entry
 def pump_ewm(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor,
              stream: torch.cuda.Stream | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """LiquidationSweepPump's candidate_atr (TR.ewm(alpha=1/14, min_periods=14))

@@ -243,6 +243,11 @@ _SPIKE_FUSED = True
 # panel mode of pump_score_features through bq_pump_features (False: the staged
 # panel pipeline; tests compare the two)
 _PUMP_FUSED = True
+# the pump pass forms its ewm columns itself (bq_pump_features_ewm) instead of
+# reading them from bq_pump_ewm's scans. Measured slower at 12.5k x 2k (2.11
+# vs 1.90 ms per row: the three scans sit between the tile's barriers of a
+# pass that runs 2 workgroups per CU), so off; tested both ways.
+_PUMP_EWM_IN_PASS = False
 
 
 @dataclass
@@ -317,16 +322,21 @@ def pump_score_features(o, h, l, c, v, btc_close, p: PumpParams | None = None,
 
 
 def _pump_score_fused(h, l, c, v, bench, p: PumpParams) -> dict[str, torch.Tensor]:
-    """Panel mode of pump_score_features: the per-symbol ewm series by
-    bq_pump_ewm (the ATR's true range formed in the kernel), the benchmark's
-    by bq_rolling_batch, every other column but the quantiles and score_cross
-    in one pass per row (bq_pump_features: the volume mean, the high / low
-    windows and the pad-filled pct_change inside the kernel), then the two
-    rolling quantiles and score_cross."""
-    atr, e20, e50 = engine.pump_ewm(h, l, c)
+    """Panel mode of pump_score_features: the per-symbol ewm columns by
+    bq_pump_ewm (the ATR's true range formed in the scan), the benchmark's
+    ffill / ewm rows by bq_rolling_batch, every other column but the
+    quantiles and score_cross in one pass per row (bq_pump_features: the
+    volume mean, the high / low windows and the pad-filled pct_change inside
+    the kernel), then the two rolling quantiles and score_cross.
+    _PUMP_EWM_IN_PASS: the ewm scans inside the pass (bq_pump_features_ewm)."""
     bf, be20, be50 = engine.rolling_many(FF(bench), E(bench, span=20), E(bench, span=50), exact=False)
-    st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
-                              p.volume_lookback, p.compression_bars)
+    if _PUMP_EWM_IN_PASS:
+        st = engine.pump_features_ewm(h, l, c, v, bf[0], be20[0], be50[0], p.momentum_bars, p.volume_lookback,
+                                      p.compression_bars)
+    else:
+        atr, e20, e50 = engine.pump_ewm(h, l, c)
+        st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
+                                  p.volume_lookback, p.compression_bars)
     thr_s, thr_v = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)
         R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
         R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1), exact=False,

@@ -384,6 +384,18 @@ enum bq_pump_col {
 int bq_pump_features(const double* const* in, int64_t S, int64_t T, int64_t ld_in, const double* const* bench,
                      int32_t momentum_bars, int32_t volume_lookback, int32_t compression_bars, double* const* out,
                      int64_t ld_out, void* stream);
+/*
+ * The same pass with the three per-symbol ewm columns formed inside it
+ * (candidate_atr = TR.ewm(alpha=1/14, adjust=False, min_periods=14).mean(),
+ * ema20 / ema50 = close.ewm(span=20 / 50, adjust=False).mean(),
+ * liquidation_sweep_pump.py:206-217, 252-253; within rounding of pandas, a
+ * row with a missing / infinite value continuing with pandas' recursion):
+ * in = {high, low, close, volume} only; out[BQ_PUMP_CANDIDATE_ATR /
+ * BQ_PUMP_EMA20 / BQ_PUMP_EMA50] must be non-NULL.
+ */
+int bq_pump_features_ewm(const double* const* in, int64_t S, int64_t T, int64_t ld_in, const double* const* bench,
+                         int32_t momentum_bars, int32_t volume_lookback, int32_t compression_bars,
+                         double* const* out, int64_t ld_out, void* stream);
 
 /*
  * ActivityBurstPump.compute_indicators (strategies/activity_burst_pump.py:51-158)

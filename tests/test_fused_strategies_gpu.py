@@ -19,14 +19,20 @@ from tests.util import assert_close
 pytestmark = pytest.mark.gpu
 
 
-def test_pump_fused_equals_staged_panel(cuda):
+@pytest.mark.parametrize("ewm_in_pass", [True, False])
+def test_pump_fused_equals_staged_panel(cuda, ewm_in_pass, monkeypatch):
     """bq_pump_features (one pass per row) against the staged panel pipeline
     on a 200 x 2500 panel with halts, gaps and zero volume: columns whose
     windows are order statistics / shifts equal bit for bit, the volume mean
     and what depends on it within 1e-12 of each row's magnitude (its sliding
     sum restarts at each lane's 4 candles instead of 8), flags equal away
-    from near-ties."""
+    from near-ties. With the ewm columns formed in the pass
+    (bq_pump_features_ewm: 4-candle lane maps and a DPP scan instead of the
+    panel kernel's 8-candle maps) those columns and what depends on them are
+    within 1e-12 of the row's magnitude too."""
     from binquant_amd import strategies
+
+    monkeypatch.setattr(strategies, "_PUMP_EWM_IN_PASS", ewm_in_pass)
     from binquant_amd.synth import numpy_panel
 
     S, T = 200, 2500
@@ -46,6 +52,9 @@ def test_pump_fused_equals_staged_panel(cuda):
     assert list(fused) == list(staged)
     exact_cols = ("candidate_atr", "momentum_3", "pre_breakout_compression", "prior_high", "close_location", "ema20",
                   "ema50", "trend_score", "momentum_atr", "btc_momentum_3", "btc_trend_score", "relative_strength")
+    if ewm_in_pass:
+        exact_cols = tuple(k for k in exact_cols if k not in ("candidate_atr", "ema20", "ema50", "trend_score",
+                                                               "momentum_atr"))
     for k in staged:
         x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
         if k in exact_cols:
@@ -57,6 +66,8 @@ def test_pump_fused_equals_staged_panel(cuda):
                 fin = np.where(np.isfinite(y), np.abs(y), np.nan)
                 sc = np.nan_to_num(np.nanmax(fin, axis=1, initial=0.0), nan=1.0)
             sc = np.where(sc > 0, sc, 1.0)
+            if k == "trend_score":   # (ema20 - ema50) / ema50: the emas' rounding relative to 1, not to the difference
+                sc = np.maximum(sc, 1.0)
             assert_close(x, y, f"fused.{k}", rtol=1e-12, scale=np.broadcast_to(sc[:, None], y.shape), atol_rel=1e-13)
 
 
@@ -219,8 +230,54 @@ def test_fused_odd_shapes_equal_staged(cuda, S, T):
                 sc = np.nan_to_num(np.nanmax(fin, axis=1, initial=0.0), nan=1.0)
                 sc = np.where(sc > 0, sc, 1.0)
                 lim = 1e-12 * np.abs(y) + 1e-13 * (sc[:, None] if y.ndim == 2 else sc)
+                if name == "pump" and k == "trend_score":   # the emas' rounding relative to 1 (cancellation)
+                    lim = lim + 1e-13
                 if name == "spike" and k in zb:   # the cancellation bound of test_spike_fused_equals_staged
                     sd, base = zb[k]
                     lim = lim + 1e-13 * np.abs(base) / (sd + 1e-6)
                 ok = np.isnan(y) | (x == y) | (np.abs(x - y) <= lim)   # x == y: equal infinities (v / 0)
             assert ok.all(), (name, k, int((~ok).sum()))
+
+
+@pytest.mark.parametrize("S,T", [(9, 3100), (4, 3), (3, 1024), (2, 1)])
+def test_pump_ewm_in_pass_against_pandas(cuda, S, T):
+    """bq_pump_features_ewm's candidate_atr / ema20 / ema50 (the scans inside
+    the pass, pandas' recursion from the first tile holding a missing or
+    infinite value) against pandas' ewm (adjust=False) of the true range /
+    close and against bq_pump_ewm, at 1e-12 of each row's magnitude with the
+    NaN positions equal: a late listing (leading NaNs past the first tile), a
+    NaN high only (the true range alone turns serial), an infinite close, a
+    NaN first candle, a NaN stretch across a tile boundary, an all-NaN row."""
+    import pandas as pd
+
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    p = numpy_panel(S, T, seed0=7 * S + T, edges=False)
+    h, l, c, v = (p[k].copy() for k in ("high", "low", "close", "volume"))
+    if T > 3000:
+        h[0, :] = l[0, :] = c[0, :] = np.nan
+        h[1, :1500] = l[1, :1500] = c[1, :1500] = np.nan
+        h[2, 700] = np.nan
+        c[3, 2000] = np.inf
+        h[4, 0] = l[4, 0] = c[4, 0] = np.nan
+        c[5, 1020:1030] = np.nan
+        h[6, 2040:2060] = l[6, 2040:2060] = np.nan
+    d = [torch.from_numpy(x).cuda() for x in (h, l, c, v)]
+    bench = torch.from_numpy(c[-1].copy()).cuda()
+    got = engine.pump_features_ewm(*d, bench, bench, bench)
+    ref = engine.pump_ewm(d[0], d[1], d[2])
+    for r in range(S):
+        hs, ls, cs = pd.Series(h[r]), pd.Series(l[r]), pd.Series(c[r])
+        tr = pd.concat([hs - ls, (hs - cs.shift(1)).abs(), (ls - cs.shift(1)).abs()], axis=1).max(axis=1)
+        want = {"candidate_atr": tr.ewm(alpha=1 / 14, adjust=False, min_periods=14).mean().to_numpy(),
+                "ema20": cs.ewm(span=20, adjust=False).mean().to_numpy(),
+                "ema50": cs.ewm(span=50, adjust=False).mean().to_numpy()}
+        for i, k in enumerate(("candidate_atr", "ema20", "ema50")):
+            x = got[k][r].cpu().numpy()
+            for name, y in ((f"pandas {k} row {r}", want[k]), (f"bq_pump_ewm {k} row {r}", ref[i][r].cpu().numpy())):
+                np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=name)
+                fin = np.isfinite(y)
+                np.testing.assert_array_equal(x[~fin & ~np.isnan(y)], y[~fin & ~np.isnan(y)], err_msg=name)
+                sc = float(np.max(np.abs(y[fin]))) if fin.any() else 1.0
+                assert np.all(np.abs(x[fin] - y[fin]) <= 1e-12 * np.abs(y[fin]) + 1e-13 * sc), name
