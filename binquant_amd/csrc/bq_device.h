@@ -22,6 +22,9 @@ __device__ __forceinline__ double qnan() { return __builtin_nan(""); }
 // pandas/core/window/rolling.py). ffill, element-wise ops and np.quantile keep
 // infinities. x - x == 0 is false exactly for NaN and +-inf.
 __device__ __forceinline__ double win_val(double x) { return x - x == 0.0 ? x : qnan(); }
+// the same rule as an observation test (one add + one compare), for loops
+// that already select on their observation flag
+__device__ __forceinline__ bool win_ok(double x) { return x - x == 0.0; }
 
 // ---- compensated (double-double) accumulation ------------------------------
 struct dd {

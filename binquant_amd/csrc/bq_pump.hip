@@ -333,8 +333,8 @@ __global__ __launch_bounds__(PF_NT) void pump_features_kernel(const PumpArgs A, 
       double s = 0.0;
       int nobs = 0, neg = 0;
       for (int j = -VW; j <= -1; ++j) {
-        const double v = win_val(sV[pf_slot(pb + j)]);
-        const bool ok = v == v;
+        const double v = sV[pf_slot(pb + j)];
+        const bool ok = win_ok(v);   // NaN and +-inf are missing (window op)
         s += ok ? v : 0.0;
         nobs += ok;
         neg += ok && signbit(v);
@@ -344,8 +344,8 @@ __global__ __launch_bounds__(PF_NT) void pump_features_kernel(const PumpArgs A, 
       for (int k = 0; k < PF_K; ++k) {
         const int t = tb + k, p = pb + k;
         if (k > 0) {
-          const double vi = win_val(sV[pf_slot(p - 1)]), vo_ = win_val(sV[pf_slot(p - 1 - VW)]);
-          const bool oi = vi == vi, oo = vo_ == vo_;
+          const double vi = sV[pf_slot(p - 1)], vo_ = sV[pf_slot(p - 1 - VW)];
+          const bool oi = win_ok(vi), oo = win_ok(vo_);
           s = (s + (oi ? vi : 0.0)) - (oo ? vo_ : 0.0);
           nobs += (int)oi - (int)oo;
           neg += (int)(oi && signbit(vi)) - (int)(oo && signbit(vo_));
@@ -364,11 +364,12 @@ __global__ __launch_bounds__(PF_NT) void pump_features_kernel(const PumpArgs A, 
         double hm = -__builtin_inf(), lm = __builtin_inf();
         int nh = 0, nl = 0;
         for (int j = -CW; j <= -1; ++j) {
-          const double hv = win_val(sH[pf_slot(p + j)]), lv = win_val(sL[pf_slot(p + j)]);
-          nh += hv == hv;
-          nl += lv == lv;
-          hm = hv > hm ? hv : hm;
-          lm = lv < lm ? lv : lm;
+          const double hv = sH[pf_slot(p + j)], lv = sL[pf_slot(p + j)];
+          const bool oh = win_ok(hv), ol = win_ok(lv);   // NaN and +-inf are missing (window op)
+          nh += oh;
+          nl += ol;
+          hm = oh && hv > hm ? hv : hm;
+          lm = ol && lv < lm ? lv : lm;
         }
         hmax[k] = nh >= CW ? hm : qnan();
         const double lmin = nl >= CW ? lm : qnan();

@@ -100,7 +100,7 @@ struct Moments {
   // step into a dozen basic blocks with their exec-mask bookkeeping; the
   // values are those of the branchy form bit for bit.
   __device__ __forceinline__ void add(double v, bool welford) {
-    const bool ok = v == v;
+    const bool ok = win_ok(v);   // NaN and +-inf are missing (pandas' window ops); v is used only under ok
     nobs += ok ? 1 : 0;
     if (welford) {
       const double vn1 = vn + 1.0;
@@ -126,7 +126,7 @@ struct Moments {
     prev = ok ? v : prev;
   }
   __device__ __forceinline__ void remove(double v, bool welford) {
-    const bool ok = v == v;
+    const bool ok = win_ok(v);
     nobs -= ok ? 1 : 0;
     if (welford) {
       const double vn1 = vn - 1.0;
@@ -202,23 +202,23 @@ struct ReplayLane {
       if (v_in == v_in) weighted = v_in;
       return weighted;
     }
-    v_in = win_val(v_in);   // window operations: +-inf is missing
-    v_out = win_val(v_out);
+    // window operations: NaN and +-inf are missing (every use of v_in / v_out
+    // below is under its observation flag)
     if (EWM) {   // straight-line, as Moments (selects, the same values)
       const double alpha = A.alpha, om = 1.0 - alpha;
-      const bool obs = v_in == v_in;
+      const bool obs = win_ok(v_in);
       const bool wv = weighted == weighted;
       const double ow = wv ? old_wt * om : old_wt;
       const double nw = (ow * weighted + alpha * v_in) / (ow + alpha);
       double w2 = (wv && obs && weighted != v_in) ? nw : weighted;
       w2 = (!wv && obs) ? v_in : w2;
       const bool first = !steady && t == 0;
-      weighted = first ? v_in : w2;
+      weighted = first ? (obs ? v_in : qnan()) : w2;
       old_wt = first ? old_wt : ((wv && obs) ? 1.0 : ow);
       nobs = first ? (obs ? 1 : 0) : nobs + (obs ? 1 : 0);
       return nobs >= A.minp ? weighted : qnan();
     }
-    if (!steady && t == 0) m.init(v_in);   // pandas: prev_value = first value of the series
+    if (!steady && t == 0) m.init(win_val(v_in));   // pandas: prev_value = first value of the series
     if (steady || (t >= A.win && t - A.shift - A.win >= 0)) m.remove(v_out, welford);
     m.add(v_in, welford);
     return m.result(A.mode, A.minp, welford);
@@ -728,12 +728,12 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
 #pragma unroll
       for (int j = 0; j < SL_C; j += 2) {
         const dbl2u p = *reinterpret_cast<const dbl2u*>(x + i0 + j);
-        v[j] = win_val(p.x);
-        v[j + 1] = win_val(p.y);
+        v[j] = p.x;
+        v[j + 1] = p.y;
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? win_val(x[i0 + j]) : qnan();
+      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
     }
   };
   // Placeholders split so the wanted rank sits in a FIXED slot: with n
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
       load_chunk(t0 + c * SL_C, v);
 #pragma unroll
       for (int j = 0; j < SL_C; ++j) {
-        const bool num = t0 + c * SL_C + j >= t_start && v[j] == v[j];
+        const bool num = t0 + c * SL_C + j >= t_start && win_ok(v[j]);   // +-inf: missing (window op)
         n += num ? 1 : 0;
         const double a = num ? v[j] + 0.0 : inf;
 #pragma unroll
@@ -795,8 +795,8 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
     for (int j = 0; j < SL_C; ++j) {
       const int t = tc + j;
       const bool has_out = t - W >= t_start;   // else a placeholder leaves
-      const bool in_num = t < t_end && vin[j] == vin[j];
-      const bool out_num = t < t_end && has_out && vout[j] == vout[j];
+      const bool in_num = t < t_end && win_ok(vin[j]);   // NaN and +-inf are missing (window op)
+      const bool out_num = t < t_end && has_out && win_ok(vout[j]);
       const int n2 = n + (in_num ? 1 : 0) - (out_num ? 1 : 0);
       const int nb2 = b_of(n2);
       // a leaving placeholder is a bottom one when B drops, an entering one a

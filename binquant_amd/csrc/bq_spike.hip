@@ -84,8 +84,8 @@ __device__ __forceinline__ double sp_window(int t, int w, F f) {
   int n = 0;
   unsigned sor = 0u, sand = 1u;
   for (int j = -w + 1; j <= 0; ++j) {
-    const double v = win_val(f(j));   // +-inf is missing (pandas' window ops)
-    const bool ok = v == v;
+    const double v = f(j);
+    const bool ok = win_ok(v);   // NaN and +-inf are missing (pandas' window ops)
     const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
     s += ok ? v : 0.0;
     n += ok;
@@ -125,8 +125,7 @@ struct SpAgg {
     sand = 1u;
   }
   __device__ __forceinline__ void add(double v) {
-    v = win_val(v);   // +-inf is missing (pandas' window ops)
-    const bool ok = v == v;
+    const bool ok = win_ok(v);   // NaN and +-inf are missing (pandas' window ops); v only under ok
     const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
     s += ok ? v : 0.0;
     n += ok;

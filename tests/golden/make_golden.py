@@ -33,6 +33,9 @@ Fixtures:
                         (tests/test_coinrule_price_tracker.py:148-189) behind its
                         Indicators.mfi pins (:226-248) and the docstring's RSI < 30 /
                         MACD < 0 claim for the oversold frame
+  inf_windows.npz       the burst / pump / spike frames of 6 x 700 candles whose rolling
+                        windows meet +-inf (long zero-volume halts, zero closes), every
+                        column at every candle (pandas' window ops skip infinities)
   leadership.npz        GradualGainerRetest._leadership_allows on every prefix frame
                         (strategies/gradual_gainer_retest.py:131-196): the reference
                         test's make_frames + a 20 x 360 panel with BTC gaps
@@ -44,7 +47,7 @@ Fixtures:
                         helpers; outputs recorded at 48 sampled positions per symbol
                         (panel_gen.sample_positions: last rows, tile boundary, random)
 
-Usage: python tests/golden/make_golden.py [--only pins,panel,leadership]
+Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf]
 """
 
 from __future__ import annotations
@@ -161,6 +164,8 @@ def child(out_dir: Path, only: set[str] | None = None) -> None:
             strategy_panel(out_dir)
         if "leadership" in only:
             leadership(out_dir)
+        if "inf" in only:
+            inf_windows(out_dir)
         return
     import numpy as np
     import pandas as pd
@@ -574,6 +579,78 @@ def strategy_panel(out_dir: Path) -> None:
     out["tg_keys"] = np.array(tg_keys)
     out["feature_columns"] = np.array(feat_cols)
     np.savez_compressed(out_dir / "strategy_panel.npz", **out)
+
+
+def inf_windows(out_dir: Path) -> None:
+    """inf_windows.npz: the three strategy frames on 6 symbols x 700 candles
+    built so that their rolling windows meet +-inf — halts of 30-60 zero-volume
+    bars (relative_volume = v / 0 = inf once the volume mean's window is all
+    zero, then inside the 48-bar score / volume quantiles), zero closes (the
+    pct changes after them are inf, inside the spike pass's sums and the
+    quantile of |pct change|) — every output column at every candle:
+      lsp__*  LiquidationSweepPump.compute_pump_score (liquidation_sweep_pump.py:195-269)
+      abp__*  ActivityBurstPump.compute_indicators (activity_burst_pump.py:51-158)
+      fsf__*  FailedSpikeFade.detect (failed_spike_fade.py:258-544)
+    Inputs are stored beside them (open / high / low / close / volume / qv)."""
+    from types import SimpleNamespace
+
+    import numpy as np
+    import pandas as pd
+
+    from strategies.activity_burst_pump import ActivityBurstPump
+    from strategies.failed_spike_fade import FailedSpikeFade
+    from strategies.liquidation_sweep_pump import LiquidationSweepPump
+
+    S, T = 6, 700
+    g = np.random.default_rng(2024)
+    P = {k: np.zeros((S, T)) for k in ("open", "high", "low", "close", "volume", "qv")}
+    for s in range(S):
+        c = 10.0 * (s + 1) * np.exp(np.cumsum(g.normal(0.0, 0.006, T)))
+        v = g.lognormal(3.0, 1.0, T)
+        o = np.r_[c[0], c[:-1]]
+        h = np.maximum(o, c) * (1.0 + g.uniform(0.0, 0.003, T))
+        l = np.minimum(o, c) * (1.0 - g.uniform(0.0, 0.003, T))
+        for a, n in ((120 + 40 * s, 30 + 6 * s), (420, 45)):   # halts: flat bars, no volume
+            c[a : a + n] = c[a]
+            o[a : a + n] = h[a : a + n] = l[a : a + n] = c[a]
+            v[a : a + n] = 0.0
+        if s % 2 == 0:   # a zero close (and bar) -> inf pct changes after it
+            z = 300 + 10 * s
+            o[z] = h[z] = l[z] = c[z] = 0.0
+        P["open"][s], P["high"][s], P["low"][s], P["close"][s], P["volume"][s] = o, h, l, c, v
+        P["qv"][s] = v * c
+    out = {k: v for k, v in P.items()}
+    open_time = 1_700_000_000_000 + 900_000 * np.arange(T, dtype=np.int64)
+    bc = 60000.0 * np.exp(np.cumsum(g.normal(0.0, 0.004, T)))
+    out["btc_close"] = bc
+    dfb = pd.DataFrame({"open_time": open_time, "close": bc})
+    ctx_ns = SimpleNamespace(config=SimpleNamespace(env="test"), symbol="TESTUSDT", kucoin_symbol="TEST-USDT",
+                             exchange=None, binbot_api=None, telegram_consumer=None, market_type=None,
+                             at_consumer=None, _breadth_cross_tolerance=0.05, _autotrade_stress_threshold=0.35,
+                             current_symbol_data=None, price_precision=8, qty_precision=8)
+    abp = ActivityBurstPump(ctx_ns)
+    lsp = object.__new__(LiquidationSweepPump)
+    rec: dict[str, list] = {}
+    for s in range(S):
+        o, h, l, c, v, qv = (P[k][s] for k in ("open", "high", "low", "close", "volume", "qv"))
+        df = pd.DataFrame({"open": o, "high": h, "low": l, "close": c, "volume": v, "quote_asset_volume": qv})
+        for col, ser in abp.compute_indicators(df.copy()).items():
+            if col not in df.columns:
+                rec.setdefault(f"abp__{col}", [None] * S)[s] = np.asarray(ser, dtype=float)
+        dfl = pd.DataFrame({"open_time": open_time, "open": o, "high": h, "low": l, "close": c, "volume": v})
+        for col, ser in lsp.compute_pump_score(dfl, dfb).items():
+            if col not in dfl.columns:
+                rec.setdefault(f"lsp__{col}", [None] * S)[s] = np.asarray(ser, dtype=float)
+        ns = SimpleNamespace(symbol="TESTUSDT", market_type=None, df_15m=df.copy(), telegram_consumer=None,
+                             at_consumer=None, current_symbol_data=None, price_precision=8,
+                             market_breadth_data=None, strategy_cooldowns={}, strategy_states={})
+        fsf = FailedSpikeFade(ns)
+        for col, ser in fsf.detect().items():
+            if col not in df.columns:
+                rec.setdefault(f"fsf__{col}", [None] * S)[s] = np.asarray(ser, dtype=float)
+    for k, rows in rec.items():
+        out[k] = np.stack(rows)
+    np.savez_compressed(out_dir / "inf_windows.npz", **out)
 
 
 def leadership(out_dir: Path) -> None:
