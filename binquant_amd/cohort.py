@@ -23,9 +23,12 @@ all S symbols of the cohort in one call:
   FailedSpikeFade, TopGainerEarlyMomentum, GradualGainerRetest's leadership
   (:445-499).
 
-Every launch goes on the current stream and nothing reads back to the host,
-so the whole cohort can be captured once as a hipGraph
-(``graphs.CapturedPipeline(process_cohort, ...)``) and replayed per message.
+Nothing reads back to the host, so the whole cohort can be captured once
+as a hipGraph (``graphs.CapturedPipeline(process_cohort, ...)``) and
+replayed per message; captured, the stages run as four concurrent branches
+of the graph (the current stream and three side streams forked from it and
+joined before the return; eager calls stay on one stream, see
+_COHORT_STREAMS).
 Frames share one geometry per call: [S, T5] 5m and [S, T15] 15m panels, the
 BTC 15m close index-aligned with the 15m panel (a cohort closes on the same
 15-minute grid); the 1h resample's bin count is fixed by T15.
@@ -40,6 +43,25 @@ from . import engine, signals, strategies
 RESAMPLE_AGG = {"open": "first", "high": "max", "low": "min", "close": "last", "volume": "sum"}
 HOUR_MS = 3_600_000
 
+# The stages read only the cohort's inputs, so they can run as four
+# concurrent branches (the current stream + three side streams forked from it
+# and joined back before the return; captured, the joins become graph
+# edges). At live shapes most stages are a few hundred waves — a quarter of
+# the chip — so overlapping them is what is left to gain on the device:
+# 1000 x 400 as a graph 1.03 -> 0.70 ms. Eager calls are bound by the host's
+# launches, which the stream switches and record_stream calls lengthen (2.62
+# -> 3.66 ms), so by default ("capture") the branches are used only while a
+# graph is being captured; True: always, False: never.
+_COHORT_STREAMS: bool | str = "capture"
+_SIDE: dict[int, list[torch.cuda.Stream]] = {}
+
+
+def _side_streams(device: torch.device, n: int) -> list[torch.cuda.Stream]:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _SIDE:
+        _SIDE[idx] = [torch.cuda.Stream(device=idx) for _ in range(n)]
+    return _SIDE[idx][:n]
+
 
 def process_cohort(o5, h5, l5, c5, v5, o15, h15, l15, c15, v15, ts15, btc_ts15, btc_c15,
                    max_bars: int = 400, exact: bool = True) -> dict[str, torch.Tensor]:
@@ -49,40 +71,77 @@ def process_cohort(o5, h5, l5, c5, v5, o15, h15, l15, c15, v15, ts15, btc_ts15, 
     pipelines' bit-exact replays (the live path); False their panel mode.
     Returns a flat dict of tensors (names prefixed by the stage)."""
     S, T15 = c15.shape
-    out: dict[str, torch.Tensor] = {}
-    # ---- 5m frame (:364-388)
-    for k, v in engine.enrich(o5, h5, l5, c5, v5).items():
-        out[f"e5.{k}"] = v
-    for k, v in strategies.activity_burst_features(o5, h5, l5, c5, v5, v5 * c5).items():
-        out[f"burst.{k}"] = v
-    # ---- 15m frame (:402-432)
-    for k, v in engine.enrich(o15, h15, l15, c15, v15).items():
-        out[f"e15.{k}"] = v
-    bins, res, nbins = engine.resample(ts15, {"open": o15, "high": h15, "low": l15, "close": c15, "volume": v15},
-                                       RESAMPLE_AGG, HOUR_MS, max_bins=T15 // 4 + 2)
-    out["h1.open_time"] = bins
-    out["h1.bins"] = nbins
-    for k, v in res.items():
-        out[f"h1.{k}"] = v
-    bc = engine.beta_corr(c15, btc_c15, 50)
-    out["btc.beta"], out["btc.corr"] = bc["beta"][:, -1], bc["corr"][:, -1]
-    out["btc.change_24h"] = ((btc_c15[-1] / btc_c15[-97] - 1.0) * 100.0).reshape(1) if T15 > 96 else \
-        torch.full((1,), float("nan"), dtype=torch.float64, device=c15.device)
-    # ---- context refresh at the cohort's close (klines_provider.py:181-199)
-    part, last = engine.context_partials(h15, l15, c15, max_bars=max_bars, last=True)
-    out["context.partial"] = part
-    for k, v in last.items():
-        out[f"context.{k}"] = v
-    # ---- 15m strategies (:445-499)
     btc_c = btc_c15.reshape(-1)
-    for k, v in strategies.pump_score_features(o15, h15, l15, c15, v15, btc_c, exact=exact).items():
-        out[f"pump.{k}"] = v
-    for k, v in strategies.failed_spike_features(o15, h15, l15, c15, v15, v15 * c15, exact=exact).items():
-        out[f"spike.{k}"] = v
-    top, status = signals.top_gainer_features(o15, h15, l15, c15, v15, v15 * c15)
-    for k, v in top.items():
-        out[f"top.{k}"] = v
-    out["top.status"] = status
-    for k, v in signals.gradual_gainer_leadership(ts15, c15, btc_ts15, btc_c).items():
-        out[f"lead.{k}"] = v
+
+    def frame_5m(out):   # :364-388
+        for k, v in engine.enrich(o5, h5, l5, c5, v5).items():
+            out[f"e5.{k}"] = v
+        for k, v in strategies.activity_burst_features(o5, h5, l5, c5, v5, v5 * c5).items():
+            out[f"burst.{k}"] = v
+
+    def frame_15m(out):   # :402-432
+        for k, v in engine.enrich(o15, h15, l15, c15, v15).items():
+            out[f"e15.{k}"] = v
+        bins, res, nbins = engine.resample(ts15, {"open": o15, "high": h15, "low": l15, "close": c15,
+                                                  "volume": v15}, RESAMPLE_AGG, HOUR_MS, max_bins=T15 // 4 + 2)
+        out["h1.open_time"] = bins
+        out["h1.bins"] = nbins
+        for k, v in res.items():
+            out[f"h1.{k}"] = v
+        bc = engine.beta_corr(c15, btc_c15, 50)
+        out["btc.beta"], out["btc.corr"] = bc["beta"][:, -1], bc["corr"][:, -1]
+        out["btc.change_24h"] = ((btc_c15[-1] / btc_c15[-97] - 1.0) * 100.0).reshape(1) if T15 > 96 else \
+            torch.full((1,), float("nan"), dtype=torch.float64, device=c15.device)
+
+    def context(out):   # klines_provider.py:181-199
+        part, last = engine.context_partials(h15, l15, c15, max_bars=max_bars, last=True)
+        out["context.partial"] = part
+        for k, v in last.items():
+            out[f"context.{k}"] = v
+
+    def pump(out):   # :445-499
+        for k, v in strategies.pump_score_features(o15, h15, l15, c15, v15, btc_c, exact=exact).items():
+            out[f"pump.{k}"] = v
+
+    def spike(out):
+        for k, v in strategies.failed_spike_features(o15, h15, l15, c15, v15, v15 * c15, exact=exact).items():
+            out[f"spike.{k}"] = v
+
+    def top(out):
+        feats, status = signals.top_gainer_features(o15, h15, l15, c15, v15, v15 * c15)
+        for k, v in feats.items():
+            out[f"top.{k}"] = v
+        out["top.status"] = status
+
+    def lead(out):
+        for k, v in signals.gradual_gainer_leadership(ts15, c15, btc_ts15, btc_c).items():
+            out[f"lead.{k}"] = v
+
+    order = (frame_5m, frame_15m, context, pump, spike, top, lead)
+    parts = {f: {} for f in order}
+    branches = _COHORT_STREAMS is True or (_COHORT_STREAMS == "capture"
+                                            and torch.cuda.is_current_stream_capturing())
+    if not branches:
+        for f in order:
+            f(parts[f])
+    else:
+        main = torch.cuda.current_stream(c15.device)
+        sides = _side_streams(c15.device, 3)
+        groups = ((main, (frame_5m, lead)), (sides[0], (frame_15m, context)), (sides[1], (pump, top)),
+                  (sides[2], (spike,)))
+        for st in sides:
+            st.wait_stream(main)
+        for st, fs in groups:
+            with torch.cuda.stream(st):
+                for f in fs:
+                    f(parts[f])
+        for st in sides:
+            main.wait_stream(st)
+        for st, fs in groups[1:]:   # outputs made on a side stream are used on the caller's
+            for f in fs:
+                for v in parts[f].values():
+                    v.record_stream(main)
+    out: dict[str, torch.Tensor] = {}
+    for f in order:
+        out.update(parts[f])
     return out

@@ -68,3 +68,30 @@ def test_cohort_graph_replays_bit_exact(cuda):
             n = int(want["h1.bins"].max())
             x, y = x[..., :n] if x.ndim == 2 else x, y[..., :n] if y.ndim == 2 else y
         np.testing.assert_array_equal(x, y, err_msg=k)
+
+
+def test_cohort_branches_equal_one_stream(cuda, monkeypatch):
+    """The four concurrent branches (side streams forked from and joined to
+    the caller's stream) give the one-stream outputs bit for bit, eager and
+    as a replayed graph, and the caller's stream sees finished outputs."""
+    from binquant_amd import cohort
+    from binquant_amd.graphs import CapturedPipeline
+
+    S, T = 96, 400
+    a, b = _inputs(S, T, 21), _inputs(S, T, 22)
+    monkeypatch.setattr(cohort, "_COHORT_STREAMS", False)
+    one = {k: v.clone() for k, v in cohort.process_cohort(*b).items()}
+    monkeypatch.setattr(cohort, "_COHORT_STREAMS", True)
+    many = cohort.process_cohort(*b)
+    monkeypatch.setattr(cohort, "_COHORT_STREAMS", "capture")   # the default: branches inside the capture only
+    g = CapturedPipeline(cohort.process_cohort, *a)
+    rep = g(*b)
+    torch.cuda.synchronize()
+    assert list(many) == list(one)
+    n = int(one["h1.bins"].max())
+    for k in one:
+        for name, got in (("eager", many[k]), ("graph", rep[k])):
+            x, y = got.cpu().numpy(), one[k].cpu().numpy()
+            if k.startswith("h1.") and x.ndim == 2:
+                x, y = x[:, :n], y[:, :n]
+            np.testing.assert_array_equal(x, y, err_msg=f"{name} {k}")
