@@ -71,6 +71,8 @@ struct ResampleArgs {
   int T, nf;
 };
 
+constexpr int RS_FULL = 4;   // candles of a full bin on the reference's 15m -> 1h resample
+
 // one thread per (symbol, output bin); consecutive threads take consecutive
 // bins of a row, so the candles a wave reads are contiguous
 __global__ __launch_bounds__(256) void resample_kernel(const ResampleArgs A) {
@@ -89,6 +91,53 @@ __global__ __launch_bounds__(256) void resample_kernel(const ResampleArgs A) {
   const int lo = lower_bound_guess(ts, n, key, t0v, step);
   const int hi = lower_bound_guess(ts, n, key + A.I, t0v, step);
   if (A.out_ts) A.out_ts[s * A.ld_out + b] = key;
+  if (hi - lo == RS_FULL) {
+    // a full bin (every candle of the interval present, the common case): the
+    // fields' values are loaded together, then aggregated with selects in the
+    // same order and with the same NaN rules as the walks below (one round
+    // trip to memory instead of one per field and candle)
+    for (int f = 0; f < A.nf; ++f) {
+      const double* __restrict__ x = A.in[f] + s * A.ld_in + lo;
+      double v[RS_FULL];
+#pragma unroll
+      for (int j = 0; j < RS_FULL; ++j) v[j] = x[j];
+      double r = qnan();
+      switch (A.agg[f]) {
+        case BQ_AGG_FIRST:
+#pragma unroll
+          for (int j = RS_FULL - 1; j >= 0; --j) r = v[j] == v[j] ? v[j] : r;
+          break;
+        case BQ_AGG_LAST:
+#pragma unroll
+          for (int j = 0; j < RS_FULL; ++j) r = v[j] == v[j] ? v[j] : r;
+          break;
+        case BQ_AGG_MAX:
+#pragma unroll
+          for (int j = 0; j < RS_FULL; ++j) r = (v[j] == v[j] && (r != r || v[j] > r)) ? v[j] : r;
+          break;
+        case BQ_AGG_MIN:
+#pragma unroll
+          for (int j = 0; j < RS_FULL; ++j) r = (v[j] == v[j] && (r != r || v[j] < r)) ? v[j] : r;
+          break;
+        default: {   // BQ_AGG_SUM: pandas group_sum (Kahan)
+          double sum = 0.0, comp = 0.0;
+#pragma unroll
+          for (int j = 0; j < RS_FULL; ++j) {
+            const bool ok = v[j] == v[j];
+            const double y = v[j] - comp;
+            const double t = sum + y;
+            double c2 = t - sum - y;
+            c2 = c2 != c2 ? 0.0 : c2;
+            comp = ok ? c2 : comp;
+            sum = ok ? t : sum;
+          }
+          r = sum;
+        }
+      }
+      A.out[f][s * A.ld_out + b] = r;
+    }
+    return;
+  }
   for (int f = 0; f < A.nf; ++f) {
     const double* __restrict__ x = A.in[f] + s * A.ld_in;
     double r;
