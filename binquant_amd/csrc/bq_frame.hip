@@ -277,6 +277,99 @@ __global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __re
   if (tid == 0) out_lens[s] = sBase;
 }
 
+// The same join for rows of up to JR_NT * K candles with the whole row in
+// registers (candle t = k * JR_NT + tid: every load instruction of a wave is
+// one contiguous 512-byte span): every row's loads go out together — closes
+// and times, then the benchmark times at the guessed index, then the
+// benchmark closes — three dependent round trips per row instead of three
+// per 256-candle tile; the kept values are placed from the waves' ballots of
+// each k (one barrier), in the same order and with the same values as the
+// tiled kernel.
+template <int K>
+__global__ __launch_bounds__(JR_NT) void join_returns_row_kernel(const int64_t* __restrict__ ts,
+                                                                 const double* __restrict__ close,
+                                                                 const int64_t* __restrict__ lens, int T, int64_t ld_in,
+                                                                 const int64_t* __restrict__ bts,
+                                                                 const double* __restrict__ bclose, int nb,
+                                                                 double* __restrict__ x, double* __restrict__ y,
+                                                                 int64_t ld_out, int64_t* __restrict__ out_lens) {
+  constexpr int NW = JR_NT / WAVE;
+  __shared__ int sCnt[K][NW];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const int64_t s = blockIdx.x;
+  const int64_t* __restrict__ rts = ts + s * ld_in;
+  const double* __restrict__ rc = close + s * ld_in;
+  const int n = row_len(lens, s, T);
+  const int j0 = n > 0 ? match_last(bts, nb, rts[0]) : -1;
+  const int off = j0 >= 0 ? j0 : 0;
+  double c[K], cp[K];
+  int64_t key[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int t = k * JR_NT + tid;
+    c[k] = t < n ? rc[t] : qnan();
+    cp[k] = t >= 1 && t <= n ? rc[t - 1] : qnan();
+    key[k] = t < n ? rts[t] : 0;
+  }
+  // the benchmark row at the guessed index (index-aligned frames), both
+  // neighbours for the keep-last check; the binary search only where it misses
+  int64_t g0[K], g1[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int g = k * JR_NT + tid + off;
+    g0[k] = g < nb ? bts[g] : INT64_MIN;
+    g1[k] = g + 1 < nb ? bts[g + 1] : INT64_MIN;
+  }
+  int j[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int t = k * JR_NT + tid, g = t + off;
+    const bool live = t > 0 && t < n;
+    const bool hit = g < nb && g0[k] == key[k] && (g + 1 >= nb || g1[k] != key[k]);
+    j[k] = !live ? -1 : (hit ? g : -2);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (j[k] == -2) j[k] = match_last(bts, nb, key[k]);   // off-grid candles (rare)
+  double b0[K], b1[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    b0[k] = j[k] > 0 ? bclose[j[k]] : qnan();
+    b1[k] = j[k] > 0 ? bclose[j[k] - 1] : qnan();
+  }
+  double xa[K], yb[K];
+  uint64_t m[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    xa[k] = yb[k] = qnan();
+    if (j[k] > 0) {   // t in (0, n) with a benchmark row before it
+      xa[k] = log_return(c[k], cp[k]);   // the frame's own previous row
+      yb[k] = log_return(b0[k], b1[k]);
+    }
+    m[k] = __ballot(xa[k] == xa[k] && yb[k] == yb[k]);
+    if (lane == 0) sCnt[k][w] = __popcll(m[k]);
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int before = base;
+    for (int u = 0; u < w; ++u) before += sCnt[k][u];
+    for (int u = 0; u < NW; ++u) base += sCnt[k][u];
+    if ((m[k] >> lane) & 1ull) {
+      const int pos = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0));
+      x[s * ld_out + pos] = xa[k];
+      y[s * ld_out + pos] = yb[k];
+    }
+  }
+  for (int t = base + tid; t < T; t += JR_NT) {   // NaN tail: a dropna'd series of length out_lens[s]
+    x[s * ld_out + t] = qnan();
+    y[s * ld_out + t] = qnan();
+  }
+  if (tid == 0) out_lens[s] = base;
+}
+
 }  // namespace bq
 
 extern "C" {
@@ -341,8 +434,16 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
       ld_out < T || n_bench < 0 || T > 0x7fffffff || n_bench > 0x7fffffff)
     return BQ_EINVAL;
   if (S == 0) return BQ_OK;
-  hipLaunchKernelGGL(join_returns_kernel, dim3((unsigned)S), dim3(JR_NT), 0, (hipStream_t)stream, ts, close, lens,
-                     (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  const hipStream_t st = (hipStream_t)stream;
+  if (T <= JR_NT * 8)
+    hipLaunchKernelGGL(join_returns_row_kernel<8>, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T,
+                       ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  else if (T <= JR_NT * 16)
+    hipLaunchKernelGGL(join_returns_row_kernel<16>, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T,
+                       ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  else
+    hipLaunchKernelGGL(join_returns_kernel, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T, ld_in,
+                       bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
