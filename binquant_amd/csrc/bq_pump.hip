@@ -27,7 +27,7 @@
 // ffilled close, momentum_3, pump_score ...): ~2.4x its algorithmic bytes.
 //
 // Mapping (as bq_enrich): one 256-thread workgroup per symbol walks its row in
-// tiles of 1024 candles (4 per lane, the next tile's loads in flight); an LDS
+// tiles of 1024 candles (4 per lane, 3 workgroups per CU); an LDS
 // ring with a 32-candle halo holds high, low, close, volume, the ffilled
 // close and the volume's run starts (the same-value rule), so every window
 // reads the ring and every input byte crosses HBM once. Outputs leave through
@@ -95,7 +95,10 @@ __device__ __forceinline__ double clip0(double x) { return x < 0.0 ? 0.0 : x; }
 __device__ __forceinline__ double rep0(double x) { return x == 0.0 ? qnan() : x; }
 
 template <bool EWM_IN>
-__global__ __launch_bounds__(PF_NT) void pump_features_kernel(const PumpArgs A, int vin, int vout) {
+// 3 workgroups per CU for the default pass (168 VGPRs, 8 B of spill): its
+// inputs are loaded at the tile start instead of a tile ahead (the prefetch's
+// 32 registers cost a workgroup per CU) — a18 1.91-2.01 -> 1.86-1.87 ms (A/B)
+__global__ __launch_bounds__(PF_NT, EWM_IN ? 2 : 3) void pump_features_kernel(const PumpArgs A, int vin, int vout) {
   __shared__ double sH[PF_R], sL[PF_R], sC[PF_R], sV[PF_R], sF[PF_R];
   __shared__ double sEB[EWM_IN ? 3 : 1][PF_NW];   // the waves' scan totals
   __shared__ double sEC[EWM_IN ? 3 : 1];          // the ewm values at the previous tile's last candle
@@ -136,30 +139,21 @@ __global__ __launch_bounds__(PF_NT) void pump_features_kernel(const PumpArgs A, 
       snobs[e] = 0;
     }
   }
-  // high, low, close, volume: the next tile in flight; the ewm columns (read
-  // in phase C only) are loaded at the start of their own tile
+  // high, low, close, volume and the ewm columns: loaded at the start of
+  // their own tile (no prefetch: see the launch bounds)
   constexpr int NP = PF_V_IN + 1;
-  double nx[NP][PF_K];
-#pragma unroll
-  for (int f = 0; f < NP; ++f) pf_load(A.in[f] + irow, PF_K * tid, T, vin, nx[f]);
 
   for (int t0 = 0; t0 < T; t0 += PF_TT) {
     const int tb = t0 + PF_K * tid, pb = PF_H + PF_K * tid;
     double x[NP][PF_K], atr[PF_K], e20[PF_K], e50[PF_K], ewy[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int f = 0; f < NP; ++f)
-#pragma unroll
-      for (int k = 0; k < PF_K; ++k) x[f][k] = nx[f][k];
+    for (int f = 0; f < NP; ++f) pf_load(A.in[f] + irow, tb, T, vin, x[f]);
     if (!EWM_IN) {
       pf_load(A.in[PF_ATR_IN] + irow, tb, T, vin, atr);
       pf_load(A.in[PF_E20_IN] + irow, tb, T, vin, e20);
       pf_load(A.in[PF_E50_IN] + irow, tb, T, vin, e50);
     }
     const double pv0 = tb >= 1 && tb <= T ? A.in[PF_V_IN][irow + tb - 1] : qnan();
-    if (t0 + PF_TT < T) {
-#pragma unroll
-      for (int f = 0; f < NP; ++f) pf_load(A.in[f] + irow, tb + PF_TT, T, vin, nx[f]);
-    }
     // ---- phase A: ring, run starts of the volume, last valid close (and the
     // ewm series' lane maps / wave scans)
     int lrv[PF_K], lvc[PF_K];
