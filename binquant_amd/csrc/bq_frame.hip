@@ -219,9 +219,119 @@ __global__ __launch_bounds__(256) void align_kernel(const int64_t* __restrict__ 
   out[s * ld_out + t] = r;
 }
 
-// One workgroup per symbol row: keep flag per candle, block-wide exclusive
-// scan (wave ballots + LDS wave offsets), scatter the kept pairs in order.
+// The inner join of the two return frames on open_time
+// (context_evaluator.py:171-175: df_15m[["returns"]].join(df_btc_15m["returns"],
+// how="inner") then dropna): a candle whose time the benchmark holds k times
+// joins k rows, in the benchmark's order (pandas' many-to-one join), each
+// with its own benchmark return (log of its close over the row before it).
+// [jf, jl]: the benchmark rows with this time (jf > jl: none). guess: the
+// expected index on an index-aligned grid; a unique hit costs the three
+// neighbouring loads the caller made, anything else two binary searches.
+__device__ __forceinline__ void jr_range(const int64_t* __restrict__ bts, int nb, int64_t key, int g, int64_t gm,
+                                         int64_t g0, int64_t g1, int& jf, int& jl) {
+  if (g >= 0 && g < nb && g0 == key && (g == 0 || gm != key) && (g + 1 >= nb || g1 != key)) {
+    jf = jl = g;
+    return;
+  }
+  jf = lower_bound_i64(bts, nb, key);
+  jl = lower_bound_i64(bts, nb, key + 1) - 1;
+}
+
+// inclusive wave sum of an int (shfl ladder)
+__device__ __forceinline__ int jr_wave_incl(int v, int lane) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int u = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+// the joined pairs of one candle, written from position pos (pairs past
+// ld_out dropped: the row's count is capped at ld_out by the caller)
+__device__ __forceinline__ void jr_write(const double* __restrict__ bclose, double xa, int jf, int jl, int pos,
+                                         int64_t ld_out, double* __restrict__ xr, double* __restrict__ yr) {
+  for (int j = jf; j <= jl; ++j) {
+    const double yb = j > 0 ? log_return(bclose[j], bclose[j - 1]) : qnan();
+    if (yb == yb) {
+      if (pos < ld_out) {
+        xr[pos] = xa;
+        yr[pos] = yb;
+      }
+      ++pos;
+    }
+  }
+}
+
+__device__ __forceinline__ int jr_count(const double* __restrict__ bclose, double xa, int jf, int jl) {
+  if (!(xa == xa)) return 0;
+  int c = 0;
+  for (int j = jf; j <= jl; ++j) c += (j > 0 && log_return(bclose[j], bclose[j - 1]) == log_return(bclose[j], bclose[j - 1])) ? 1 : 0;
+  return c;
+}
+
+// One workgroup per symbol row, 256-candle tiles: pair count per candle,
+// block-wide exclusive scan (wave shfl scans + LDS wave offsets), the pairs
+// written in order.
 constexpr int JR_NT = 256;
+#ifndef JR_ROW_NT
+#define JR_ROW_NT 512   // whole-row kernel block (4 / 8 candles per thread)
+#endif
+
+template <int NT>
+__device__ __forceinline__ void jr_row_tiled(int64_t s, const int64_t* __restrict__ ts,
+                                             const double* __restrict__ close, const int64_t* __restrict__ lens,
+                                             int T, int64_t ld_in, const int64_t* __restrict__ bts,
+                                             const double* __restrict__ bclose, int nb, double* __restrict__ x,
+                                             double* __restrict__ y, int64_t ld_out, int64_t* __restrict__ out_lens) {
+  __shared__ int sWave[NT / WAVE];
+  __shared__ int sBase;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const int64_t* __restrict__ rts = ts + s * ld_in;
+  const double* __restrict__ rc = close + s * ld_in;
+  double* __restrict__ xr = x + s * ld_out;
+  double* __restrict__ yr = y + s * ld_out;
+  const int n = row_len(lens, s, T);
+  // the row's offset into the benchmark's index, from its first candle
+  const int j0 = n > 0 ? lower_bound_i64(bts, nb, rts[0]) : 0;
+  const int guess_off = j0 < nb && n > 0 && bts[j0] == rts[0] ? j0 : 0;
+  if (tid == 0) sBase = 0;
+  __syncthreads();
+  for (int t0 = 0; t0 < n; t0 += NT) {
+    const int t = t0 + tid;
+    double xa = qnan();
+    int jf = 0, jl = -1;
+    if (t < n && t > 0) {
+      xa = log_return(rc[t], rc[t - 1]);   // the frame's own previous row
+      const int64_t key = rts[t];
+      const int g = t + guess_off;
+      jr_range(bts, nb, key, g, g >= 1 && g - 1 < nb ? bts[g - 1] : INT64_MIN, g < nb ? bts[g] : INT64_MIN,
+               g + 1 < nb ? bts[g + 1] : INT64_MIN, jf, jl);
+    }
+    const int c = jr_count(bclose, xa, jf, jl);
+    const int inc = jr_wave_incl(c, lane);
+    if (lane == WAVE - 1) sWave[w] = inc;
+    __syncthreads();
+    int off = sBase + inc - c;
+    for (int k = 0; k < w; ++k) off += sWave[k];
+    if (c) jr_write(bclose, xa, jf, jl, off, ld_out, xr, yr);
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int k = 0; k < NT / WAVE; ++k) tot += sWave[k];
+      sBase += tot;
+    }
+    __syncthreads();
+  }
+  const int total = sBase < ld_out ? sBase : (int)ld_out;
+  // NaN tail so the row reads as a dropna'd series of length out_lens[s]
+  for (int t = total + tid; t < T; t += NT) {
+    xr[t] = qnan();
+    yr[t] = qnan();
+  }
+  if (tid == 0) out_lens[s] = total;
+}
+
 
 __global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __restrict__ ts,
                                                              const double* __restrict__ close,
@@ -230,107 +340,94 @@ __global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __re
                                                              const double* __restrict__ bclose, int nb,
                                                              double* __restrict__ x, double* __restrict__ y,
                                                              int64_t ld_out, int64_t* __restrict__ out_lens) {
-  __shared__ int sWave[JR_NT / WAVE];
-  __shared__ int sBase;
-  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
-  const int64_t s = blockIdx.x;
-  const int64_t* __restrict__ rts = ts + s * ld_in;
-  const double* __restrict__ rc = close + s * ld_in;
-  const int n = row_len(lens, s, T);
-  // the row's offset into the benchmark's index, from its first candle
-  const int j0 = n > 0 ? match_last(bts, nb, rts[0]) : -1;
-  const int guess_off = j0 >= 0 ? j0 : 0;
-  if (tid == 0) sBase = 0;
-  __syncthreads();
-  for (int t0 = 0; t0 < n; t0 += JR_NT) {
-    const int t = t0 + tid;
-    double xa = qnan(), yb = qnan();
-    if (t < n && t > 0) {
-      xa = log_return(rc[t], rc[t - 1]);   // the frame's own previous row
-      const int j = match_last_near(bts, nb, rts[t], t + guess_off);
-      if (j > 0) yb = log_return(bclose[j], bclose[j - 1]);
-    }
-    const bool keep = xa == xa && yb == yb;
-    const uint64_t m = __ballot(keep);
-    const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-    if (lane == 0) sWave[w] = __popcll(m);
-    __syncthreads();
-    int off = sBase;
-    for (int k = 0; k < w; ++k) off += sWave[k];
-    if (keep) {
-      x[s * ld_out + off + before] = xa;
-      y[s * ld_out + off + before] = yb;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int tot = 0;
-      for (int k = 0; k < JR_NT / WAVE; ++k) tot += sWave[k];
-      sBase += tot;
-    }
-    __syncthreads();
+  jr_row_tiled<JR_NT>(blockIdx.x, ts, close, lens, T, ld_in, bts, bclose, nb, x, y, ld_out, out_lens);
+}
+
+// The rows the whole-row kernel handed back (out_lens[s] == -1: the benchmark
+// repeats a time the row joins or looks at), through the tiled join; a few
+// hundred workgroups stride over the rows, nearly all of which they skip.
+__global__ __launch_bounds__(JR_NT) void join_returns_fixup_kernel(const int64_t* __restrict__ ts,
+                                                                   const double* __restrict__ close,
+                                                                   const int64_t* __restrict__ lens, int T,
+                                                                   int64_t ld_in, const int64_t* __restrict__ bts,
+                                                                   const double* __restrict__ bclose, int nb,
+                                                                   double* __restrict__ x, double* __restrict__ y,
+                                                                   int64_t ld_out, int64_t* __restrict__ out_lens,
+                                                                   int64_t S) {
+  for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
+    if (out_lens[s] >= 0) continue;   // block-uniform
+    jr_row_tiled<JR_NT>(s, ts, close, lens, T, ld_in, bts, bclose, nb, x, y, ld_out, out_lens);
+    __syncthreads();   // sBase is reset by the next row
   }
-  // NaN tail so the row reads as a dropna'd series of length out_lens[s]
-  for (int t = sBase + tid; t < T; t += JR_NT) {
-    x[s * ld_out + t] = qnan();
-    y[s * ld_out + t] = qnan();
-  }
-  if (tid == 0) out_lens[s] = sBase;
 }
 
 // The same join for rows of up to JR_NT * K candles with the whole row in
 // registers (candle t = k * JR_NT + tid: every load instruction of a wave is
 // one contiguous 512-byte span): every row's loads go out together — closes
-// and times, then the benchmark times at the guessed index, then the
+// and times, then the benchmark times around the guessed index, then the
 // benchmark closes — three dependent round trips per row instead of three
-// per 256-candle tile; the kept values are placed from the waves' ballots of
-// each k (one barrier), in the same order and with the same values as the
-// tiled kernel.
-template <int K>
-__global__ __launch_bounds__(JR_NT) void join_returns_row_kernel(const int64_t* __restrict__ ts,
+// per 256-candle tile; the pairs are placed from per-k wave scans of the
+// pair counts (one barrier), in the same order and with the same values as
+// the tiled kernel.
+template <int NT, int K>
+__global__ __launch_bounds__(NT) void join_returns_row_kernel(const int64_t* __restrict__ ts,
                                                                  const double* __restrict__ close,
                                                                  const int64_t* __restrict__ lens, int T, int64_t ld_in,
                                                                  const int64_t* __restrict__ bts,
                                                                  const double* __restrict__ bclose, int nb,
                                                                  double* __restrict__ x, double* __restrict__ y,
                                                                  int64_t ld_out, int64_t* __restrict__ out_lens) {
-  constexpr int NW = JR_NT / WAVE;
+  constexpr int NW = NT / WAVE;
   __shared__ int sCnt[K][NW];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const int64_t s = blockIdx.x;
   const int64_t* __restrict__ rts = ts + s * ld_in;
   const double* __restrict__ rc = close + s * ld_in;
+  double* __restrict__ xr = x + s * ld_out;
+  double* __restrict__ yr = y + s * ld_out;
   const int n = row_len(lens, s, T);
-  const int j0 = n > 0 ? match_last(bts, nb, rts[0]) : -1;
-  const int off = j0 >= 0 ? j0 : 0;
+  const int j0 = n > 0 ? lower_bound_i64(bts, nb, rts[0]) : 0;
+  const int off = j0 < nb && n > 0 && bts[j0] == rts[0] ? j0 : 0;
   double c[K], cp[K];
   int64_t key[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int t = k * JR_NT + tid;
+    const int t = k * NT + tid;
     c[k] = t < n ? rc[t] : qnan();
     cp[k] = t >= 1 && t <= n ? rc[t - 1] : qnan();
     key[k] = t < n ? rts[t] : 0;
   }
-  // the benchmark row at the guessed index (index-aligned frames), both
-  // neighbours for the keep-last check; the binary search only where it misses
+  // the benchmark row at the guessed index (index-aligned frames) and the one
+  // after it: a guessed hit is the only row with its time unless the
+  // benchmark repeats a time inside the block's guessed span, which the same
+  // loads show (two equal neighbours); candles the guess misses take the two
+  // binary searches. A block with a repeated time anywhere it looks (dup) or
+  // a candle that joins several rows (multi) runs the tiled join instead.
   int64_t g0[K], g1[K];
+  bool odd = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int g = k * JR_NT + tid + off;
+    const int g = k * NT + tid + off;
     g0[k] = g < nb ? bts[g] : INT64_MIN;
     g1[k] = g + 1 < nb ? bts[g + 1] : INT64_MIN;
+    odd |= g + 1 < nb && g0[k] == g1[k];
   }
   int j[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const int t = k * JR_NT + tid, g = t + off;
+    const int t = k * NT + tid, g = t + off;
     const bool live = t > 0 && t < n;
     const bool hit = g < nb && g0[k] == key[k] && (g + 1 >= nb || g1[k] != key[k]);
     j[k] = !live ? -1 : (hit ? g : -2);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k)
-    if (j[k] == -2) j[k] = match_last(bts, nb, key[k]);   // off-grid candles (rare)
+    if (j[k] == -2) {   // off-grid candles (rare)
+      const int jf = lower_bound_i64(bts, nb, key[k]);
+      const bool found = jf < nb && bts[jf] == key[k];
+      odd |= found && jf + 1 < nb && bts[jf + 1] == key[k];   // several rows: the tiled join
+      j[k] = found ? jf : -1;
+    }
   double b0[K], b1[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -349,7 +446,16 @@ __global__ __launch_bounds__(JR_NT) void join_returns_row_kernel(const int64_t* 
     m[k] = __ballot(xa[k] == xa[k] && yb[k] == yb[k]);
     if (lane == 0) sCnt[k][w] = __popcll(m[k]);
   }
+  const bool odd_w = __ballot(odd) != 0;
+  if (lane == 0 && odd_w) sCnt[0][w] |= 1 << 30;   // rides on the count barrier
   __syncthreads();
+  bool odd_b = false;
+#pragma unroll
+  for (int u = 0; u < NW; ++u) odd_b |= (sCnt[0][u] >> 30) != 0;
+  if (odd_b) {   // the speculative pairs are dropped: join_returns_fixup_kernel's row
+    if (tid == 0) out_lens[s] = -1;
+    return;
+  }
   int base = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -359,15 +465,16 @@ __global__ __launch_bounds__(JR_NT) void join_returns_row_kernel(const int64_t* 
     if ((m[k] >> lane) & 1ull) {
       const int pos = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[k] >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m[k], 0));
-      x[s * ld_out + pos] = xa[k];
-      y[s * ld_out + pos] = yb[k];
+      xr[pos] = xa[k];
+      yr[pos] = yb[k];
     }
   }
-  for (int t = base + tid; t < T; t += JR_NT) {   // NaN tail: a dropna'd series of length out_lens[s]
-    x[s * ld_out + t] = qnan();
-    y[s * ld_out + t] = qnan();
+  const int total = base < ld_out ? base : (int)ld_out;
+  for (int t = total + tid; t < T; t += NT) {   // NaN tail: a dropna'd series of length out_lens[s]
+    xr[t] = qnan();
+    yr[t] = qnan();
   }
-  if (tid == 0) out_lens[s] = base;
+  if (tid == 0) out_lens[s] = total;
 }
 
 }  // namespace bq
@@ -435,15 +542,18 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
     return BQ_EINVAL;
   if (S == 0) return BQ_OK;
   const hipStream_t st = (hipStream_t)stream;
-  if (T <= JR_NT * 8)
-    hipLaunchKernelGGL(join_returns_row_kernel<8>, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T,
-                       ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
-  else if (T <= JR_NT * 16)
-    hipLaunchKernelGGL(join_returns_row_kernel<16>, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T,
-                       ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  if (T <= JR_ROW_NT * 4)
+    hipLaunchKernelGGL((join_returns_row_kernel<JR_ROW_NT, 4>), dim3((unsigned)S), dim3(JR_ROW_NT), 0, st, ts, close,
+                       lens, (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  else if (T <= JR_ROW_NT * 8)
+    hipLaunchKernelGGL((join_returns_row_kernel<JR_ROW_NT, 8>), dim3((unsigned)S), dim3(JR_ROW_NT), 0, st, ts, close,
+                       lens, (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
   else
     hipLaunchKernelGGL(join_returns_kernel, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T, ld_in,
                        bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
+  if (T <= JR_ROW_NT * 8)
+    hipLaunchKernelGGL(join_returns_fixup_kernel, dim3((unsigned)(S < 512 ? S : 512)), dim3(JR_NT), 0, st, ts, close,
+                       lens, (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens, S);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 

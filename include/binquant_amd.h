@@ -542,6 +542,10 @@ int bq_align(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64
  * (producers/context_evaluator.py:161-177): log(c/c.shift(1)) on each frame's
  * own rows, inner-joined on the timestamp, dropna'd, compacted in order into
  * x (symbol) / y (benchmark) [S][ld_out] with out_lens[s] pairs (NaN tail).
+ * A time the benchmark holds k times joins k pairs, in the benchmark's order,
+ * each with the return over the benchmark row before it (pandas' inner join
+ * on a repeated right index); a row whose pairs would pass ld_out keeps the
+ * first ld_out (out_lens[s] = ld_out). bench_ts ascending.
  */
 int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in,
                     const int64_t* bench_ts, const double* bench_close, int64_t n_bench, double* x, double* y,

@@ -143,3 +143,48 @@ def test_dynamic_btc_beta_corr_on_timestamp_index(cuda):
     r = fref.joined_returns(bts[keep], close, bts, bclose)
     wb, wc = fref.beta_corr_series(r, 50)
     assert abs(beta - wb[-1]) <= 1e-9 * abs(wb[-1]) and abs(corr - wc[-1]) <= 1e-9
+
+
+@pytest.mark.parametrize("T", [2048, 3000, 4096, 5000])
+@pytest.mark.parametrize("dup", [0, 1, 3])
+def test_joined_returns_long_rows(cuda, T, dup):
+    """Rows on the benchmark's 15-minute grid (the index guess hits) with
+    missing candles on both sides, a zero close and `dup` extra copies of one
+    benchmark time (pandas' inner join, context_evaluator.py:171-175, joins a
+    candle to every copy, each with the return over the row before it), at
+    the lengths that pick the whole-row kernel with 8 / 16 candles per thread
+    (T <= 2 048 / 4 096) and the tiled kernel (T > 4 096): the oracle's joined
+    returns, element for element."""
+    rng = np.random.default_rng(T + dup)
+    base = 1_700_000_000_000
+    nb = 3 * T + 300
+    d = 2 * T + 100                                      # the repeated time, past every whole-row span
+    grid = base + M15 * np.arange(nb)
+    keepb = np.ones(nb, bool)
+    keepb[rng.choice(np.r_[0:d, d + 1:nb], 20, replace=False)] = False
+    bts = np.sort(np.r_[grid[keepb], np.full(dup, grid[d])])
+    bclose = 30000 * np.exp(np.cumsum(rng.normal(0, 0.003, bts.size)))
+    S = 4
+    ts = np.stack([base + M15 * (np.arange(T) + 17 * s) for s in range(S)])
+    for s in range(1, S):   # gaps in the symbol rows too
+        drop = rng.choice(T, 10, replace=False)
+        row = np.delete(ts[s], drop)
+        ts[s] = np.r_[row, row[-1] + M15 * np.arange(1, 11)]
+    # row 0 jumps to the repeated time (the guess misses, the search finds
+    # it); row 3 starts just before it (its guessed span holds it)
+    h = T // 2
+    ts[0, h:] = grid[d - 5] + M15 * np.arange(T - h)
+    ts[3] = grid[d - T // 4] + M15 * np.arange(T)
+    close = 10 * np.exp(np.cumsum(rng.normal(0, 0.004, (S, T)), axis=1))
+    close[2, T // 3] = 0.0
+    lens = np.array([T, T, T - 5, T // 2])
+    x, y, n = engine.join_returns(torch.from_numpy(ts).cuda(), torch.from_numpy(close).cuda(),
+                                  torch.from_numpy(bts).cuda(), torch.from_numpy(bclose).cuda(), lens=lens)
+    x, y, n = x.cpu().numpy(), y.cpu().numpy(), n.cpu().numpy()
+    for s in range(S):
+        r = fref.joined_returns(ts[s, : lens[s]], close[s, : lens[s]], bts, bclose)
+        k = len(r)
+        assert n[s] == k, (s, n[s], k)
+        assert_close(x[s, :k], r["alt"].to_numpy(), f"alt[{s}]", rtol=1e-14)
+        assert_close(y[s, :k], r["btc"].to_numpy(), f"btc[{s}]", rtol=1e-14)
+        assert np.isnan(x[s, k:]).all() and np.isnan(y[s, k:]).all()
