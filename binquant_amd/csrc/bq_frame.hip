@@ -325,7 +325,7 @@ __device__ __forceinline__ void jr_row_tiled(int64_t s, const int64_t* __restric
   }
   const int total = sBase < ld_out ? sBase : (int)ld_out;
   // NaN tail so the row reads as a dropna'd series of length out_lens[s]
-  for (int t = total + tid; t < T; t += NT) {
+  for (int64_t t = total + tid; t < ld_out; t += NT) {
     xr[t] = qnan();
     yr[t] = qnan();
   }
@@ -344,8 +344,9 @@ __global__ __launch_bounds__(JR_NT) void join_returns_kernel(const int64_t* __re
 }
 
 // The rows the whole-row kernel handed back (out_lens[s] == -1: the benchmark
-// repeats a time the row joins or looks at), through the tiled join; a few
-// hundred workgroups stride over the rows, nearly all of which they skip.
+// repeats a time the row joins or looks at), through the tiled join: each
+// workgroup reads the flags of 256 rows at once and runs its flagged rows
+// (nearly always none).
 __global__ __launch_bounds__(JR_NT) void join_returns_fixup_kernel(const int64_t* __restrict__ ts,
                                                                    const double* __restrict__ close,
                                                                    const int64_t* __restrict__ lens, int T,
@@ -354,11 +355,18 @@ __global__ __launch_bounds__(JR_NT) void join_returns_fixup_kernel(const int64_t
                                                                    double* __restrict__ x, double* __restrict__ y,
                                                                    int64_t ld_out, int64_t* __restrict__ out_lens,
                                                                    int64_t S) {
-  for (int64_t s = blockIdx.x; s < S; s += gridDim.x) {
-    if (out_lens[s] >= 0) continue;   // block-uniform
-    jr_row_tiled<JR_NT>(s, ts, close, lens, T, ld_in, bts, bclose, nb, x, y, ld_out, out_lens);
-    __syncthreads();   // sBase is reset by the next row
-  }
+  __shared__ uint64_t sMask[JR_NT / WAVE];
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * JR_NT;
+  const uint64_t m = __ballot(s0 + tid < S && out_lens[s0 + tid] < 0);
+  if ((tid & (WAVE - 1)) == 0) sMask[tid / WAVE] = m;
+  __syncthreads();
+  for (int u = 0; u < JR_NT / WAVE; ++u)
+    for (uint64_t mm = sMask[u]; mm; mm &= mm - 1) {
+      jr_row_tiled<JR_NT>(s0 + u * WAVE + __builtin_ctzll(mm), ts, close, lens, T, ld_in, bts, bclose, nb, x, y,
+                          ld_out, out_lens);
+      __syncthreads();   // sBase is reset by the next row
+    }
 }
 
 // The same join for rows of up to JR_NT * K candles with the whole row in
@@ -470,7 +478,7 @@ __global__ __launch_bounds__(NT) void join_returns_row_kernel(const int64_t* __r
     }
   }
   const int total = base < ld_out ? base : (int)ld_out;
-  for (int t = total + tid; t < T; t += NT) {   // NaN tail: a dropna'd series of length out_lens[s]
+  for (int64_t t = total + tid; t < ld_out; t += NT) {   // NaN tail: a dropna'd series of length out_lens[s]
     xr[t] = qnan();
     yr[t] = qnan();
   }
@@ -552,7 +560,7 @@ int bq_join_returns(const int64_t* ts, const double* close, const int64_t* lens,
     hipLaunchKernelGGL(join_returns_kernel, dim3((unsigned)S), dim3(JR_NT), 0, st, ts, close, lens, (int)T, ld_in,
                        bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens);
   if (T <= JR_ROW_NT * 8)
-    hipLaunchKernelGGL(join_returns_fixup_kernel, dim3((unsigned)(S < 512 ? S : 512)), dim3(JR_NT), 0, st, ts, close,
+    hipLaunchKernelGGL(join_returns_fixup_kernel, dim3((unsigned)((S + JR_NT - 1) / JR_NT)), dim3(JR_NT), 0, st, ts, close,
                        lens, (int)T, ld_in, bench_ts, bench_close, (int)n_bench, x, y, ld_out, out_lens, S);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }

@@ -1134,22 +1134,27 @@ def leadership(open_time: torch.Tensor, close: torch.Tensor, bench_ts: torch.Ten
 
 @device_entry
 def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
-                 lens=None, stream: torch.cuda.Stream | None = None):
+                 lens=None, capacity: int | None = None, stream: torch.cuda.Stream | None = None):
     """Aligned (symbol, benchmark) log-return pairs of
     ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:161-177):
     returns on each frame's own rows, inner join on the timestamp, dropna,
-    compacted per row. Returns (x [S, T], y [S, T], pairs per row int64 [S])."""
+    compacted per row. Returns (x [S, C], y [S, C], pairs per row int64 [S]),
+    C = max(T, capacity). A benchmark time held k times joins k pairs (pandas'
+    inner join), so a row can hold up to T + (repeated benchmark times) pairs:
+    pass that as `capacity` when the benchmark repeats times (a row's pairs
+    past C are cut at C)."""
     ts = _check_ts(ts)
     S, T = ts.shape
     close = _check_panel(close, "close", (S, T)).contiguous()
     bts = _check_ts(bench_ts, "bench_ts").reshape(-1)
     bc = _check_panel(bench_close.reshape(1, -1), "bench_close", (1, bts.numel())).contiguous()
     lens = _check_lens(lens, S, ts.device)
-    x = torch.empty((S, T), dtype=torch.float64, device=ts.device)
+    C = max(T, int(capacity or 0))
+    x = torch.empty((S, C), dtype=torch.float64, device=ts.device)
     y = torch.empty_like(x)
     n = torch.empty(S, dtype=torch.int64, device=ts.device)
     st = _lib.load().bq_join_returns(_ptr(ts), _ptr(close), _ptr(lens), S, T, T, _ptr(bts), _ptr(bc), bts.numel(),
-                                     _ptr(x), _ptr(y), T, _ptr(n), _stream_handle(stream))
+                                     _ptr(x), _ptr(y), C, _ptr(n), _stream_handle(stream))
     _lib.check(st, "bq_join_returns")
     return x, y, n
 

@@ -253,9 +253,12 @@ def dynamic_btc_beta_corr_frames(frames: Sequence[pd.DataFrame], df_btc: pd.Data
             ts[s, :n] = pd.to_numeric(df[key]).to_numpy(np.int64)
             ts[s, n:] = ts[s, n - 1]
             cl[s, :n] = pd.to_numeric(df["close"], errors="coerce").to_numpy(np.float64)
-    bts = torch.from_numpy(pd.to_numeric(df_btc[key]).to_numpy(np.int64)).to(dev)
+    bts_h = pd.to_numeric(df_btc[key]).to_numpy(np.int64)
+    bts = torch.from_numpy(bts_h).to(dev)
     bcl = torch.from_numpy(pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)).to(dev)
-    x, y, n = engine.join_returns(torch.from_numpy(ts).to(dev), torch.from_numpy(cl).to(dev), bts, bcl, lens=lens)
+    repeats = bts_h.size - np.unique(bts_h).size   # each repeated time can add one pair per row
+    x, y, n = engine.join_returns(torch.from_numpy(ts).to(dev), torch.from_numpy(cl).to(dev), bts, bcl, lens=lens,
+                                  capacity=T + repeats)
     bc = engine.beta_corr_pairs(x, y, window=window)
     n = n.cpu().numpy()
     last = torch.from_numpy(np.maximum(n - 1, 0)).to(dev)

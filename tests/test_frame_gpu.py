@@ -188,3 +188,39 @@ def test_joined_returns_long_rows(cuda, T, dup):
         assert_close(x[s, :k], r["alt"].to_numpy(), f"alt[{s}]", rtol=1e-14)
         assert_close(y[s, :k], r["btc"].to_numpy(), f"btc[{s}]", rtol=1e-14)
         assert np.isnan(x[s, k:]).all() and np.isnan(y[s, k:]).all()
+
+
+def test_joined_returns_capacity(cuda):
+    """Every benchmark time held three times: a row joins up to 3 (T - 1)
+    pairs. With the default capacity (T) the row is cut at T pairs (the
+    oracle's first T); with capacity T + repeats it holds all of them, and
+    the drop-in dynamic_btc_beta_corr_frames sizes it that way itself."""
+    from binquant_amd.indicators import dynamic_btc_beta_corr_frames
+
+    rng = np.random.default_rng(5)
+    base = 1_700_000_000_000
+    T, nb = 120, 150
+    bts = np.repeat(base + M15 * np.arange(nb), 3)
+    bclose = 30000 * np.exp(np.cumsum(rng.normal(0, 0.003, bts.size)))
+    ts = (base + M15 * (np.arange(T) + 7))[None]
+    close = 10 * np.exp(np.cumsum(rng.normal(0, 0.004, (1, T)), axis=1))
+    r = fref.joined_returns(ts[0], close[0], bts, bclose)
+    k = len(r)
+    assert k > T
+    args = (torch.from_numpy(ts).cuda(), torch.from_numpy(close).cuda(), torch.from_numpy(bts).cuda(),
+            torch.from_numpy(bclose).cuda())
+    x, y, n = engine.join_returns(*args)
+    assert x.shape == (1, T) and int(n[0]) == T
+    assert_close(x[0].cpu().numpy(), r["alt"].to_numpy()[:T], "alt cut", rtol=1e-14)
+    assert_close(y[0].cpu().numpy(), r["btc"].to_numpy()[:T], "btc cut", rtol=1e-14)
+    cap = T + bts.size - np.unique(bts).size
+    x, y, n = engine.join_returns(*args, capacity=cap)
+    assert x.shape == (1, cap) and int(n[0]) == k
+    assert_close(x[0, :k].cpu().numpy(), r["alt"].to_numpy(), "alt", rtol=1e-14)
+    assert_close(y[0, :k].cpu().numpy(), r["btc"].to_numpy(), "btc", rtol=1e-14)
+    assert torch.isnan(x[0, k:]).all() and torch.isnan(y[0, k:]).all()
+    df = pd.DataFrame({"open_time": ts[0], "close": close[0]})
+    df_btc = pd.DataFrame({"open_time": bts, "close": bclose})
+    beta, corr = dynamic_btc_beta_corr_frames([df], df_btc, window=50, decimals=None)[0]
+    wb, wc = fref.beta_corr_series(r, 50)
+    assert abs(beta - wb[-1]) <= 1e-9 * abs(wb[-1]) and abs(corr - wc[-1]) <= 1e-9
