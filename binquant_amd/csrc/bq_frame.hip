@@ -274,6 +274,12 @@ __device__ __forceinline__ int jr_count(const double* __restrict__ bclose, doubl
 // block-wide exclusive scan (wave shfl scans + LDS wave offsets), the pairs
 // written in order.
 constexpr int JR_NT = 256;
+#ifndef JR_SPEC
+#define JR_SPEC 1   // whole-row kernel: benchmark closes loaded with the guess
+#endif
+#ifndef JR_WAVES
+#define JR_WAVES 8   // whole-row kernel (512 threads): 8 waves per SIMD, 4 rows per CU in flight
+#endif
 #ifndef JR_ROW_NT
 #define JR_ROW_NT 512   // whole-row kernel block (4 / 8 candles per thread)
 #endif
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(JR_NT) void join_returns_fixup_kernel(const int64_t
 // pair counts (one barrier), in the same order and with the same values as
 // the tiled kernel.
 template <int NT, int K>
-__global__ __launch_bounds__(NT) void join_returns_row_kernel(const int64_t* __restrict__ ts,
+__global__ __launch_bounds__(NT, K <= 4 ? JR_WAVES : 4) void join_returns_row_kernel(const int64_t* __restrict__ ts,
                                                                  const double* __restrict__ close,
                                                                  const int64_t* __restrict__ lens, int T, int64_t ld_in,
                                                                  const int64_t* __restrict__ bts,
@@ -394,54 +400,76 @@ __global__ __launch_bounds__(NT) void join_returns_row_kernel(const int64_t* __r
   double* __restrict__ xr = x + s * ld_out;
   double* __restrict__ yr = y + s * ld_out;
   const int n = row_len(lens, s, T);
-  const int j0 = n > 0 ? lower_bound_i64(bts, nb, rts[0]) : 0;
-  const int off = j0 < nb && n > 0 && bts[j0] == rts[0] ? j0 : 0;
   double c[K], cp[K];
   int64_t key[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+  for (int k = 0; k < K; ++k) {   // the row's own loads go out first
     const int t = k * NT + tid;
     c[k] = t < n ? rc[t] : qnan();
     cp[k] = t >= 1 && t <= n ? rc[t - 1] : qnan();
     key[k] = t < n ? rts[t] : 0;
   }
-  // the benchmark row at the guessed index (index-aligned frames) and the one
-  // after it: a guessed hit is the only row with its time unless the
-  // benchmark repeats a time inside the block's guessed span, which the same
-  // loads show (two equal neighbours); candles the guess misses take the two
-  // binary searches. A block with a repeated time anywhere it looks (dup) or
-  // a candle that joins several rows (multi) runs the tiled join instead.
-  int64_t g0[K], g1[K];
+  // the row's offset into the benchmark's index: one probe at the benchmark's
+  // own step (a regular grid), the binary search where that misses
+  int off = 0;
+  if (n > 0 && nb > 0) {
+    const int64_t k0 = rts[0], bt0 = bts[0], step = nb > 1 ? bts[1] - bt0 : 0;
+    const int64_t q = step > 0 && k0 > bt0 ? (k0 - bt0) / step : 0;
+    int gg = (int)(q < nb - 1 ? q : nb - 1);
+    if (bts[gg] != k0) {
+      gg = lower_bound_i64(bts, nb, k0);
+      if (gg >= nb || bts[gg] != k0) gg = 0;
+    }
+    off = gg;
+  }
+  // the benchmark row at the guessed index (index-aligned frames), the one
+  // after it, and (speculatively) the two benchmark closes a hit reads: a
+  // guessed hit is the only row with its time unless the benchmark repeats a
+  // time inside the block's guessed span, which the same loads show (two
+  // equal neighbours); candles the guess misses take the binary search. A
+  // block that meets a repeated time hands its row to the fixup pass.
+  // (the row after the guess is the next lane's guess: only a wave's last
+  // lane loads it)
+  int64_t g0[K];
+  double b0[K], b1[K];
   bool odd = false;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int g = k * NT + tid + off;
     g0[k] = g < nb ? bts[g] : INT64_MIN;
-    g1[k] = g + 1 < nb ? bts[g + 1] : INT64_MIN;
-    odd |= g + 1 < nb && g0[k] == g1[k];
+#if JR_SPEC
+    b0[k] = g >= 1 && g < nb ? bclose[g] : qnan();
+    b1[k] = g >= 1 && g < nb ? bclose[g - 1] : qnan();
+#endif
   }
   int j[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int t = k * NT + tid, g = t + off;
+    int64_t g1 = __shfl_down(g0[k], 1, WAVE);
+    if (lane == WAVE - 1) g1 = g + 1 < nb ? bts[g + 1] : INT64_MIN;
+    odd |= g + 1 < nb && g0[k] == g1;
     const bool live = t > 0 && t < n;
-    const bool hit = g < nb && g0[k] == key[k] && (g + 1 >= nb || g1[k] != key[k]);
+    const bool hit = g < nb && g0[k] == key[k];   // unique unless odd
     j[k] = !live ? -1 : (hit ? g : -2);
   }
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-    if (j[k] == -2) {   // off-grid candles (rare)
-      const int jf = lower_bound_i64(bts, nb, key[k]);
-      const bool found = jf < nb && bts[jf] == key[k];
-      odd |= found && jf + 1 < nb && bts[jf + 1] == key[k];   // several rows: the tiled join
-      j[k] = found ? jf : -1;
-    }
-  double b0[K], b1[K];
+#if !JR_SPEC
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     b0[k] = j[k] > 0 ? bclose[j[k]] : qnan();
     b1[k] = j[k] > 0 ? bclose[j[k] - 1] : qnan();
   }
+#endif
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (j[k] == -2) {   // off-grid candles (rare)
+      const int jf = lower_bound_i64(bts, nb, key[k]);
+      const bool found = jf < nb && bts[jf] == key[k];
+      odd |= found && jf + 1 < nb && bts[jf + 1] == key[k];   // several rows: the fixup pass
+      j[k] = found ? jf : -1;
+      b0[k] = j[k] > 0 ? bclose[j[k]] : qnan();
+      b1[k] = j[k] > 0 ? bclose[j[k] - 1] : qnan();
+    }
   double xa[K], yb[K];
   uint64_t m[K];
 #pragma unroll
