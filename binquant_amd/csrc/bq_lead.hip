@@ -25,7 +25,10 @@
 //      returns them (0 where the gate is shut), and where the gate is open
 //      and both strengths are > 0, one walk over the 96 entries of its
 //      window counting n (entries), c2 = #{h2 <= rs_2h}, c6 = #{h6 <= rs_6h}:
-//      leader = n >= min_count and c2, c6 >= int(q (n - 1)) + 1.
+//      leader = n >= min_count and c2, c6 >= int(q (n - 1)) + 1. A thread
+//      walks two neighbouring candles (one LDS read per step serves both),
+//      and the pairs that walk are packed into the tile's first waves (a
+//      ballot scan through LDS).
 // Inputs cross HBM once (the halo re-reads hit L2); nothing but the outputs
 // is written.
 #include "bq_device.h"
@@ -35,7 +38,10 @@
 
 namespace bq {
 
-constexpr int LD_NT = 256;
+#ifndef LD_TILE
+#define LD_TILE 256
+#endif
+constexpr int LD_NT = LD_TILE;
 constexpr int LD_W = 96;                 // RS_LOOKBACK (compiled)
 constexpr int LD_LMAX = 31;              // the long offset's bound (RS 6h: 24)
 constexpr int LD_HH = LD_W - 1;          // history halo before the tile
@@ -55,7 +61,8 @@ struct LeadArgs {
 
 __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
   __shared__ double sC[LD_CH + LD_NT], sB[LD_CH + LD_NT];
-  __shared__ double sH[2][LD_HH + LD_NT];
+  __shared__ double2 sH[LD_HH + LD_NT];   // (rs_2h, rs_6h) entries: one 16-byte LDS read per walk step
+  __shared__ uint64_t sPos[(LD_CH + LD_NT + WAVE - 1) / WAVE];   // bit: close and benchmark close > 0
   const int tid = threadIdx.x;
   const int64_t s = blockIdx.y;
   const int t0 = blockIdx.x * LD_NT;
@@ -76,6 +83,8 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     }
     sC[i] = c;
     sB[i] = b;
+    const uint64_t pm = __ballot(c > 0.0 && b > 0.0);   // slots i - lane .. i - lane + 63 (LD_NT % 64 == 0)
+    if ((tid & (WAVE - 1)) == 0) sPos[i / WAVE] = pm;
   }
   __syncthreads();
   // 2. history entries of candles t0 - LD_HH .. t0 + LD_NT - 1 (none outside the row)
@@ -86,42 +95,100 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     // a history entry: all three times in the benchmark, min(...) > 0 (:172-180),
     // the reference's float arithmetic c / c[-9] - b / b[-9] (:179-180)
     const bool pos = c0 > 0.0 && c2 > 0.0 && c6 > 0.0 && b0 > 0.0 && b2 > 0.0 && b6 > 0.0;
-    sH[0][i] = pos ? c0 / c2 - b0 / b2 : qnan();
-    sH[1][i] = pos ? c0 / c6 - b0 / b6 : qnan();
+    sH[i] = make_double2(pos ? c0 / c2 - b0 / b2 : qnan(), pos ? c0 / c6 - b0 / b6 : qnan());
   }
   __syncthreads();
   const int t = t0 + tid;
-  if (t >= T) return;
+  const int lane = tid & (WAVE - 1), w = tid / WAVE;
   // 3. _relative_strengths: the last lng + 1 times present, every close > 0
   //    (:143-149); len(df) >= MIN_HISTORY (:160)
-  const int k = LD_CH + tid;
-  bool gate = t + 1 >= A.min_hist && t >= lng;
-  for (int d = 0; d <= lng && gate; ++d) gate = sC[k - d] > 0.0 && sB[k - d] > 0.0;
-  const double c0 = sC[k], b0 = sB[k];
-  const double r2 = c0 / sC[k - shrt] - b0 / sB[k - shrt];   // (:150-153)
-  const double r6 = c0 / sC[k - lng] - b0 / sB[k - lng];
-  const int64_t o = s * A.ld_out + t;
-  A.rs[0][o] = gate ? r2 : 0.0;   // (False, 0.0, 0.0) when the strengths are None (:160-161)
-  A.rs[1][o] = gate ? r6 : 0.0;
-  bool lead = false;
-  if (gate && r2 > 0.0 && r6 > 0.0) {   // otherwise the method's answer is False whatever the thresholds
-    // the window of the last LD_W positions (:170): entries counted, and how
-    // many are <= the current strengths; gate implies the entry at t exists
-    // (it equals r2 / r6)
-    const int h = LD_HH + tid;
-    int n = 0, c2 = 0, c6 = 0;
-#pragma unroll 8
-    for (int d = 0; d < LD_W; ++d) {
-      const double e2 = sH[0][h - d], e6 = sH[1][h - d];
-      n += e2 == e2 ? 1 : 0;
-      c2 += e2 <= r2 ? 1 : 0;   // NaN: no entry, not counted
-      c6 += e6 <= r6 ? 1 : 0;
+  bool act = false;
+  if (t < T) {
+    const int k = LD_CH + tid;
+    bool gate = t + 1 >= A.min_hist && t >= lng;
+    {   // slots k - lng .. k all positive (lng < 64: at most two mask words)
+      const int lo = k - lng, wl = lo / WAVE, wh = k / WAVE;
+      const uint64_t hi_mask = ~0ull >> (WAVE - 1 - (k & (WAVE - 1)));   // bits 0 .. k % 64
+      const uint64_t lo_mask = ~0ull << (lo & (WAVE - 1));                // bits lo % 64 .. 63
+      gate = gate && (wl == wh ? (sPos[wh] & (hi_mask & lo_mask)) == (hi_mask & lo_mask)
+                               : (sPos[wl] & lo_mask) == lo_mask && (sPos[wh] & hi_mask) == hi_mask);
     }
-    // sorted(h)[int((n - 1) q)] <= rs  <=>  #{h <= rs} >= int((n - 1) q) + 1 (:183-193)
-    const int need = (int)((double)(n - 1) * A.q) + 1;
-    lead = n >= A.minc && c2 >= need && c6 >= need;
+    const double c0 = sC[k], b0 = sB[k];
+    const double r2 = c0 / sC[k - shrt] - b0 / sB[k - shrt];   // (:150-153)
+    const double r6 = c0 / sC[k - lng] - b0 / sB[k - lng];
+    const int64_t o = s * A.ld_out + t;
+    A.rs[0][o] = gate ? r2 : 0.0;   // (False, 0.0, 0.0) when the strengths are None (:160-161)
+    A.rs[1][o] = gate ? r6 : 0.0;
+    // otherwise the method's answer is False whatever the thresholds
+    act = gate && r2 > 0.0 && r6 > 0.0;
+    if (!act) A.leader[o] = 0;
   }
-  A.leader[o] = lead ? 1 : 0;
+  // the window walks, two neighbouring candles per thread (their windows
+  // share 95 of 96 entries: one LDS read serves both), the pairs that need
+  // one packed into the tile's first waves (the others' waves skip it)
+  constexpr int NP = LD_NT / 2;
+  __shared__ unsigned char sAct[LD_NT];
+  __shared__ int sList[NP], sWc[LD_NT / WAVE];
+  sAct[tid] = act;
+  __syncthreads();
+  const bool pa = tid < NP && (sAct[2 * tid] | sAct[2 * tid + 1]);
+  const uint64_t m = __ballot(pa);
+  if (lane == 0) sWc[w] = __popcll(m);
+  __syncthreads();
+  int base = 0, total = 0;
+  for (int u = 0; u < LD_NT / WAVE; ++u) {
+    base += u < w ? sWc[u] : 0;
+    total += sWc[u];
+  }
+  if (pa) sList[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = tid;
+  __syncthreads();
+  if (tid >= total) return;
+  const int u0 = 2 * sList[tid], u1 = u0 + 1;
+  const bool a0 = sAct[u0], a1 = sAct[u1];
+  // the same strengths, recomputed (a candle of the pair that does not walk
+  // is counted and dropped)
+  const double r20 = sC[LD_CH + u0] / sC[LD_CH + u0 - shrt] - sB[LD_CH + u0] / sB[LD_CH + u0 - shrt];
+  const double r60 = sC[LD_CH + u0] / sC[LD_CH + u0 - lng] - sB[LD_CH + u0] / sB[LD_CH + u0 - lng];
+  const double r21 = sC[LD_CH + u1] / sC[LD_CH + u1 - shrt] - sB[LD_CH + u1] / sB[LD_CH + u1 - shrt];
+  const double r61 = sC[LD_CH + u1] / sC[LD_CH + u1 - lng] - sB[LD_CH + u1] / sB[LD_CH + u1 - lng];
+  // the window of the last LD_W positions (:170): entries counted, and how
+  // many are <= the current strengths; the gate implies the entry at t exists
+  // (it equals r2 / r6). Entry h1 - d is candle u1's d-th and u0's (d - 1)-th.
+  const int h1 = LD_HH + u1;
+  int n0 = 0, c20 = 0, c60 = 0, n1, c21, c61;
+  {
+    const double2 e = sH[h1];
+    n1 = e.x == e.x ? 1 : 0;
+    c21 = e.x <= r21 ? 1 : 0;   // NaN: no entry, not counted
+    c61 = e.y <= r61 ? 1 : 0;
+  }
+#pragma unroll 5
+  for (int d = 1; d < LD_W; ++d) {
+    const double2 e = sH[h1 - d];
+    const int v = e.x == e.x ? 1 : 0;
+    n1 += v;
+    n0 += v;
+    c21 += e.x <= r21 ? 1 : 0;
+    c61 += e.y <= r61 ? 1 : 0;
+    c20 += e.x <= r20 ? 1 : 0;
+    c60 += e.y <= r60 ? 1 : 0;
+  }
+  {
+    const double2 e = sH[h1 - LD_W];
+    n0 += e.x == e.x ? 1 : 0;
+    c20 += e.x <= r20 ? 1 : 0;
+    c60 += e.y <= r60 ? 1 : 0;
+  }
+  // sorted(h)[int((n - 1) q)] <= rs  <=>  #{h <= rs} >= int((n - 1) q) + 1 (:183-193)
+  const int64_t o = s * A.ld_out + t0;
+  if (a0) {
+    const int need = (int)((double)(n0 - 1) * A.q) + 1;
+    A.leader[o + u0] = n0 >= A.minc && c20 >= need && c60 >= need ? 1 : 0;
+  }
+  if (a1) {
+    const int need = (int)((double)(n1 - 1) * A.q) + 1;
+    A.leader[o + u1] = n1 >= A.minc && c21 >= need && c61 >= need ? 1 : 0;
+  }
 }
 
 }  // namespace bq
