@@ -190,11 +190,16 @@ SIGNATURES: dict[str, tuple] = {
         ctypes.c_int,
         [ctypes.POINTER(ctypes.c_void_p), _I64, ctypes.POINTER(BqParams)],
     ),
+    "bq_state_create_frame": (
+        ctypes.c_int,
+        [ctypes.POINTER(ctypes.c_void_p), _I64, ctypes.POINTER(BqParams), _I64],
+    ),
     "bq_state_destroy": (ctypes.c_int, [_P]),
     "bq_state_seed": (ctypes.c_int, [_P, _PP, _I64, _I64, _P]),
     "bq_tick": (ctypes.c_int, [_P, _PP, _PP, _P]),
     "bq_state_symbols": (_I64, [_P]),
     "bq_state_count": (_I64, [_P]),
+    "bq_state_frame": (_I64, [_P]),
     "bq_market_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _PP, _I64, _P]),
     "bq_breadth_partial": (ctypes.c_int, [_P, _PP, _I64, _I64, _I64, _I64, _P, _P]),
     "bq_context_workspace_bytes": (ctypes.c_size_t, [_I64, _I64]),
@@ -219,6 +224,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_supertrend_panel": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_resample_count": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I64, _P, _P]),
     "bq_resample": (ctypes.c_int, [_P, _PP, _P, _I32, _P, _I64, _I64, _I64, _I64, _P, _PP, _I64, _P]),
+    "bq_resample_tail": (ctypes.c_int, [_P, _PP, _P, _I32, _P, _I64, _I64, _I64, _I64, _P, _PP, _I64, _P]),
     "bq_align": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _I64, _P]),
     "bq_join_returns": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, _P, _P]),
     "bq_beta_corr_bret": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),

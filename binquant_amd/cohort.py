@@ -64,13 +64,20 @@ def _side_streams(device: torch.device, n: int) -> list[torch.cuda.Stream]:
 
 
 def process_cohort(o5, h5, l5, c5, v5, o15, h15, l15, c15, v15, ts15, btc_ts15, btc_c15,
-                   max_bars: int = 400, exact: bool = True) -> dict[str, torch.Tensor]:
+                   max_bars: int = 400, exact: bool = True, h1_max_bins: int | None = None) -> dict[str, torch.Tensor]:
     """Device outputs of process_data for a cohort: 5m / 15m panels [S, T5] /
     [S, T15] float64, ts15 [S, T15] int64 open times, btc_ts15 / btc_c15 [T15]
     (index-aligned with the 15m panel). exact=True runs the strategy
     pipelines' bit-exact replays (the live path); False their panel mode.
-    Returns a flat dict of tensors (names prefixed by the stage)."""
+    h1_max_bins: width of the h1.* arrays (default T15 // 4 + 2, every bin
+    of a gap-free 15m grid). pandas emits every empty hour of a gap, so a row
+    spanning more hours keeps its NEWEST h1_max_bins bins (bq_resample_tail):
+    h1.bins is the count written (<= h1_max_bins, bin h1.bins - 1 is the
+    row's latest hour) and h1.dropped the oldest bins left out (0 on a
+    gap-free grid). Returns a flat dict of tensors (names prefixed by the
+    stage)."""
     S, T15 = c15.shape
+    B1 = T15 // 4 + 2 if h1_max_bins is None else int(h1_max_bins)
     btc_c = btc_c15.reshape(-1)
 
     def frame_5m(out):   # :364-388
@@ -83,15 +90,16 @@ def process_cohort(o5, h5, l5, c5, v5, o15, h15, l15, c15, v15, ts15, btc_ts15, 
         for k, v in engine.enrich(o15, h15, l15, c15, v15).items():
             out[f"e15.{k}"] = v
         bins, res, nbins = engine.resample(ts15, {"open": o15, "high": h15, "low": l15, "close": c15,
-                                                  "volume": v15}, RESAMPLE_AGG, HOUR_MS, max_bins=T15 // 4 + 2)
+                                                  "volume": v15}, RESAMPLE_AGG, HOUR_MS, max_bins=B1, tail=True)
         out["h1.open_time"] = bins
-        out["h1.bins"] = nbins
+        out["h1.bins"] = nbins.clamp(max=B1)
+        out["h1.dropped"] = (nbins - B1).clamp(min=0)
         for k, v in res.items():
             out[f"h1.{k}"] = v
         bc = engine.beta_corr(c15, btc_c15, 50)
         out["btc.beta"], out["btc.corr"] = bc["beta"][:, -1], bc["corr"][:, -1]
-        out["btc.change_24h"] = ((btc_c15[-1] / btc_c15[-97] - 1.0) * 100.0).reshape(1) if T15 > 96 else \
-            torch.full((1,), float("nan"), dtype=torch.float64, device=c15.device)
+        # pct_change(96) with pandas' default pad fill (context_evaluator.py:427-430)
+        out["btc.change_24h"] = engine.pct_change(btc_c15.reshape(1, -1), 96)[0, -1:] * 100.0
 
     def context(out):   # klines_provider.py:181-199
         part, last = engine.context_partials(h15, l15, c15, max_bars=max_bars, last=True)

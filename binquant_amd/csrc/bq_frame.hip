@@ -69,6 +69,7 @@ struct ResampleArgs {
   int64_t* out_ts;
   int64_t S, ld_in, ld_out, I;
   int T, nf;
+  int tail;   // a row with more bins than ld_out keeps its NEWEST ld_out bins
 };
 
 constexpr int RS_FULL = 4;   // candles of a full bin on the reference's 15m -> 1h resample
@@ -85,7 +86,10 @@ __global__ __launch_bounds__(256) void resample_kernel(const ResampleArgs A) {
   int64_t origin, b0, nb;
   row_bins(ts, n, A.I, origin, b0, nb);
   if (b >= nb) return;
-  const int64_t key = origin + (b0 + b) * A.I;
+  // tail mode: output bin b is the row's bin b + (nb - ld_out) when the row
+  // has more bins than the output holds (a gap widened its span)
+  const int64_t skip = A.tail && nb > A.ld_out ? nb - A.ld_out : 0;
+  const int64_t key = origin + (b0 + skip + b) * A.I;
   const int64_t t0v = ts[0], span = ts[n - 1] - t0v;   // n >= 1 here (nb > b >= 0)
   const int64_t step = n > 1 && span > 0 && span % (n - 1) == 0 ? span / (n - 1) : 0;
   const int lo = lower_bound_guess(ts, n, key, t0v, step);
@@ -527,9 +531,9 @@ int bq_resample_count(const int64_t* ts, const int64_t* lens, int64_t S, int64_t
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
-int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
-                const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
-                double* const* out_fields, int64_t ld_out, void* stream) {
+static int resample_launch(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                           const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms,
+                           int64_t* out_ts, double* const* out_fields, int64_t ld_out, int tail, void* stream) {
   using namespace bq;
   if (!ts || S < 0 || T < 0 || ld_in < T || ld_out < 0 || interval_ms <= 0 || nfields < 0 ||
       nfields > BQ_MAX_RESAMPLE_FIELDS || (nfields > 0 && (!fields || !aggs || !out_fields)) || T > 0x7fffffff)
@@ -551,9 +555,24 @@ int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* a
   A.I = interval_ms;
   A.T = (int)T;
   A.nf = nfields;
+  A.tail = tail;
   const int64_t items = S * ld_out;
   hipLaunchKernelGGL(resample_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
+                double* const* out_fields, int64_t ld_out, void* stream) {
+  return resample_launch(ts, fields, aggs, nfields, lens, S, T, ld_in, interval_ms, out_ts, out_fields, ld_out, 0,
+                         stream);
+}
+
+int bq_resample_tail(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                     const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
+                     double* const* out_fields, int64_t ld_out, void* stream) {
+  return resample_launch(ts, fields, aggs, nfields, lens, S, T, ld_in, interval_ms, out_ts, out_fields, ld_out, 1,
+                         stream);
 }
 
 int bq_align(const int64_t* ts, const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, const int64_t* bench_ts,

@@ -616,16 +616,31 @@ def context_partials(
 
 
 class TickState:
-    """Device-resident streaming state for S symbols (bq_state)."""
+    """Device-resident streaming state for S symbols (bq_state).
 
-    def __init__(self, n_symbols: int, params: IndicatorParams | None = None):
+    ``frame`` is the per-message frame the reference re-enriches on every
+    closed kline: KlinesProvider.LIMIT = 400 candles
+    (consumers/klines_provider.py:40,201-215 -> producers/context_evaluator.py:
+    367-371). Each tick returns the last row of indicators_enrichment over the
+    symbol's last ``frame`` candles, the EMA family seeded at the frame's first
+    candle exactly as the reference's re-enrichment is. ``frame=0`` keeps
+    unbounded-history EMA carries (the full-series pandas EMA) instead."""
+
+    FRAME = 400
+
+    def __init__(self, n_symbols: int, params: IndicatorParams | None = None, frame: int = FRAME):
         self._lib = _lib.load()
         self._h = ctypes.c_void_p()
         p = (params or IndicatorParams()).to_c()
         # device memory of the state lives on the current device (bq_state_create)
         self.device = torch.device("cuda", torch.cuda.current_device())
-        _lib.check(self._lib.bq_state_create(ctypes.byref(self._h), int(n_symbols), ctypes.byref(p)), "bq_state_create")
+        frame = int(frame)
+        if frame != 0 and not (_lib.MAX_WINDOW + 2 <= frame <= 1 << 20):
+            raise ValueError(f"frame must be 0 or in [{_lib.MAX_WINDOW + 2}, {1 << 20}], got {frame}")
+        _lib.check(self._lib.bq_state_create_frame(ctypes.byref(self._h), int(n_symbols), ctypes.byref(p), frame),
+                   "bq_state_create_frame")
         self.n_symbols = int(n_symbols)
+        self.frame = frame
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -1032,6 +1047,7 @@ def resample(
     interval_ms: int,
     lens=None,
     max_bins: int | None = None,
+    tail: bool = False,
     stream: torch.cuda.Stream | None = None,
 ) -> tuple[torch.Tensor, dict[str, torch.Tensor], torch.Tensor]:
     """Candles.resample (producers/context_evaluator.py:403-407) on a ragged
@@ -1040,7 +1056,10 @@ def resample(
     bins per row int64 [S]); B = the longest row's bin count, read back from
     the device — or, with max_bins (fixed frame geometry, e.g. a captured
     graph: no host synchronisation), B = max_bins, which must be at least
-    every row's bin count (bins past a row's count are left unwritten)."""
+    every row's bin count (bins past a row's count are left unwritten) —
+    or, with tail=True (bq_resample_tail), a row with more bins than B keeps
+    its newest B bins, so bin min(bins, B) - 1 is always the row's latest
+    (the returned bins per row stay the true counts)."""
     ts = _check_ts(ts)
     S, T = ts.shape
     names = list(fields)
@@ -1067,7 +1086,7 @@ def resample(
     out_ts = torch.empty((S, B), dtype=torch.int64, device=ts.device)
     outs = [torch.empty((S, B), dtype=torch.float64, device=ts.device) for _ in names]
     agg_arr = (ctypes.c_int32 * max(1, len(codes)))(*codes)
-    st = L.bq_resample(
+    st = (L.bq_resample_tail if tail else L.bq_resample)(
         _ptr(ts), _lib.ptr_array([t.data_ptr() for t in ins]), ctypes.cast(agg_arr, ctypes.c_void_p), len(names),
         _ptr(lens), S, T, T, int(interval_ms), _ptr(out_ts), _lib.ptr_array([t.data_ptr() for t in outs]), B,
         _stream_handle(stream),
@@ -1175,12 +1194,23 @@ def beta_corr_pairs(x: torch.Tensor, y: torch.Tensor, window: int = 50,
     return {"beta": beta, "corr": corr}
 
 
-def pct_change(x: torch.Tensor, periods: int = 1) -> torch.Tensor:
-    """x.pct_change(periods) along T of a [S, T] panel (pandas:
-    x / x.shift(periods) - 1; NaN for the first `periods` rows). Device
-    element-wise, same IEEE operations as pandas."""
+@device_entry
+def pct_change(x: torch.Tensor, periods: int = 1, fill_method: str | None = "pad") -> torch.Tensor:
+    """x.pct_change(periods) along T of a [S, T] panel with pandas 2.3.3's
+    default fill_method='pad': f / f.shift(periods) - 1 over the
+    forward-filled series f (leading NaNs stay NaN; [1, 2, nan, 4, 5] ->
+    [nan, 1, 0, 1, 0.25]) — the BTC 24h change of
+    producers/context_evaluator.py:427-430. fill_method=None: the raw series.
+    The fill is the device ffill replay (bq_rolling_batch), the quotient the
+    same IEEE operations as pandas."""
     x = _check_panel(x, "x")
-    out = torch.full_like(x, float("nan"))
-    if periods < x.shape[1]:
-        out[:, periods:] = x[:, periods:] / x[:, :-periods] - 1
+    if fill_method not in ("pad", "ffill", None):
+        raise ValueError(f"fill_method must be 'pad' or None, got {fill_method!r}")
+    periods = int(periods)
+    if periods < 1:
+        raise ValueError(f"periods must be >= 1, got {periods}")
+    f = rolling_many(Ffill(x))[0] if fill_method is not None else x
+    out = torch.full_like(f, float("nan"))
+    if periods < f.shape[1]:
+        out[:, periods:] = f[:, periods:] / f[:, :-periods] - 1
     return out

@@ -280,10 +280,13 @@ def dynamic_btc_beta_corr_frames(frames: Sequence[pd.DataFrame], df_btc: pd.Data
 
 def btc_price_change(df_btc: pd.DataFrame, periods: int = 96) -> float:
     """BTC 24h change of ContextEvaluator.process_data (producers/context_evaluator.py:427-430):
-    close.pct_change(periods=96) * 100 at the last row, on the device
-    (engine.pct_change); NaN when the frame is too short."""
+    close.pct_change(periods=96) * 100 at the last row, with pandas 2.3.3's
+    default pad fill (a missing close takes the previous one, at the last row
+    and at t - 96 alike, reaching as far back as the frame goes), on the device
+    (engine.pct_change over the whole column); NaN when the frame is too short
+    or no close precedes t - 96, as pandas."""
     c = pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)
     if len(c) <= periods:
         return float("nan")
-    x = torch.from_numpy(c[-periods - 1 :]).to(_device())[None, :]
+    x = torch.from_numpy(np.ascontiguousarray(c)).to(_device())[None, :]
     return float(engine.pct_change(x, periods)[0, -1] * 100)

@@ -134,15 +134,31 @@ int bq_enrich(const double* const* in, int64_t S, int64_t T, int64_t ld_in,
 /* ---- streaming tick path ------------------------------------------------- */
 typedef struct bq_state bq_state;   /* opaque, device-resident */
 
-/* Create state for S symbols. Allocates device memory once (not per tick). */
+/* Candles in the per-message frame the tick path reproduces: the reference
+ * re-fetches KlinesProvider.LIMIT = 400 candles and re-enriches them on every
+ * closed kline (consumers/klines_provider.py:40,201-215 ->
+ * producers/context_evaluator.py:367-371), so its EMAs are seeded at the
+ * frame's first candle. */
+#define BQ_TICK_FRAME 400
+
+/* Create state for S symbols. Allocates device memory once (not per tick).
+ * bq_state_create = bq_state_create_frame(.., BQ_TICK_FRAME). `frame` = 0
+ * keeps unbounded-history EMA carries (the full-series pandas EMA) instead;
+ * otherwise BQ_MAX_WINDOW + 2 <= frame <= 2^20 (the frame holds every rolling
+ * window, so only the EMA family depends on it). */
 int bq_state_create(bq_state** st, int64_t S, const bq_params* params);
+int bq_state_create_frame(bq_state** st, int64_t S, const bq_params* params, int64_t frame);
 int bq_state_destroy(bq_state* st);
 /* Seed the state from a [S][T] history panel (T >= 1): ring of the last
- * BQ_MAX_WINDOW+2 candles and exact EMA carries at the last candle. */
+ * BQ_MAX_WINDOW+2 candles, and the last `frame` closes (frame mode) or the
+ * exact EMA carries at the last candle (frame 0). */
 int bq_state_seed(bq_state* st, const double* const* in, int64_t T, int64_t ld_in,
                   void* stream);
 /* Append one candle per symbol. new_ohlcv[BQ_NUM_INPUTS] device pointers of
  * length S; out[BQ_NUM_ENRICH_COLS] device pointers of length S (NULL skip).
+ * The outputs are the last row of indicators_enrichment over the symbol's
+ * frame (the last `frame` candles; all candles when frame = 0): ema20, ema50,
+ * macd and macd_signal bit-equal to pandas' ewm(adjust=False) over that frame.
  * A symbol without a candle this tick passes NaN in all five fields: the
  * outputs are then what pandas gives for a frame with that NaN row — EMAs
  * hold their value and decay their old weight by (1 - alpha)
@@ -151,6 +167,7 @@ int bq_state_seed(bq_state* st, const double* const* in, int64_t T, int64_t ld_i
 int bq_tick(bq_state* st, const double* const* new_ohlcv, double* const* out,
             void* stream);
 int64_t bq_state_symbols(const bq_state* st);
+int64_t bq_state_frame(const bq_state* st);   /* 0 = unbounded */
 int64_t bq_state_count(const bq_state* st);   /* candles seen per symbol */
 
 /* ---- market context (breadth / regime) ----------------------------------- */
@@ -529,6 +546,14 @@ int bq_resample_count(const int64_t* ts, const int64_t* lens, int64_t S, int64_t
 int bq_resample(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
                 const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
                 double* const* out_fields, int64_t ld_out, void* stream);
+/* bq_resample for a fixed output geometry (a captured graph sizes ld_out on
+ * the host): a row with more bins than ld_out — a gap in the candles widens
+ * the span, and pandas emits every empty bin of it — keeps its NEWEST ld_out
+ * bins (output bin b = the row's bin b + out_lens[s] - ld_out), so the last
+ * written bin is always the row's latest, the one process_data reads. */
+int bq_resample_tail(const int64_t* ts, const double* const* fields, const int32_t* aggs, int32_t nfields,
+                     const int64_t* lens, int64_t S, int64_t T, int64_t ld_in, int64_t interval_ms, int64_t* out_ts,
+                     double* const* out_fields, int64_t ld_out, void* stream);
 /*
  * Left merge of a benchmark series on the timestamp
  * (strategies/liquidation_sweep_pump.py:255-263, duplicates keep "last"):

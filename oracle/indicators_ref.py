@@ -197,6 +197,27 @@ def ema_family_panel(c, p: dict | None = None) -> dict[str, np.ndarray]:
     return {k: np.ascontiguousarray(v.to_numpy().T) for k, v in out.items()}
 
 
+def tick_frame_rows(o, h, l, c, v, t: int, frame: int = 400, p: dict | None = None) -> dict[str, np.ndarray]:
+    """What the reference computes per closed-kline message at candle t: it
+    re-fetches the last KlinesProvider.LIMIT = 400 candles
+    (consumers/klines_provider.py:40,201-215) and runs indicators_enrichment on
+    that frame (producers/context_evaluator.py:367-371); the value it reads is
+    the frame's last row. frame = 0: the whole history [0, t]."""
+    a = 0 if frame == 0 else max(0, t - frame + 1)
+    sl = slice(a, t + 1)
+    got = enrich_panel(*(np.asarray(x)[:, sl] for x in (o, h, l, c, v)), p)
+    return {k: x[:, -1] for k, x in got.items()}
+
+
+def ema_family_frame(c, t: int, frame: int = 400, p: dict | None = None) -> dict[str, np.ndarray]:
+    """ema_family_panel over each row's frame [t - frame + 1, t] (the
+    reference's per-message frame, see tick_frame_rows), last column: equal
+    bit for bit to tick_frame_rows' EMA family, for every row of a wide panel."""
+    a = 0 if frame == 0 else max(0, t - frame + 1)
+    got = ema_family_panel(np.asarray(c)[:, a : t + 1], p)
+    return {k: x[:, -1] for k, x in got.items()}
+
+
 def ewm_scalar(x, alpha: float) -> np.ndarray:
     """Pure-Python restatement of pandas' ewm(adjust=False, ignore_na=False)
     mean recursion (pandas/_libs/window/aggregations.pyx `ewm`), used to pin the
@@ -224,6 +245,22 @@ def ewm_scalar(x, alpha: float) -> np.ndarray:
         elif is_obs:
             weighted = cur
         out[i] = weighted
+    return out
+
+
+def pct_change_pad(x, periods: int = 96) -> np.ndarray:
+    """Series.pct_change(periods) under pandas 2.3.3's default
+    fill_method='pad' (the BTC 24h change, producers/context_evaluator.py:
+    427-430): forward-fill, then f / f.shift(periods) - 1. numpy restatement
+    (leading NaNs stay NaN), pinned to tests/golden/btc_change.npz."""
+    x = np.asarray(x, dtype=np.float64)
+    idx = np.where(np.isnan(x), -1, np.arange(x.size))
+    idx = np.maximum.accumulate(idx) if x.size else idx
+    f = np.where(idx >= 0, x[np.maximum(idx, 0)], np.nan)
+    out = np.full_like(f, np.nan)
+    if periods < f.size:
+        with np.errstate(divide="ignore", invalid="ignore"):
+            out[periods:] = f[periods:] / f[:-periods] - 1
     return out
 
 

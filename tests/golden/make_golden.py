@@ -47,7 +47,7 @@ Fixtures:
                         helpers; outputs recorded at 48 sampled positions per symbol
                         (panel_gen.sample_positions: last rows, tile boundary, random)
 
-Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf]
+Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf,btc_change]
 """
 
 from __future__ import annotations
@@ -166,6 +166,8 @@ def child(out_dir: Path, only: set[str] | None = None) -> None:
             leadership(out_dir)
         if "inf" in only:
             inf_windows(out_dir)
+        if "btc_change" in only:
+            btc_change(out_dir)
         return
     import numpy as np
     import pandas as pd
@@ -909,6 +911,62 @@ def store_sequence(out_dir: Path, context_dict) -> None:
     with open(out_dir / "store_sequence.json", "w") as f:
         json.dump(dict(max_bars=M, btc="BTCUSDT", ops=ops, contexts=contexts, final=final), f,
                   separators=(",", ":"), default=float)
+
+
+def btc_change(out_dir: Path) -> None:
+    """a12: the BTC 24h change exactly as ContextEvaluator.process_data forms
+    it (producers/context_evaluator.py:427-430) —
+    df_btc_15m["close"].pct_change(periods=96) * 100, read at [-1:] — on BTC
+    closes with missing values (pandas 2.3.3's default fill_method='pad'
+    forward-fills them first): NaN at the last row, at t - 96, runs across
+    both, leading NaNs reaching past t - 96, short frames, a zero close.
+    Writes btc_change.npz: <case>__close, <case>__pct (the whole series) and
+    <case>__last (the value process_data keeps)."""
+    import warnings
+
+    import numpy as np
+    import pandas as pd
+
+    rng = np.random.default_rng(20261018)
+
+    def walk(n):
+        return 30000.0 * np.exp(np.cumsum(rng.normal(0, 0.004, n)))
+
+    cases = {}
+    c = walk(400)
+    cases["clean"] = c.copy()
+    x = c.copy(); x[-1] = np.nan
+    cases["nan_last"] = x
+    x = c.copy(); x[-97] = np.nan
+    cases["nan_t96"] = x
+    x = c.copy(); x[-100:-95] = np.nan; x[-3:] = np.nan
+    cases["nan_runs_both"] = x
+    x = c.copy(); x[:310] = np.nan
+    cases["leading_past_t96"] = x
+    x = c.copy(); x[:303] = np.nan
+    cases["leading_to_t96"] = x
+    x = c.copy(); x[rng.choice(400, 60, replace=False)] = np.nan
+    cases["scattered"] = x
+    x = c[:97].copy(); x[0] = np.nan
+    cases["short97_nan_first"] = x
+    cases["short97"] = c[:97].copy()
+    cases["short96"] = c[:96].copy()
+    x = c.copy(); x[-97] = 0.0
+    cases["zero_t96"] = x
+    x = c.copy(); x[-98] = np.nan; x[-97] = np.nan; x[-150] = np.nan
+    cases["nan_t96_t97"] = x
+    out = {}
+    for name, close in cases.items():
+        df_btc_15m = pd.DataFrame({"close": close})
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", FutureWarning)   # pandas 2.3.3's pad-fill deprecation notice
+            df_pct_change = df_btc_15m["close"].pct_change(periods=96) * 100
+        last = df_pct_change[-1:].iloc[0] if not df_pct_change.empty else 0.0
+        out[f"{name}__close"] = close
+        out[f"{name}__pct"] = df_pct_change.to_numpy()
+        out[f"{name}__last"] = np.float64(last)
+    np.savez_compressed(out_dir / "btc_change.npz", **out)
+    print("btc_change.npz", len(cases), "cases, pandas", pd.__version__)
 
 
 def pd_frame(rows):

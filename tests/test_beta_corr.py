@@ -156,3 +156,46 @@ def test_kernel_tile_edges(cuda, T):
         wb, wc = ref.beta_corr_series(close[s], btc, w)
         assert_close(out["beta"][s].cpu().numpy(), wb, f"beta[{s}]", rtol=1e-8, scale=1.0)
         assert_close(out["corr"][s].cpu().numpy(), wc, f"corr[{s}]", rtol=1e-8, scale=1.0)
+
+
+# ---- a12: the BTC 24h change with pandas' default pad fill -----------------
+def _btc_change_cases():
+    z = np.load(G / "btc_change.npz")
+    names = sorted({k.split("__")[0] for k in z.files})
+    return z, names
+
+
+def test_pct_change_pad_oracle_matches_pandas_fixture():
+    """oracle.pct_change_pad == pandas 2.3.3's pct_change(96) (default pad
+    fill) on every case of tests/golden/btc_change.npz, bit for bit."""
+    z, names = _btc_change_cases()
+    assert len(names) == 12
+    for n in names:
+        got = ref.pct_change_pad(z[f"{n}__close"], 96) * 100
+        np.testing.assert_array_equal(got, z[f"{n}__pct"], err_msg=n)
+        np.testing.assert_array_equal(got[-1:], np.atleast_1d(z[f"{n}__last"]), err_msg=n)
+
+
+@pytest.mark.gpu
+def test_btc_change_pad_fill_matches_pandas_fixture(cuda):
+    """a12 on the device, bit for bit against pandas' own values: the [S, T]
+    engine.pct_change over all 400-candle cases in one panel, the drop-in
+    btc_price_change per frame, and the message cohort's btc.change_24h
+    stage (cohort.py) — NaN at the last row / at t - 96 / across both,
+    leading NaNs, short frames, a zero close."""
+    from binquant_amd import engine
+    from binquant_amd.indicators import btc_price_change
+
+    z, names = _btc_change_cases()
+    full = [n for n in names if z[f"{n}__close"].size == 400]
+    panel = torch.from_numpy(np.stack([z[f"{n}__close"] for n in full])).cuda()
+    got = (engine.pct_change(panel, 96) * 100).cpu().numpy()
+    for i, n in enumerate(full):
+        np.testing.assert_array_equal(got[i], z[f"{n}__pct"], err_msg=n)
+    for n in names:
+        v = btc_price_change(pd.DataFrame({"close": z[f"{n}__close"]}))
+        want = float(z[f"{n}__last"])
+        assert (np.isnan(v) and np.isnan(want)) or v == want, (n, v, want)
+    raw = (engine.pct_change(panel, 96, fill_method=None) * 100).cpu().numpy()
+    i = full.index("nan_t96")
+    assert np.isnan(raw[i, -1]) and not np.isnan(got[i, -1])

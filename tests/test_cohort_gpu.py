@@ -95,3 +95,44 @@ def test_cohort_branches_equal_one_stream(cuda, monkeypatch):
             if k.startswith("h1.") and x.ndim == 2:
                 x, y = x[:, :n], y[:, :n]
             np.testing.assert_array_equal(x, y, err_msg=f"{name} {k}")
+
+
+def test_cohort_h1_gap_keeps_newest_bins_and_btc_change(cuda):
+    """pandas' 1h resample emits every empty hour of a gap, so a
+    15m frame with a multi-hour gap has more bins than T15 // 4 + 2. The
+    cohort keeps each row's NEWEST bins (bq_resample_tail): h1.bins - 1 is
+    the latest hour, h1.dropped counts the oldest bins left out, and the kept
+    bins equal the tail of the full read-back resample. Also the a12 BTC
+    change with a missing close at t - 96 (pandas' pad fill)."""
+    from binquant_amd import engine
+    from binquant_amd.cohort import RESAMPLE_AGG, process_cohort
+    from oracle import indicators_ref as ref
+
+    S, T = 16, 400
+    ins = _inputs(S, T, 31)
+    ts = 1_700_000_000_000 + 900_000 * np.arange(T, dtype=np.int64)
+    ts = np.broadcast_to(ts, (S, T)).copy()
+    ts[::2, 200:] += 3_600_000 * np.arange(1, S // 2 + 1)[:, None] * 5   # gaps of 5, 10, ... hours
+    ins[10] = torch.from_numpy(ts).cuda()
+    btc = ins[12].cpu().numpy().copy()
+    btc[-97] = np.nan
+    btc[-1] = np.nan
+    ins[12] = torch.from_numpy(btc).cuda()
+    out = process_cohort(*ins)
+    B1 = T // 4 + 2
+    _, res, nb = engine.resample(ins[10], {k: ins[5 + i] for i, k in enumerate(("open", "high", "low", "close", "volume"))},
+                                 RESAMPLE_AGG, 3_600_000)
+    nb = nb.cpu().numpy()
+    assert nb.max() > B1
+    bins = out["h1.bins"].cpu().numpy()
+    drop = out["h1.dropped"].cpu().numpy()
+    np.testing.assert_array_equal(bins, np.minimum(nb, B1))
+    np.testing.assert_array_equal(drop, np.maximum(nb - B1, 0))
+    for k, v in res.items():
+        full = v.cpu().numpy()
+        got = out[f"h1.{k}"].cpu().numpy()
+        for s in range(S):
+            np.testing.assert_array_equal(got[s, : bins[s]], full[s, drop[s] : nb[s]], err_msg=f"{k}[{s}]")
+    want = ref.pct_change_pad(btc, 96)[-1] * 100
+    got = float(out["btc.change_24h"].cpu().numpy()[0])
+    assert got == want, (got, want)

@@ -1,6 +1,12 @@
-"""GPU parity of the streaming tick path (bq_state_seed + bq_tick) against
-the pandas oracle on the full series: tick t must equal row t of
-indicators_enrichment over candles [0, t]."""
+"""GPU parity of the streaming tick path (bq_state_seed + bq_tick).
+
+The reference re-fetches the last KlinesProvider.LIMIT = 400 candles and
+re-enriches that frame on every closed kline
+(consumers/klines_provider.py:40,201-215 -> producers/context_evaluator.py:
+367-371), so tick t must equal the LAST ROW of indicators_enrichment over the
+frame [t - 399, t] — the EMA family seeded at the frame's first candle. The
+default TickState (frame=400) is checked against exactly that; frame=0 (the
+unbounded-history mode) against the full series [0, t]."""
 
 import numpy as np
 import pytest
@@ -13,72 +19,129 @@ from tests.util import assert_close
 
 pytestmark = pytest.mark.gpu
 
-
-@pytest.mark.parametrize("S,T0,N", [(64, 400, 60), (8, 1, 130), (300, 150, 5)])
-def test_tick_matches_full_series(cuda, S, T0, N):
-    T = T0 + N
-    panel = numpy_panel(S, T, seed0=S + T)
-    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
-    dev = {k: torch.from_numpy(v).cuda() for k, v in panel.items()}
-    st = engine.TickState(S)
-    st.seed(*(dev[k][:, :T0] for k in ("open", "high", "low", "close", "volume")))
-    assert st.count == T0
-    price = np.abs(panel["close"]).mean(axis=1)
-    for t in range(T0, T):
-        out = st.tick([dev[k][:, t].contiguous() for k in ("open", "high", "low", "close", "volume")])
-        torch.cuda.synchronize()
-        for k in ref.CANONICAL:
-            scale = 100.0 if k in ("rsi", "mfi") else price
-            assert_close(out[k].cpu().numpy(), want[k][:, t], f"{k}@{t}", scale=scale)
-    assert st.count == T
-    # EMAs are the exact pandas recursion once seeded: bitwise equal
-    np.testing.assert_array_equal(out["ema20"].cpu().numpy(), want["ema20"][:, -1])
+FIELDS = ("open", "high", "low", "close", "volume")
+EMA_FAMILY = ("ema20", "ema50", "macd", "macd_signal")
 
 
-def _run_ticks(panel, T0, on_tick):
+def _run_ticks(panel, T0, on_tick, frame=engine.TickState.FRAME):
     dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in panel.items()}
     S, T = panel["close"].shape
-    st = engine.TickState(S)
-    st.seed(*(dev[k][:, :T0] for k in ("open", "high", "low", "close", "volume")))
+    st = engine.TickState(S, frame=frame)
+    assert st.frame == frame
+    st.seed(*(dev[k][:, :T0] for k in FIELDS))
+    assert st.count == T0
     for t in range(T0, T):
-        out = st.tick([dev[k][:, t].contiguous() for k in ("open", "high", "low", "close", "volume")])
+        out = st.tick([dev[k][:, t].contiguous() for k in FIELDS])
         torch.cuda.synchronize()
         on_tick(t, {k: v.cpu().numpy() for k, v in out.items()})
     assert st.count == T
 
 
-def test_c3_ten_thousand_symbols(cuda):
-    """BASELINE configs[2] (C3): 10 000 symbols seeded with 400 bars (the
-    MarketStateStore cap, klines_provider.py:40), 24 ticks of one candle per
-    symbol. Every column at 96 symbols spread over the panel (incl. the first
-    and last) against the per-frame pandas oracle; the EMA family (ema20,
-    ema50, macd, macd_signal) bit-exact on all 10 000 symbols at every tick."""
-    S, T0, N = 10_000, 400, 24
+@pytest.mark.parametrize("S,T0,N", [(64, 400, 60), (8, 1, 130), (300, 150, 5)])
+def test_tick_unbounded_matches_full_series(cuda, S, T0, N):
+    """frame=0: tick t equals row t of indicators_enrichment over [0, t]; the
+    EMA carries are the exact pandas recursion, bitwise."""
     T = T0 + N
-    panel = numpy_panel(S, T, seed0=3)
-    sample = np.unique(np.r_[0, S - 1, np.linspace(0, S - 1, 94).astype(int)])
-    want = ref.enrich_panel(*(panel[k][sample] for k in ("open", "high", "low", "close", "volume")))
-    ema = ref.ema_family_panel(panel["close"])
-    price = np.abs(panel["close"][sample]).mean(axis=1)
-    seen = []
+    panel = numpy_panel(S, T, seed0=S + T)
+    want = ref.enrich_panel(*(panel[k] for k in FIELDS))
+    price = np.abs(panel["close"]).mean(axis=1)
+    last = {}
 
     def check(t, out):
         for k in ref.CANONICAL:
             scale = 100.0 if k in ("rsi", "mfi") else price
-            assert_close(out[k][sample], want[k][:, t], f"{k}@{t}", scale=scale)
-        for k in ("ema20", "ema50", "macd", "macd_signal"):
-            np.testing.assert_array_equal(out[k], ema[k][:, t], err_msg=f"{k}@{t}")
+            assert_close(out[k], want[k][:, t], f"{k}@{t}", scale=scale)
+        for k in EMA_FAMILY:
+            np.testing.assert_array_equal(out[k], want[k][:, t], err_msg=f"{k}@{t}")
+        last.update(out)
+
+    _run_ticks(panel, T0, check, frame=0)
+
+
+@pytest.mark.parametrize("S,T0,N,frame", [(64, 400, 40, 400), (33, 130, 120, 128), (8, 1, 140, 128), (70, 900, 3, 700)])
+def test_tick_frame_matches_reference_frame(cuda, S, T0, N, frame):
+    """Frame mode: every column of tick t against the reference's own
+    computation for that message — indicators_enrichment over the frame
+    [t - frame + 1, t], last row — at a spread of ticks; the EMA family bit
+    for bit at every tick and symbol."""
+    T = T0 + N
+    panel = numpy_panel(S, T, seed0=5 * S + T)
+    price = np.abs(panel["close"]).mean(axis=1)
+    full_ticks = set(np.linspace(T0, T - 1, 5).astype(int).tolist())
+    seen = []
+
+    def check(t, out):
+        ema = ref.ema_family_frame(panel["close"], t, frame)
+        for k in EMA_FAMILY:
+            np.testing.assert_array_equal(out[k], ema[k], err_msg=f"{k}@{t}")
+        if t in full_ticks:
+            want = ref.tick_frame_rows(*(panel[k] for k in FIELDS), t, frame)
+            for k in ref.CANONICAL:
+                scale = 100.0 if k in ("rsi", "mfi") else price
+                assert_close(out[k], want[k], f"{k}@{t}", scale=scale)
+                if k in EMA_FAMILY:
+                    np.testing.assert_array_equal(out[k], want[k], err_msg=f"{k}@{t} vs frame enrich")
+        seen.append(t)
+
+    _run_ticks(panel, T0, check, frame=frame)
+    assert len(seen) == N
+
+
+def test_tick_frame_differs_from_full_history(cuda):
+    """The frame matters: after 400+ candles a volatile series' ema50 over the
+    400-candle frame differs from the full-history EMA by more than the 1e-9
+    tolerance (up to 7.8x) — the tick path must return the frame's."""
+    S, T0, N = 32, 1200, 2
+    panel = numpy_panel(S, T0 + N, seed0=77)
+    rng = np.random.default_rng(1)
+    panel["close"] = panel["close"] * np.exp(np.cumsum(rng.normal(0, 0.01, panel["close"].shape), axis=1))
+    got = {}
+    _run_ticks(panel, T0, lambda t, out: got.update(out))
+    t = T0 + N - 1
+    frame = ref.ema_family_frame(panel["close"], t, 400)["ema50"]
+    full = ref.ema_family_frame(panel["close"], t, 0)["ema50"]
+    np.testing.assert_array_equal(got["ema50"], frame)
+    assert np.any(np.abs(full - frame) > 1e-9 * np.abs(frame)), "fixture too tame to tell the two apart"
+
+
+def test_c3_ten_thousand_symbols(cuda):
+    """BASELINE configs[2] (C3): 10 000 symbols seeded with 400 bars (the
+    MarketStateStore cap, klines_provider.py:40), 24 ticks of one candle per
+    symbol, frame 400 (the reference's per-message frame). Every column at 96
+    symbols spread over the panel (incl. the first and last) against
+    indicators_enrichment over each message's 400-candle frame at 1e-9; the
+    EMA family (ema20, ema50, macd, macd_signal) bit-exact against pandas'
+    ewm over that frame on all 10 000 symbols at every tick."""
+    S, T0, N = 10_000, 400, 24
+    T = T0 + N
+    panel = numpy_panel(S, T, seed0=3)
+    sample = np.unique(np.r_[0, S - 1, np.linspace(0, S - 1, 94).astype(int)])
+    sub = {k: panel[k][sample] for k in FIELDS}
+    price = np.abs(panel["close"][sample]).mean(axis=1)
+    seen = []
+
+    def check(t, out):
+        want = ref.tick_frame_rows(*(sub[k] for k in FIELDS), t, 400)
+        for k in ref.CANONICAL:
+            scale = 100.0 if k in ("rsi", "mfi") else price
+            assert_close(out[k][sample], want[k], f"{k}@{t}", scale=scale)
+        ema = ref.ema_family_frame(panel["close"], t, 400)
+        for k in EMA_FAMILY:
+            np.testing.assert_array_equal(out[k], ema[k], err_msg=f"{k}@{t}")
         seen.append(t)
 
     _run_ticks(panel, T0, check)
     assert len(seen) == N
 
 
-def test_tick_nan_candles_follow_pandas(cuda):
+@pytest.mark.parametrize("frame", [0, 128])
+def test_tick_nan_candles_follow_pandas(cuda, frame):
     """A symbol without a candle in a tick (NaN in all five fields) gives what
     pandas gives for that NaN row: EMAs hold and decay their old weight
     (ewm(adjust=False, ignore_na=False)), windows containing it are NaN, RSI /
-    MFI count it as no move. Also NaN rows inside the seed history."""
+    MFI count it as no move. Also NaN rows inside the seed history; with a
+    128-candle frame, NaN rows that enter, sit at the start of, and leave the
+    frame."""
     S, T0, N = 48, 160, 140
     T = T0 + N
     panel = numpy_panel(S, T, seed0=91)
@@ -90,14 +153,25 @@ def test_tick_nan_candles_follow_pandas(cuda):
     for k in panel:   # a two-candle gap in the live ticks and one at the seed end
         panel[k][1, T0 + 30 : T0 + 32] = np.nan
         panel[k][2, T0 - 1] = np.nan
-    want = ref.enrich_panel(*(panel[k] for k in ("open", "high", "low", "close", "volume")))
+        panel[k][4, T0 + 10 - frame + 1] = np.nan   # the first candle of tick T0+10's frame
+    want = ref.enrich_panel(*(panel[k] for k in FIELDS))
     price = np.nanmean(np.abs(panel["close"]), axis=1)
 
     def check(t, out):
         for k in ref.CANONICAL:
+            if k in EMA_FAMILY and frame:
+                continue
             scale = 100.0 if k in ("rsi", "mfi") else price
             assert_close(out[k], want[k][:, t], f"{k}@{t}", scale=scale)
-        for k in ("ema20", "ema50", "macd", "macd_signal"):
-            np.testing.assert_array_equal(out[k], want[k][:, t], err_msg=f"{k}@{t}")
+        ema = ref.ema_family_frame(panel["close"], t, frame) if frame else {k: want[k][:, t] for k in EMA_FAMILY}
+        for k in EMA_FAMILY:
+            np.testing.assert_array_equal(out[k], ema[k], err_msg=f"{k}@{t}")
 
-    _run_ticks(panel, T0, check)
+    _run_ticks(panel, T0, check, frame=frame)
+
+
+def test_tick_frame_bounds():
+    with pytest.raises(ValueError):
+        engine.TickState(4, frame=100)
+    with pytest.raises(ValueError):
+        engine.TickState(4, frame=(1 << 20) + 1)
