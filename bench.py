@@ -91,6 +91,32 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args) -> int | None:
+    """`bench.py --gpus N` run by itself (no WORLD_SIZE in the environment,
+    N > 1): start N fresh child interpreters of this script, one per GPU
+    (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1 at a free
+    port), wait for all of them and return the worst exit code; rank 0
+    prints the JSON line. Called before anything touches the GPU in this
+    process (the children are new processes, not an exec of this one).
+    Returns None when this process is itself a rank."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for i in range(args.gpus):
+        env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def setup_dist(args):
     """One process per GPU, RCCL ("nccl") over xGMI. BQ_BENCH_BACKEND=gloo
     rehearses the multi-rank path on fewer GPUs (ranks share devices round-robin,
@@ -99,6 +125,10 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); "
+                         "run `bench.py --gpus N` alone (it starts N ranks) or under "
+                         "torch.distributed.run --nproc-per-node N")
     backend = os.environ.get("BQ_BENCH_BACKEND", "nccl")
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
@@ -613,6 +643,9 @@ def time_enrich(panel, steps: int, warmup: int, world: int):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     lo, hi = shard_bounds(args.symbols, world, rank)

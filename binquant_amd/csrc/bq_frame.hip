@@ -452,7 +452,11 @@ __global__ __launch_bounds__(NT, K <= 4 ? JR_WAVES : 4) void join_returns_row_ke
     const int t = k * NT + tid, g = t + off;
     int64_t g1 = __shfl_down(g0[k], 1, WAVE);
     if (lane == WAVE - 1) g1 = g + 1 < nb ? bts[g + 1] : INT64_MIN;
-    odd |= g + 1 < nb && g0[k] == g1;
+    // a repeat matters only where a candle of the row joins: lane t checks
+    // the pair (g, g + 1) around its own guess, and lane t - 1 covers
+    // (g - 1, g); lanes past the row (t >= n) do not send the row to the
+    // fixup pass for a repeat it never joins
+    odd |= t < n && g + 1 < nb && g0[k] == g1;
     const bool live = t > 0 && t < n;
     const bool hit = g < nb && g0[k] == key[k];   // unique unless odd
     j[k] = !live ? -1 : (hit ? g : -2);

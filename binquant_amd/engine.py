@@ -1151,24 +1151,45 @@ def leadership(open_time: torch.Tensor, close: torch.Tensor, bench_ts: torch.Ten
     return {"leader": leader, "rs_2h": rs2, "rs_6h": rs6}
 
 
+def _join_capacity(ts: torch.Tensor, lens: torch.Tensor | None, bts: torch.Tensor) -> int:
+    """Largest per-row count of (candle, benchmark row) matches over the
+    candles t >= 1 that join (bench_ts ascending): an upper bound on every
+    row's joined pairs (dropna only removes some)."""
+    S, T = ts.shape
+    if S == 0 or T < 2 or bts.numel() == 0:
+        return T
+    keys = ts[:, 1:].contiguous()
+    mult = torch.searchsorted(bts, keys, right=True) - torch.searchsorted(bts, keys)
+    if lens is not None:
+        live = torch.arange(1, T, device=ts.device)[None, :] < lens.reshape(-1, 1)
+        mult = torch.where(live, mult, torch.zeros_like(mult))
+    return int(mult.sum(dim=1).max().item())
+
+
 @device_entry
 def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, bench_close: torch.Tensor,
                  lens=None, capacity: int | None = None, stream: torch.cuda.Stream | None = None):
     """Aligned (symbol, benchmark) log-return pairs of
     ContextEvaluator.dynamic_btc_beta_corr (producers/context_evaluator.py:161-177):
     returns on each frame's own rows, inner join on the timestamp, dropna,
-    compacted per row. Returns (x [S, C], y [S, C], pairs per row int64 [S]),
-    C = max(T, capacity). A benchmark time held k times joins k pairs (pandas'
-    inner join), so a row can hold up to T + (repeated benchmark times) pairs:
-    pass that as `capacity` when the benchmark repeats times (a row's pairs
-    past C are cut at C)."""
+    compacted per row. Returns (x [S, C], y [S, C], pairs per row int64 [S]).
+    A benchmark time held k times joins k pairs (pandas' inner join; a frame
+    repeating its own time k_l times joins k_l * k times), so a row can hold
+    more than T pairs. capacity=None: C = the largest row's joined-row count
+    (each candle's benchmark multiplicity, summed per row, on the device: one
+    host synchronisation), so no row is ever cut. An int capacity (fixed
+    geometry, e.g. a captured graph) gives C = max(T, capacity) without the
+    synchronisation; a row with more pairs than C is then cut at C, keeping
+    its oldest pairs — size it from the benchmark's repeats."""
     ts = _check_ts(ts)
     S, T = ts.shape
     close = _check_panel(close, "close", (S, T)).contiguous()
     bts = _check_ts(bench_ts, "bench_ts").reshape(-1)
     bc = _check_panel(bench_close.reshape(1, -1), "bench_close", (1, bts.numel())).contiguous()
     lens = _check_lens(lens, S, ts.device)
-    C = max(T, int(capacity or 0))
+    if capacity is None:
+        capacity = _join_capacity(ts, lens, bts)
+    C = max(T, int(capacity))
     x = torch.empty((S, C), dtype=torch.float64, device=ts.device)
     y = torch.empty_like(x)
     n = torch.empty(S, dtype=torch.int64, device=ts.device)

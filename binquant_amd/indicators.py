@@ -256,9 +256,17 @@ def dynamic_btc_beta_corr_frames(frames: Sequence[pd.DataFrame], df_btc: pd.Data
     bts_h = pd.to_numeric(df_btc[key]).to_numpy(np.int64)
     bts = torch.from_numpy(bts_h).to(dev)
     bcl = torch.from_numpy(pd.to_numeric(df_btc["close"], errors="coerce").to_numpy(np.float64)).to(dev)
-    repeats = bts_h.size - np.unique(bts_h).size   # each repeated time can add one pair per row
+    # pairs per row: each candle t >= 1 joins every benchmark row holding its
+    # time (pandas' many-to-many inner join), so the exact bound is the sum of
+    # those multiplicities — known here on the host, no device round trip
+    cap = T
+    if bts_h.size:
+        for s, n_s in enumerate(lens):
+            if n_s > 1:
+                k = ts[s, 1:n_s]
+                cap = max(cap, int((np.searchsorted(bts_h, k, "right") - np.searchsorted(bts_h, k, "left")).sum()))
     x, y, n = engine.join_returns(torch.from_numpy(ts).to(dev), torch.from_numpy(cl).to(dev), bts, bcl, lens=lens,
-                                  capacity=T + repeats)
+                                  capacity=cap)
     bc = engine.beta_corr_pairs(x, y, window=window)
     n = n.cpu().numpy()
     last = torch.from_numpy(np.maximum(n - 1, 0)).to(dev)

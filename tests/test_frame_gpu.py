@@ -192,9 +192,10 @@ def test_joined_returns_long_rows(cuda, T, dup):
 
 def test_joined_returns_capacity(cuda):
     """Every benchmark time held three times: a row joins up to 3 (T - 1)
-    pairs. With the default capacity (T) the row is cut at T pairs (the
-    oracle's first T); with capacity T + repeats it holds all of them, and
-    the drop-in dynamic_btc_beta_corr_frames sizes it that way itself."""
+    pairs. The default capacity (None) sizes the output from the rows'
+    benchmark multiplicities and holds all of them; a fixed capacity of T
+    cuts the row at T pairs (the oracle's first T); the drop-in
+    dynamic_btc_beta_corr_frames sizes it exactly itself."""
     from binquant_amd.indicators import dynamic_btc_beta_corr_frames
 
     rng = np.random.default_rng(5)
@@ -209,16 +210,46 @@ def test_joined_returns_capacity(cuda):
     assert k > T
     args = (torch.from_numpy(ts).cuda(), torch.from_numpy(close).cuda(), torch.from_numpy(bts).cuda(),
             torch.from_numpy(bclose).cuda())
-    x, y, n = engine.join_returns(*args)
+    x, y, n = engine.join_returns(*args, capacity=T)
     assert x.shape == (1, T) and int(n[0]) == T
     assert_close(x[0].cpu().numpy(), r["alt"].to_numpy()[:T], "alt cut", rtol=1e-14)
     assert_close(y[0].cpu().numpy(), r["btc"].to_numpy()[:T], "btc cut", rtol=1e-14)
-    cap = T + bts.size - np.unique(bts).size
-    x, y, n = engine.join_returns(*args, capacity=cap)
-    assert x.shape == (1, cap) and int(n[0]) == k
+    x, y, n = engine.join_returns(*args)
+    cap = x.shape[1]
+    assert cap == 3 * (T - 1) and int(n[0]) == k
     assert_close(x[0, :k].cpu().numpy(), r["alt"].to_numpy(), "alt", rtol=1e-14)
     assert_close(y[0, :k].cpu().numpy(), r["btc"].to_numpy(), "btc", rtol=1e-14)
     assert torch.isnan(x[0, k:]).all() and torch.isnan(y[0, k:]).all()
+    df = pd.DataFrame({"open_time": ts[0], "close": close[0]})
+    df_btc = pd.DataFrame({"open_time": bts, "close": bclose})
+    beta, corr = dynamic_btc_beta_corr_frames([df], df_btc, window=50, decimals=None)[0]
+    wb, wc = fref.beta_corr_series(r, 50)
+    assert abs(beta - wb[-1]) <= 1e-9 * abs(wb[-1]) and abs(corr - wc[-1]) <= 1e-9
+
+
+def test_joined_returns_many_to_many(cuda):
+    """a frame repeating its own open_time k_l times against a
+    benchmark time held k_r times joins k_l * k_r pairs (pandas'
+    many-to-many inner join). The default capacity holds them all, and the
+    drop-in's beta / corr at the last joined row equals the oracle's."""
+    from binquant_amd.indicators import dynamic_btc_beta_corr_frames
+
+    rng = np.random.default_rng(9)
+    base = 1_700_000_000_000
+    nb, T = 160, 140
+    bt = base + M15 * np.arange(nb)
+    bts = np.sort(np.r_[bt, bt[40:60], bt[40:50], bt[-3:]])
+    bclose = 30000 * np.exp(np.cumsum(rng.normal(0, 0.003, bts.size)))
+    own = base + M15 * (np.arange(T) + 10)
+    ts = np.sort(np.r_[own, own[35:45], own[-2:]])[None]
+    close = 10 * np.exp(np.cumsum(rng.normal(0, 0.004, ts.shape), axis=1))
+    r = fref.joined_returns(ts[0], close[0], bts, bclose)
+    k = len(r)
+    x, y, n = engine.join_returns(torch.from_numpy(ts).cuda(), torch.from_numpy(close).cuda(),
+                                  torch.from_numpy(bts).cuda(), torch.from_numpy(bclose).cuda())
+    assert int(n[0]) == k and x.shape[1] >= k > ts.shape[1]
+    assert_close(x[0, :k].cpu().numpy(), r["alt"].to_numpy(), "alt", rtol=1e-14)
+    assert_close(y[0, :k].cpu().numpy(), r["btc"].to_numpy(), "btc", rtol=1e-14)
     df = pd.DataFrame({"open_time": ts[0], "close": close[0]})
     df_btc = pd.DataFrame({"open_time": bts, "close": bclose})
     beta, corr = dynamic_btc_beta_corr_frames([df], df_btc, window=50, decimals=None)[0]
