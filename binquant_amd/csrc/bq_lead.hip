@@ -39,7 +39,10 @@
 namespace bq {
 
 #ifndef LD_TILE
-#define LD_TILE 256
+#define LD_TILE 1024
+#endif
+#ifndef LD_UNROLL
+#define LD_UNROLL 5
 #endif
 constexpr int LD_NT = LD_TILE;
 constexpr int LD_W = 96;                 // RS_LOOKBACK (compiled)
@@ -63,6 +66,7 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
   __shared__ double sC[LD_CH + LD_NT], sB[LD_CH + LD_NT];
   __shared__ double2 sH[LD_HH + LD_NT];   // (rs_2h, rs_6h) entries: one 16-byte LDS read per walk step
   __shared__ uint64_t sPos[(LD_CH + LD_NT + WAVE - 1) / WAVE];   // bit: close and benchmark close > 0
+  __shared__ uint64_t sVal[(LD_HH + LD_NT + WAVE - 1) / WAVE];    // bit: a history entry exists
   const int tid = threadIdx.x;
   const int64_t s = blockIdx.y;
   const int t0 = blockIdx.x * LD_NT;
@@ -78,8 +82,26 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     if (t >= 0 && t < T) {
       c = cl[t];
       const int64_t key = ts[t];
-      const int j = lower_bound_guess(A.bts, nb, key + 1, bt0, bstep) - 1;   // the last row with this time
-      if (j >= 0 && A.bts[j] == key) b = A.bclose[j];
+      // the last benchmark row with this time: on a regular grid the guessed
+      // row's time, its successor's and its close are loaded together (one
+      // dependent round trip after the candle's time); the search otherwise
+      int jg = -1;
+      if (bstep > 0 && key >= bt0) {
+        const int64_t q = (key - bt0) / bstep;
+        jg = q < nb ? (int)q : -1;
+      }
+      bool hit = false;
+      if (jg >= 0) {
+        const int64_t tg = A.bts[jg];
+        const int64_t tn = jg + 1 < nb ? A.bts[jg + 1] : INT64_MAX;
+        const double bg = A.bclose[jg];
+        hit = tg == key && tn != key;
+        if (hit) b = bg;
+      }
+      if (!hit) {
+        const int j = lower_bound_guess(A.bts, nb, key + 1, bt0, bstep) - 1;
+        if (j >= 0 && A.bts[j] == key) b = A.bclose[j];
+      }
     }
     sC[i] = c;
     sB[i] = b;
@@ -96,6 +118,9 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     // the reference's float arithmetic c / c[-9] - b / b[-9] (:179-180)
     const bool pos = c0 > 0.0 && c2 > 0.0 && c6 > 0.0 && b0 > 0.0 && b2 > 0.0 && b6 > 0.0;
     sH[i] = make_double2(pos ? c0 / c2 - b0 / b2 : qnan(), pos ? c0 / c6 - b0 / b6 : qnan());
+    // the entry exists iff pos (both strengths are then numbers: finite > 0 closes)
+    const uint64_t vm = __ballot(pos);   // slots i - lane .. i - lane + 63
+    if ((tid & (WAVE - 1)) == 0) sVal[i / WAVE] = vm;
   }
   __syncthreads();
   const int t = t0 + tid;
@@ -113,9 +138,15 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
       gate = gate && (wl == wh ? (sPos[wh] & (hi_mask & lo_mask)) == (hi_mask & lo_mask)
                                : (sPos[wl] & lo_mask) == lo_mask && (sPos[wh] & hi_mask) == hi_mask);
     }
-    const double c0 = sC[k], b0 = sB[k];
-    const double r2 = c0 / sC[k - shrt] - b0 / sB[k - shrt];   // (:150-153)
-    const double r6 = c0 / sC[k - lng] - b0 / sB[k - lng];
+    // (:150-153) c / c[-shrt - 1] - b / b[-shrt - 1]: the gate (every close of
+    // the last lng + 1 candles > 0) makes candle t's history entry exist, and
+    // the entry is that same expression
+    double r2 = 0.0, r6 = 0.0;
+    if (gate) {
+      const double2 e = sH[LD_HH + tid];
+      r2 = e.x;
+      r6 = e.y;
+    }
     const int64_t o = s * A.ld_out + t;
     A.rs[0][o] = gate ? r2 : 0.0;   // (False, 0.0, 0.0) when the strengths are None (:160-161)
     A.rs[1][o] = gate ? r6 : 0.0;
@@ -144,30 +175,24 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
   __syncthreads();
   if (tid >= total) return;
   const int u0 = 2 * sList[tid], u1 = u0 + 1;
-  const bool a0 = sAct[u0], a1 = sAct[u1];
-  // the same strengths, recomputed (a candle of the pair that does not walk
-  // is counted and dropped)
-  const double r20 = sC[LD_CH + u0] / sC[LD_CH + u0 - shrt] - sB[LD_CH + u0] / sB[LD_CH + u0 - shrt];
-  const double r60 = sC[LD_CH + u0] / sC[LD_CH + u0 - lng] - sB[LD_CH + u0] / sB[LD_CH + u0 - lng];
-  const double r21 = sC[LD_CH + u1] / sC[LD_CH + u1 - shrt] - sB[LD_CH + u1] / sB[LD_CH + u1 - shrt];
-  const double r61 = sC[LD_CH + u1] / sC[LD_CH + u1 - lng] - sB[LD_CH + u1] / sB[LD_CH + u1 - lng];
-  // the window of the last LD_W positions (:170): entries counted, and how
-  // many are <= the current strengths; the gate implies the entry at t exists
-  // (it equals r2 / r6). Entry h1 - d is candle u1's d-th and u0's (d - 1)-th.
+  // the strengths are the candles' own history entries (the gate implies
+  // they exist; a candle of the pair that does not walk is counted and dropped)
+  const double2 q0 = sH[LD_HH + u0], q1 = sH[LD_HH + u1];
+  const double r20 = q0.x, r60 = q0.y, r21 = q1.x, r61 = q1.y;
+  // the window of the last LD_W positions (:170): how many entries are <=
+  // the current strengths (a missing entry is NaN: never <=). Entry h1 - d is
+  // candle u1's d-th (d = 0 .. LD_W - 1) and u0's (d - 1)-th: one read per
+  // step serves both.
   const int h1 = LD_HH + u1;
-  int n0 = 0, c20 = 0, c60 = 0, n1, c21, c61;
+  int c20 = 0, c60 = 0, c21, c61;
   {
     const double2 e = sH[h1];
-    n1 = e.x == e.x ? 1 : 0;
-    c21 = e.x <= r21 ? 1 : 0;   // NaN: no entry, not counted
+    c21 = e.x <= r21 ? 1 : 0;
     c61 = e.y <= r61 ? 1 : 0;
   }
-#pragma unroll 5
+#pragma unroll LD_UNROLL
   for (int d = 1; d < LD_W; ++d) {
     const double2 e = sH[h1 - d];
-    const int v = e.x == e.x ? 1 : 0;
-    n1 += v;
-    n0 += v;
     c21 += e.x <= r21 ? 1 : 0;
     c61 += e.y <= r61 ? 1 : 0;
     c20 += e.x <= r20 ? 1 : 0;
@@ -175,17 +200,29 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
   }
   {
     const double2 e = sH[h1 - LD_W];
-    n0 += e.x == e.x ? 1 : 0;
     c20 += e.x <= r20 ? 1 : 0;
     c60 += e.y <= r60 ? 1 : 0;
   }
+  // entry counts from the existence bitmask: slots [h - LD_W + 1, h]
+  auto entries = [&](int h) {   // lo >= 0: the halo covers the window
+    const int lo = h - (LD_W - 1);
+    int n = 0;
+    for (int wd = lo / WAVE; wd <= h / WAVE; ++wd) {
+      uint64_t m = sVal[wd];
+      if (wd == lo / WAVE) m &= ~0ull << (lo & (WAVE - 1));
+      if (wd == h / WAVE) m &= ~0ull >> (WAVE - 1 - (h & (WAVE - 1)));
+      n += __popcll(m);
+    }
+    return n;
+  };
+  const int n0 = entries(h1 - 1), n1 = entries(h1);
   // sorted(h)[int((n - 1) q)] <= rs  <=>  #{h <= rs} >= int((n - 1) q) + 1 (:183-193)
   const int64_t o = s * A.ld_out + t0;
-  if (a0) {
+  if (sAct[u0]) {
     const int need = (int)((double)(n0 - 1) * A.q) + 1;
     A.leader[o + u0] = n0 >= A.minc && c20 >= need && c60 >= need ? 1 : 0;
   }
-  if (a1) {
+  if (sAct[u1]) {
     const int need = (int)((double)(n1 - 1) * A.q) + 1;
     A.leader[o + u1] = n1 >= A.minc && c21 >= need && c61 >= need ? 1 : 0;
   }
