@@ -58,7 +58,7 @@ rows = {
                                            {"open": "first", "high": "max", "low": "min", "close": "last",
                                             "volume": "sum"}, 3_600_000),
     "align": lambda: engine.align(ts, ts[0], btc),
-    "join_returns": lambda: engine.join_returns(ts, c, ts[0], btc),
+    "join_returns": lambda: engine.join_returns(ts, c, ts[0], btc, capacity=T),
 }
 res = {}
 for name, fn in rows.items():

@@ -43,7 +43,7 @@ calls = {
     "a20_zscore": lambda: signals.zscore(c),
     "a20_leadership": lambda: signals.gradual_gainer_leadership(ts, c, ts[0], btc),
     "supertrend": lambda: engine.supertrend(h, l, c, exact=False),
-    "f4_btc_join_returns": lambda: engine.join_returns(ts, c, ts[0], btc),
+    "f4_btc_join_returns": lambda: engine.join_returns(ts, c, ts[0], btc, capacity=T),
 }
 # input bytes read per candle; the algorithmic bytes add every returned output
 # at its dtype (bench.py output_bytes)
