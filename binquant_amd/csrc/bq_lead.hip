@@ -39,12 +39,12 @@
 namespace bq {
 
 #ifndef LD_TILE
-#define LD_TILE 1024
+#define LD_TILE 2048   // candles per workgroup tile (1 024: 0.52-0.53 ms, 2 048: 0.44-0.45 at 12.5k x 2k)
 #endif
-#ifndef LD_UNROLL
-#define LD_UNROLL 5
-#endif
-constexpr int LD_NT = LD_TILE;
+constexpr int LD_TT = LD_TILE;
+constexpr int LD_NT = LD_TT < 1024 ? LD_TT : 1024;   // threads
+constexpr int LD_CPT = LD_TT / LD_NT;                // candles per thread (gate phase)
+static_assert(LD_TT % LD_NT == 0 && LD_TT / 2 <= LD_NT, "a thread per walking pair");
 constexpr int LD_W = 96;                 // RS_LOOKBACK (compiled)
 constexpr int LD_LMAX = 31;              // the long offset's bound (RS 6h: 24)
 constexpr int LD_HH = LD_W - 1;          // history halo before the tile
@@ -63,20 +63,20 @@ struct LeadArgs {
 };
 
 __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
-  __shared__ double sC[LD_CH + LD_NT], sB[LD_CH + LD_NT];
-  __shared__ double2 sH[LD_HH + LD_NT];   // (rs_2h, rs_6h) entries: one 16-byte LDS read per walk step
-  __shared__ uint64_t sPos[(LD_CH + LD_NT + WAVE - 1) / WAVE];   // bit: close and benchmark close > 0
-  __shared__ uint64_t sVal[(LD_HH + LD_NT + WAVE - 1) / WAVE];    // bit: a history entry exists
+  __shared__ double sC[LD_CH + LD_TT], sB[LD_CH + LD_TT];
+  __shared__ double2 sH[LD_HH + LD_TT];   // (rs_2h, rs_6h) entries: one 16-byte LDS read per walk step
+  __shared__ uint64_t sPos[(LD_CH + LD_TT + WAVE - 1) / WAVE];   // bit: close and benchmark close > 0
+  __shared__ uint64_t sVal[(LD_HH + LD_TT + WAVE - 1) / WAVE];    // bit: a history entry exists
   const int tid = threadIdx.x;
   const int64_t s = blockIdx.y;
-  const int t0 = blockIdx.x * LD_NT;
+  const int t0 = blockIdx.x * LD_TT;
   const int T = A.T, nb = A.nb, shrt = A.shrt, lng = A.lng;
   const int64_t* __restrict__ ts = A.ts + s * A.ld_ts;
   const double* __restrict__ cl = A.close + s * A.ld_c;
-  // 1. closes and benchmark closes of candles t0 - LD_CH .. t0 + LD_NT - 1
+  // 1. closes and benchmark closes of candles t0 - LD_CH .. t0 + LD_TT - 1
   const int64_t bt0 = A.bts[0];
   const int64_t bstep = nb > 1 ? (A.bts[nb - 1] - bt0) / (nb - 1) : 0;
-  for (int i = tid; i < LD_CH + LD_NT; i += LD_NT) {
+  for (int i = tid; i < LD_CH + LD_TT; i += LD_NT) {
     const int t = t0 - LD_CH + i;
     double c = qnan(), b = qnan();
     if (t >= 0 && t < T) {
@@ -109,8 +109,8 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     if ((tid & (WAVE - 1)) == 0) sPos[i / WAVE] = pm;
   }
   __syncthreads();
-  // 2. history entries of candles t0 - LD_HH .. t0 + LD_NT - 1 (none outside the row)
-  for (int i = tid; i < LD_HH + LD_NT; i += LD_NT) {
+  // 2. history entries of candles t0 - LD_HH .. t0 + LD_TT - 1 (none outside the row)
+  for (int i = tid; i < LD_HH + LD_TT; i += LD_NT) {
     const int k = i + LD_LMAX;   // the candle's slot in sC / sB
     const double c0 = sC[k], c2 = sC[k - shrt], c6 = sC[k - lng];
     const double b0 = sB[k], b2 = sB[k - shrt], b6 = sB[k - lng];
@@ -123,53 +123,57 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     if ((tid & (WAVE - 1)) == 0) sVal[i / WAVE] = vm;
   }
   __syncthreads();
-  const int t = t0 + tid;
   const int lane = tid & (WAVE - 1), w = tid / WAVE;
-  // 3. _relative_strengths: the last lng + 1 times present, every close > 0
-  //    (:143-149); len(df) >= MIN_HISTORY (:160)
-  bool act = false;
-  if (t < T) {
-    const int k = LD_CH + tid;
-    bool gate = t + 1 >= A.min_hist && t >= lng;
-    {   // slots k - lng .. k all positive (lng < 64: at most two mask words)
-      const int lo = k - lng, wl = lo / WAVE, wh = k / WAVE;
-      const uint64_t hi_mask = ~0ull >> (WAVE - 1 - (k & (WAVE - 1)));   // bits 0 .. k % 64
-      const uint64_t lo_mask = ~0ull << (lo & (WAVE - 1));                // bits lo % 64 .. 63
-      gate = gate && (wl == wh ? (sPos[wh] & (hi_mask & lo_mask)) == (hi_mask & lo_mask)
-                               : (sPos[wl] & lo_mask) == lo_mask && (sPos[wh] & hi_mask) == hi_mask);
+  // 3. per candle u of the tile (LD_CPT per thread): _relative_strengths — the
+  //    last lng + 1 times present, every close > 0 (:143-149); len(df) >=
+  //    MIN_HISTORY (:160)
+  constexpr int NP = LD_TT / 2;
+  __shared__ unsigned char sAct[LD_TT];
+  __shared__ int sList[NP], sWc[LD_NT / WAVE];
+#pragma unroll
+  for (int q = 0; q < LD_CPT; ++q) {
+    const int u = q * LD_NT + tid, t = t0 + u;
+    bool act = false;
+    if (t < T) {
+      const int k = LD_CH + u;
+      bool gate = t + 1 >= A.min_hist && t >= lng;
+      {   // slots k - lng .. k all positive (lng < 64: at most two mask words)
+        const int lo = k - lng, wl = lo / WAVE, wh = k / WAVE;
+        const uint64_t hi_mask = ~0ull >> (WAVE - 1 - (k & (WAVE - 1)));   // bits 0 .. k % 64
+        const uint64_t lo_mask = ~0ull << (lo & (WAVE - 1));                // bits lo % 64 .. 63
+        gate = gate && (wl == wh ? (sPos[wh] & (hi_mask & lo_mask)) == (hi_mask & lo_mask)
+                                 : (sPos[wl] & lo_mask) == lo_mask && (sPos[wh] & hi_mask) == hi_mask);
+      }
+      // (:150-153) c / c[-shrt - 1] - b / b[-shrt - 1]: the gate (every close
+      // of the last lng + 1 candles > 0) makes candle t's history entry exist,
+      // and the entry is that same expression
+      double r2 = 0.0, r6 = 0.0;
+      if (gate) {
+        const double2 e = sH[LD_HH + u];
+        r2 = e.x;
+        r6 = e.y;
+      }
+      const int64_t o = s * A.ld_out + t;
+      A.rs[0][o] = gate ? r2 : 0.0;   // (False, 0.0, 0.0) when the strengths are None (:160-161)
+      A.rs[1][o] = gate ? r6 : 0.0;
+      // otherwise the method's answer is False whatever the thresholds
+      act = gate && r2 > 0.0 && r6 > 0.0;
+      if (!act) A.leader[o] = 0;
     }
-    // (:150-153) c / c[-shrt - 1] - b / b[-shrt - 1]: the gate (every close of
-    // the last lng + 1 candles > 0) makes candle t's history entry exist, and
-    // the entry is that same expression
-    double r2 = 0.0, r6 = 0.0;
-    if (gate) {
-      const double2 e = sH[LD_HH + tid];
-      r2 = e.x;
-      r6 = e.y;
-    }
-    const int64_t o = s * A.ld_out + t;
-    A.rs[0][o] = gate ? r2 : 0.0;   // (False, 0.0, 0.0) when the strengths are None (:160-161)
-    A.rs[1][o] = gate ? r6 : 0.0;
-    // otherwise the method's answer is False whatever the thresholds
-    act = gate && r2 > 0.0 && r6 > 0.0;
-    if (!act) A.leader[o] = 0;
+    sAct[u] = act;
   }
   // the window walks, two neighbouring candles per thread (their windows
   // share 95 of 96 entries: one LDS read serves both), the pairs that need
   // one packed into the tile's first waves (the others' waves skip it)
-  constexpr int NP = LD_NT / 2;
-  __shared__ unsigned char sAct[LD_NT];
-  __shared__ int sList[NP], sWc[LD_NT / WAVE];
-  sAct[tid] = act;
   __syncthreads();
   const bool pa = tid < NP && (sAct[2 * tid] | sAct[2 * tid + 1]);
   const uint64_t m = __ballot(pa);
   if (lane == 0) sWc[w] = __popcll(m);
   __syncthreads();
   int base = 0, total = 0;
-  for (int u = 0; u < LD_NT / WAVE; ++u) {
-    base += u < w ? sWc[u] : 0;
-    total += sWc[u];
+  for (int v = 0; v < LD_NT / WAVE; ++v) {
+    base += v < w ? sWc[v] : 0;
+    total += sWc[v];
   }
   if (pa) sList[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = tid;
   __syncthreads();
@@ -190,7 +194,7 @@ __global__ __launch_bounds__(LD_NT) void lead_kernel(const LeadArgs A) {
     c21 = e.x <= r21 ? 1 : 0;
     c61 = e.y <= r61 ? 1 : 0;
   }
-#pragma unroll LD_UNROLL
+#pragma unroll 5   // (1 / 10 / 19: equal or slower)
   for (int d = 1; d < LD_W; ++d) {
     const double2 e = sH[h1 - d];
     c21 += e.x <= r21 ? 1 : 0;
@@ -245,7 +249,7 @@ extern "C" int bq_leadership(const int64_t* open_time, int64_t ld_ts, const doub
   (void)workspace;
   (void)workspace_bytes;
   if (!open_time || !close || !leader || !rs_2h || !rs_6h || S < 0 || T < 0 || ld_ts < T || ld_c < T ||
-      ld_out < T || T > 0x7fffffff - 2 * LD_NT || S > 0x7fffffff || nb < 0 || nb > 0x7fffffff)
+      ld_out < T || T > 0x7fffffff - 2 * LD_TT || S > 0x7fffffff || nb < 0 || nb > 0x7fffffff)
     return BQ_EINVAL;
   if (lookback != LD_W || !(rs_quantile >= 0.0 && rs_quantile < 1.0) || short_bars < 1 || long_bars < short_bars ||
       long_bars > LD_LMAX || min_count < 1 || min_history < 0)
@@ -281,6 +285,6 @@ extern "C" int bq_leadership(const int64_t* open_time, int64_t ld_ts, const doub
   A.rs[0] = rs_2h;
   A.rs[1] = rs_6h;
   A.leader = leader;
-  hipLaunchKernelGGL(lead_kernel, dim3((unsigned)((T + LD_NT - 1) / LD_NT), (unsigned)S), dim3(LD_NT), 0, st, A);
+  hipLaunchKernelGGL(lead_kernel, dim3((unsigned)((T + LD_TT - 1) / LD_TT), (unsigned)S), dim3(LD_NT), 0, st, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
