@@ -175,3 +175,28 @@ def test_tick_frame_bounds():
         engine.TickState(4, frame=100)
     with pytest.raises(ValueError):
         engine.TickState(4, frame=(1 << 20) + 1)
+
+
+@pytest.mark.parametrize("frame", [0, 128])
+def test_tick_without_seed(cuda, frame):
+    """A state that was never seeded starts at candle 0 (count 0): every tick
+    is the last row of the frame (or the full series) so far."""
+    S, T = 20, 300
+    panel = numpy_panel(S, T, seed0=123)
+    dev = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in panel.items()}
+    st = engine.TickState(S, frame=frame)
+    assert st.count == 0
+    price = np.abs(panel["close"]).mean(axis=1)
+    full = ref.enrich_panel(*(panel[k] for k in FIELDS))
+    for t in range(T):
+        out = {k: v.cpu().numpy() for k, v in st.tick([dev[k][:, t].contiguous() for k in FIELDS]).items()}
+        ema = ref.ema_family_frame(panel["close"], t, frame)
+        for k in EMA_FAMILY:
+            np.testing.assert_array_equal(out[k], ema[k], err_msg=f"{k}@{t}")
+        if t % 37 == 0 or t == T - 1:
+            for k in ref.CANONICAL:
+                if k in EMA_FAMILY:
+                    continue
+                scale = 100.0 if k in ("rsi", "mfi") else price
+                assert_close(out[k], full[k][:, t], f"{k}@{t}", scale=scale)
+    assert st.count == T
