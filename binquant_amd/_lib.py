@@ -204,7 +204,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_breadth_partial": (ctypes.c_int, [_P, _PP, _I64, _I64, _I64, _I64, _P, _P]),
     "bq_context_workspace_bytes": (ctypes.c_size_t, [_I64, _I64]),
     "bq_context_partials": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _P, ctypes.c_size_t, _P, _PP, _P]),
-    "bq_pump_ewm": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _I64, _P]),
+    "bq_pump_ewm": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _P, _I64, _P]),
     "bq_leadership_workspace_bytes": (ctypes.c_size_t, [_I64, _I64]),
     "bq_leadership": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, ctypes.c_double, _I32, _I32, _I32,
                                      _I32, _I32, _P, ctypes.c_size_t, _P, _P, _P, _I64, _P]),

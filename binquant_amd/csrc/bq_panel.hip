@@ -379,40 +379,261 @@ void launch_panel(const PanelBatch& B, int n, hipStream_t st) {
   if (nt) hipLaunchKernelGGL(panel_ewm_kernel<true>, dim3((unsigned)B.S, (unsigned)nt), dim3(PN_NT), 0, st, etr);
 }
 
+// LiquidationSweepPump's three ewm columns in ONE pass per row
+// (bq_pump_ewm): high / low / close loaded once, the true range formed from
+// them, and the three series scanned side by side on the same tiles —
+// panel_ewm_kernel's map scan + exact replay per series (series 1 and 2 share
+// the close values; pandas' recursion on thread 0 for a series from the first
+// tile with a missing / infinite value, one series at a time through sX).
+// trend_score = (ema20 - ema50) / ema50 (liquidation_sweep_pump.py:254, the
+// staged program's operation) leaves with them when asked, so the pump pass
+// does not read the two ema columns back.
+struct PumpEwmArgs {
+  const double *h, *l, *c;
+  double* out[3];   // atr, ema20, ema50
+  double* trend;    // NULL: skip
+  int64_t ld_in, ld_out;
+  int T, vin, vout;
+  double alpha[3];
+  int minp[3];
+};
+
+// 256 threads x 8 candles (the panel kernels' 2 048-candle tile and lane maps:
+// the same association as panel_ewm_kernel, so the same bits), the series one
+// after another, the serial state in LDS: 111 VGPRs, 4 waves per SIMD. At
+// 12.5k x 2k 0.257 ms against 0.31 / 0.30 for 512 x 4 at 4 / 8 waves per SIMD
+// and 0.27 for the two panel_ewm launches it replaces (tools/ab_kernel.sh).
+#ifndef BQ_P3_K
+#define BQ_P3_K 8
+#endif
+#ifndef BQ_P3_WPS
+#define BQ_P3_WPS 4
+#endif
+constexpr int P3_K = BQ_P3_K;
+constexpr int P3_NT = 2048 / P3_K;
+constexpr int P3_NW = P3_NT / WAVE;
+constexpr int P3_TT = P3_NT * P3_K;
+
+__device__ __forceinline__ void p3_load(const double* __restrict__ row, int tb, int T, bool vec, double (&x)[P3_K]) {
+  if (vec && tb + P3_K <= T) {
+    const pn_dbl2* p = reinterpret_cast<const pn_dbl2*>(row + tb);
+#pragma unroll
+    for (int j = 0; j < P3_K / 2; ++j) {
+      const pn_dbl2 a = p[j];
+      x[2 * j] = a.x;
+      x[2 * j + 1] = a.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < P3_K; ++k) x[k] = tb + k < T ? row[tb + k] : qnan();
+  }
+}
+
+__global__ __launch_bounds__(P3_NT, BQ_P3_WPS) void pump_ewm3_kernel(const PumpEwmArgs A) {
+  __shared__ double sA[P3_NW], sB[P3_NW];
+  __shared__ double sCarry[3];
+  __shared__ double sX[P3_TT];   // the serial replay's tile (one series at a time)
+  __shared__ double sWv[3], sOwt[3];   // pandas' state of a serial series (thread 0)
+  __shared__ int sNobs[3];
+  const int64_t row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
+  const double* __restrict__ xh = A.h + row * A.ld_in;
+  const double* __restrict__ xl = A.l + row * A.ld_in;
+  const double* __restrict__ xc = A.c + row * A.ld_in;
+  const int64_t orow = row * A.ld_out;
+  const int T = A.T;
+  const bool vin = A.vin != 0, vout = A.vout != 0;
+  if (tid < 3) {
+    sCarry[tid] = 0.0;
+    sWv[tid] = qnan();
+    sOwt[tid] = 1.0;
+    sNobs[tid] = 0;
+  }
+  unsigned serial = 0;   // bit e: series e runs pandas' recursion (block-uniform)
+  for (int t0 = 0; t0 < T; t0 += P3_TT) {
+    const int tb = t0 + P3_K * tid;
+    // loaded at the tile start, not a tile ahead: registers are occupancy
+    // here, and a row of up to 2 048 candles is one tile anyway
+    double v[2][P3_K];   // the true range; the close (+-inf: missing)
+    {
+      double nh[P3_K], nl[P3_K], nc[P3_K];
+      p3_load(xh, tb, T, vin, nh);
+      p3_load(xl, tb, T, vin, nl);
+      p3_load(xc, tb, T, vin, nc);
+      double pc = tb >= 1 && tb <= T ? xc[tb - 1] : qnan();
+#pragma unroll
+      for (int k = 0; k < P3_K; ++k) {
+        v[0][k] = tb + k < T ? win_val(true_range(nh[k], nl[k], pc)) : qnan();
+        v[1][k] = win_val(nc[k]);
+        pc = nc[k];
+      }
+    }
+    {
+      int b0 = 0, b1 = 0;
+#pragma unroll
+      for (int k = 0; k < P3_K; ++k) {
+        b0 |= (tb + k < T) && !(v[0][k] - v[0][k] == 0.0);
+        b1 |= (tb + k < T) && !(v[1][k] - v[1][k] == 0.0);
+      }
+      const unsigned bad = (__syncthreads_or(b0) ? 1u : 0u) | (__syncthreads_or(b1) ? 6u : 0u);
+      const unsigned turn = bad & ~serial;   // these series turn serial here
+      if (turn && tid == 0 && t0 > 0)        // candles 0 .. t0 - 1 were all observations
+        for (int e = 0; e < 3; ++e)
+          if ((turn >> e) & 1) {
+            sWv[e] = sCarry[e];
+            sNobs[e] = t0;
+          }
+      serial |= bad;
+    }
+    double r20[P3_K];
+    // one series at a time: the lane maps over its candles from the zero
+    // state (candle 0 resets), their wave scans, the waves' totals through
+    // LDS, then each lane's exact replay (or pandas' recursion on thread 0)
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const double al = A.alpha[e], om = 1.0 - al, den = om + al;
+      const bool div = den != 1.0;
+      const double* c = v[e == 0 ? 0 : 1];
+      double res[P3_K];
+      if ((serial >> e) & 1) {
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) sX[P3_K * tid + k] = c[k];
+        __syncthreads();
+        if (tid == 0) {
+          const int n = min(P3_TT, T - t0);
+          double y = sWv[e], ow = sOwt[e];
+          int no = sNobs[e];
+          for (int i = 0; i < n; ++i) {
+            const double cur = sX[i];
+            const bool obs = cur == cur;
+            if (t0 + i == 0) {   // pandas: weighted = vals[0], nobs = its observation
+              y = cur;
+              no = obs ? 1 : 0;
+            } else {
+              no += obs ? 1 : 0;
+              if (y == y) {
+                ow *= om;
+                if (obs) {
+                  if (y != cur) {
+                    y = ow * y + al * cur;
+                    y /= ow + al;
+                  }
+                  ow = 1.0;
+                }
+              } else if (obs) {
+                y = cur;
+              }
+            }
+            sX[i] = no >= A.minp[e] ? y : qnan();
+          }
+          sWv[e] = y;
+          sOwt[e] = ow;
+          sNobs[e] = no;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) res[k] = sX[P3_K * tid + k];
+        __syncthreads();   // sX free for the next series
+      } else {
+        const double la = om / den, lb = al / den;
+        double a_ = 1.0, b_ = 0.0;
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) {
+          if (tb + k == 0) {
+            a_ = 0.0;
+            b_ = c[k];
+          } else {
+            a_ *= la;
+            b_ = fma(la, b_, lb * c[k]);
+          }
+        }
+        double sa = a_, sb = b_;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+          const double pa = __shfl_up(sa, d, WAVE), pbv = __shfl_up(sb, d, WAVE);
+          if (lane >= d) {
+            sb = fma(sa, pbv, sb);
+            sa *= pa;
+          }
+        }
+        if (lane == WAVE - 1) {
+          sA[w] = sa;
+          sB[w] = sb;
+        }
+        double ea = __shfl_up(sa, 1, WAVE), eb = __shfl_up(sb, 1, WAVE);
+        if (lane == 0) {
+          ea = 1.0;
+          eb = 0.0;
+        }
+        __syncthreads();
+        double y = sCarry[e];
+        for (int u = 0; u < w; ++u) y = fma(sA[u], y, sB[u]);
+        y = fma(ea, y, eb);
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) {   // exact replay of the lane's steps
+          const int t = tb + k;
+          const double x = c[k];
+          if (t == 0) y = x;
+          else if (y != x) {
+            y = om * y + al * x;
+            if (div) y = y / den;
+          }
+          res[k] = t + 1 >= A.minp[e] ? y : qnan();
+        }
+        __syncthreads();   // sA / sB (and sCarry[e]) read by every wave
+        if (tid == P3_NT - 1) sCarry[e] = y;   // the next tile's carry (nothing reads it before then)
+      }
+      store_lines<P3_K>(A.out[e] + orow, tb, T, vout, res);   // each column leaves as formed
+      if (e == 1) {
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) r20[k] = res[k];
+      }
+      if (e == 2 && A.trend) {
+#pragma unroll
+        for (int k = 0; k < P3_K; ++k) r20[k] = (r20[k] - res[k]) / res[k];
+        store_lines<P3_K>(A.trend + orow, tb, T, vout, r20);
+      }
+    }
+  }
+}
+
 }  // namespace bq
 
 // LiquidationSweepPump's per-symbol ewm columns in panel mode
-// (liquidation_sweep_pump.py:206-217, 252-253): candidate_atr =
-// TR.ewm(alpha = 1/14, min_periods = 14), ema20 / ema50 of close — the true
-// range formed from the high / low / close loads (no TR column in HBM).
+// (liquidation_sweep_pump.py:206-217, 252-254): candidate_atr =
+// TR.ewm(alpha = 1/14, min_periods = 14), ema20 / ema50 of close and, when
+// asked, trend_score — one pass per row (pump_ewm3_kernel).
 extern "C" int bq_pump_ewm(const double* high, const double* low, const double* close, int64_t S, int64_t T,
-                           int64_t ld_in, double* atr, double* ema20, double* ema50, int64_t ld_out, void* stream) {
+                           int64_t ld_in, double* atr, double* ema20, double* ema50, double* trend_score,
+                           int64_t ld_out, void* stream) {
   using namespace bq;
   if (!high || !low || !close || !atr || !ema20 || !ema50 || S < 0 || T < 0 || ld_in < T || ld_out < T ||
-      S > 0x7fffffff || T > 0x7fffffff - 2 * PN_TT)
+      S > 0x7fffffff || T > 0x7fffffff - 2 * P3_TT)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;
-  PanelBatch B;
-  memset(&B, 0, sizeof(B));
-  B.S = S;
-  B.T = (int)T;
+  PumpEwmArgs A;
+  memset(&A, 0, sizeof(A));
+  A.h = high;
+  A.l = low;
+  A.c = close;
+  A.out[0] = atr;
+  A.out[1] = ema20;
+  A.out[2] = ema50;
+  A.trend = trend_score;
+  A.ld_in = ld_in;
+  A.ld_out = ld_out;
+  A.T = (int)T;
+  auto aligned = [](const void* p, int64_t ld) { return (((uintptr_t)p) & 15u) == 0 && (ld % 2) == 0; };
+  A.vin = aligned(high, ld_in) && aligned(low, ld_in) && aligned(close, ld_in);
+  A.vout = aligned(atr, ld_out) && aligned(ema20, ld_out) && aligned(ema50, ld_out) &&
+           (!trend_score || aligned(trend_score, ld_out));
   // pandas: alpha = 1 / (1 + com), com = 1 / alpha - 1 or (span - 1) / 2
   const double coms[3] = {1.0 / (1.0 / 14.0) - 1.0, (20.0 - 1.0) / 2.0, (50.0 - 1.0) / 2.0};
   const int minp[3] = {14, 0, 0};
-  double* outs[3] = {atr, ema20, ema50};
   for (int i = 0; i < 3; ++i) {
-    PanelJob& J = B.j[i];
-    J.x = close;
-    J.out = outs[i];
-    J.ld_in = ld_in;
-    J.ld_out = ld_out;
-    J.rows = S;
-    J.mode = BQ_ROLL_EWM;
-    J.minp = minp[i];
-    J.alpha = 1.0 / (1.0 + coms[i]);
-    J.hi = i == 0 ? high : nullptr;
-    J.lo = i == 0 ? low : nullptr;
+    A.alpha[i] = 1.0 / (1.0 + coms[i]);
+    A.minp[i] = minp[i];
   }
-  launch_panel(B, 3, (hipStream_t)stream);
+  hipLaunchKernelGGL(pump_ewm3_kernel, dim3((unsigned)S), dim3(P3_NT), 0, (hipStream_t)stream, A);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }

@@ -150,8 +150,13 @@ __global__ __launch_bounds__(PF_NT, EWM_IN ? 2 : 3) void pump_features_kernel(co
     for (int f = 0; f < NP; ++f) pf_load(A.in[f] + irow, tb, T, vin, x[f]);
     if (!EWM_IN) {
       pf_load(A.in[PF_ATR_IN] + irow, tb, T, vin, atr);
-      pf_load(A.in[PF_E20_IN] + irow, tb, T, vin, e20);
-      pf_load(A.in[PF_E50_IN] + irow, tb, T, vin, e50);
+      if (A.in[PF_E20_IN]) {   // NULL: trend_score came with the ewm columns (bq_pump_ewm)
+        pf_load(A.in[PF_E20_IN] + irow, tb, T, vin, e20);
+        pf_load(A.in[PF_E50_IN] + irow, tb, T, vin, e50);
+      } else {
+#pragma unroll
+        for (int k = 0; k < PF_K; ++k) e20[k] = e50[k] = qnan();
+      }
     }
     const double pv0 = tb >= 1 && tb <= T ? A.in[PF_V_IN][irow + tb - 1] : qnan();
     // ---- phase A: ring, run starts of the volume, last valid close (and the
@@ -451,7 +456,10 @@ extern "C" int bq_pump_features(const double* const* in, int64_t S, int64_t T, i
   PumpArgs A;
   memset(&A, 0, sizeof(A));
   for (int f = 0; f < PF_NIN; ++f) {
-    if (!in[f]) return BQ_EINVAL;
+    // ema20 / ema50 may both be NULL when no column reads them
+    const bool opt = (f == PF_E20_IN || f == PF_E50_IN) && !out[BQ_PUMP_EMA20] && !out[BQ_PUMP_EMA50] &&
+                     !out[BQ_PUMP_TREND_SCORE] && !in[PF_E20_IN] && !in[PF_E50_IN];
+    if (!in[f] && !opt) return BQ_EINVAL;
     A.in[f] = in[f];
   }
   for (int i = 0; i < 3; ++i)
@@ -474,7 +482,8 @@ extern "C" int bq_pump_features(const double* const* in, int64_t S, int64_t T, i
   A.comp_w = compression_bars;
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
   int vin = (ld_in % 2) == 0, vout = (ld_out % 2) == 0;
-  for (int f = 0; f < PF_NIN; ++f) vin &= aligned(in[f]);
+  for (int f = 0; f < PF_NIN; ++f)
+    if (in[f]) vin &= aligned(in[f]);
   for (int c = 0; c < BQ_NUM_PUMP_COLS; ++c)
     if (out[c]) vout &= aligned(out[c]);
   hipLaunchKernelGGL(pump_features_kernel<false>, dim3((unsigned)S), dim3(PF_NT), 0, (hipStream_t)stream, A, vin,

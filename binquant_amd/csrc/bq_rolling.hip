@@ -843,6 +843,138 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
   }
 }
 
+// ---- slide rank kernel, lane groups (w >= 48) -----------------------------------------
+// slide_rank_kernel's sorted window split over G = 2 or 4 adjacent lanes:
+// lane q of a group holds slots q H .. q H + H - 1 (H = W / G), so a lane
+// holds 1/G of the registers and a SIMD two to four waves instead of one at
+// w = 80 / 96 — the single-lane step is a dependent compare -> select -> min
+// -> max chain per slot that one wave per SIMD cannot hide. The group's lanes
+// read the same leaving / entering values (the same addresses: one
+// transaction) and keep the same count n and placeholder split B(n). A step
+// is the same removal / insertion per slot; the two values that cross a lane
+// boundary go by one DPP quad permutation each: the upper neighbour's old
+// bottom slot (the successor of this lane's top slot) before the step, the
+// lower neighbour's top removal result b[H - 1] (the predecessor of this
+// lane's bottom clamp) after the removal pass, so slot 0 is clamped last.
+// The placeholders are split from the first step (no barrel shift): a
+// warm-up step is a full step. The rank slots K, K + 1 lie in one lane
+// (static_assert), which alone stores. Same multiset, same slots, same
+// arithmetic: the outputs equal slide_rank_kernel's bit for bit.
+template <int G>
+__device__ __forceinline__ double from_upper(double x) {   // lane q <- lane q + 1 of the group
+  return dpp_f64<G == 2 ? 0xB1 : 0xF9>(x);                  // quad_perm [1,0,3,2] / [1,2,3,3]
+}
+template <int G>
+__device__ __forceinline__ double from_lower(double x) {   // lane q <- lane q - 1 of the group
+  return dpp_f64<G == 2 ? 0xB1 : 0x90>(x);                  // quad_perm [1,0,3,2] / [0,0,1,2]
+}
+
+template <int W, int K, bool MED, int G>
+__global__ __launch_bounds__(256) void slide_group_kernel(const RollBatch B) {
+  constexpr int H = W / G;
+  constexpr int KL = K / H;   // the lane holding the rank slots
+  static_assert((G == 2 || G == 4) && W % G == 0 && (K + 1) / H == KL && K + 1 < W, "group layout");
+  constexpr int SL_C = 8;
+  const RollJob& A = B.j[blockIdx.y];
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int q = threadIdx.x & (G - 1);
+  const int64_t item = gid / G;
+  const int64_t sym = item % B.S;
+  const int seg = (int)(item / B.S);
+  if (seg >= A.nseg) return;   // a group leaves together (no barriers below)
+  const double* __restrict__ x = A.x + sym * A.ld_in;
+  double* __restrict__ out = A.out + sym * A.ld_out;
+  const int T = B.T, sh = A.shift;
+  const int t_begin = seg * A.seg, t_end = min(T, t_begin + A.seg);
+  const int t_start = max(0, t_begin - W + 1);
+  const double inf = __builtin_inf();
+  auto load_chunk = [&](int ts, double (&v)[SL_C]) {
+    const int i0 = ts - sh;
+    if (i0 >= 0 && i0 + SL_C <= T) {
+#pragma unroll
+      for (int j = 0; j < SL_C; j += 2) {
+        const dbl2u p = *reinterpret_cast<const dbl2u*>(x + i0 + j);
+        v[j] = p.x;
+        v[j + 1] = p.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j) v[j] = (i0 + j >= 0 && i0 + j < T) ? x[i0 + j] : qnan();
+    }
+  };
+  auto a_of = [&](int nn) -> int {
+    if constexpr (MED) return (nn - 1) >> 1;
+    else return (int)(A.q * (double)(nn - 1));
+  };
+  auto b_of = [&](int nn) -> int { return nn >= 1 ? K - a_of(nn) : K + 1; };
+  const bool top = q == G - 1, bottom = q == 0;
+  // the empty window: B(0) = K + 1 bottom placeholders, the rest on top
+  double s[H];
+#pragma unroll
+  for (int i = 0; i < H; ++i) s[i] = q * H + i < K + 1 ? -inf : inf;
+  int n = 0, nb = K + 1;
+  // steps from t_start (the W - 1 before the segment fill the window), in
+  // chunks aligned to t_begin so the output chunks are the single-lane ones
+  const int tw = t_begin - ((t_begin - t_start + SL_C - 1) / SL_C) * SL_C;
+  for (int tc = tw; tc < t_end; tc += SL_C) {
+    double vin[SL_C], vout[SL_C], r[SL_C];
+    load_chunk(tc, vin);
+    if (tc + SL_C - 1 - W >= t_start) load_chunk(tc - W, vout);   // else: placeholders leave
+#pragma unroll
+    for (int j = 0; j < SL_C; ++j) {
+      const int t = tc + j;
+      const bool live = t >= t_start && t < t_end;   // steps outside: no-ops (+inf out, +inf in)
+      const bool has_out = t - W >= t_start;
+      const bool in_num = live && win_ok(vin[j]);
+      const bool out_num = live && has_out && win_ok(vout[j]);
+      const int n2 = n + (in_num ? 1 : 0) - (out_num ? 1 : 0);
+      const int nb2 = b_of(n2);
+      const double o = out_num ? vout[j] + 0.0 : (nb2 < nb ? -inf : inf);
+      const double v = in_num ? vin[j] + 0.0 : (nb2 > nb ? -inf : inf);
+      n = n2;
+      nb = nb2;
+      const double up = from_upper<G>(s[0]);   // the old slot above this lane's top one
+      const double b0 = s[0] < o ? s[0] : (H > 1 ? s[1 < H ? 1 : 0] : (top ? inf : up));
+      double bp = b0;
+#pragma unroll
+      for (int i = 1; i < H; ++i) {
+        const double nxt = i + 1 < H ? s[i + 1 < H ? i + 1 : i] : (top ? inf : up);
+        const double b = s[i] < o ? s[i] : nxt;
+        s[i] = max_f64_nn(bp, min_f64_nn(v, b));
+        bp = b;
+      }
+      const double dn = from_lower<G>(bp);     // the removal result below this lane's bottom slot
+      s[0] = max_f64_nn(bottom ? -inf : dn, min_f64_nn(v, b0));
+      r[j] = qnan();
+      if (n >= A.minp && n > 0) {
+        constexpr int KS = K - KL * H, KS1 = K + 1 - KL * H;
+        const double lo = s[KS];
+        if constexpr (MED) {
+          r[j] = (n & 1) ? lo : (lo + s[KS1]) / 2.0;
+        } else {
+          const double idxf = A.q * (double)(n - 1);
+          const int idx = (int)idxf;
+          r[j] = ((double)idx == idxf || A.lower) ? lo : lo + (s[KS1] - lo) * (idxf - (double)idx);
+        }
+      }
+    }
+    if (q != KL || tc < t_begin) continue;
+    if (tc + SL_C <= t_end) {
+#pragma unroll
+      for (int j = 0; j < SL_C; j += 2) {
+        dbl2u p;
+        p.x = r[j];
+        p.y = r[j + 1];
+        *reinterpret_cast<dbl2u*>(out + tc + j) = p;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j)
+        if (tc + j < t_end) out[tc + j] = r[j];
+    }
+  }
+}
+
 // ---- tile rank kernel (wave = 64*OPL consecutive outputs of one symbol) --------------
 // The windows of TILE consecutive outputs all lie in one union of
 // U = w + TILE - 1 consecutive values. The wave loads the union (coalesced:
@@ -1382,6 +1514,12 @@ struct SlideCfg {
 #ifndef BQ_SLIDE_BIG
 #define BQ_SLIDE_BIG 1   // 0: w = 80 / 96 on the tile kernel (measurement)
 #endif
+#ifndef BQ_SLIDE_PAIR_DEFAULT
+#define BQ_SLIDE_PAIR_DEFAULT 80   // smallest window on slide_group_kernel (0: none)
+#endif
+#ifndef BQ_SLIDE_GROUP_DEFAULT
+#define BQ_SLIDE_GROUP_DEFAULT 2   // lanes per window there
+#endif
 constexpr SlideCfg kSlide[] = {{19, 9, 1}, {48, 37, 0}, {60, 50, 0}
 #if BQ_SLIDE_BIG
                                , {80, 72, 0}, {96, 76, 0}
@@ -1406,13 +1544,32 @@ int slide_variant(int w, int mode, double q) {
 // BQ_SLIDE_WAVES waves per SIMD over 1024 SIMDs (the kernel is VALU-bound and
 // every slot update is independent, so a few waves hide its loads); each
 // segment replays W - 1 warm-up values, so segments stay >= 2 W
+// lanes per window of the slide kernel: 1, or BQ_SLIDE_GROUP (2 / 4) for
+// windows >= BQ_SLIDE_PAIR_MIN (0: never) — slide_group_kernel
+int slide_pair_min() {
+  static const int v = [] {
+    const char* e = getenv("BQ_SLIDE_PAIR_MIN");
+    return e ? atoi(e) : BQ_SLIDE_PAIR_DEFAULT;
+  }();
+  return v;
+}
+int slide_group(int w) {
+  static const int g = [] {
+    const char* e = getenv("BQ_SLIDE_GROUP");
+    const int v = e ? atoi(e) : BQ_SLIDE_GROUP_DEFAULT;
+    return v == 4 ? 4 : 2;
+  }();
+  return slide_pair_min() > 0 && w >= slide_pair_min() && w % g == 0 ? g : 1;
+}
+
 int slide_segment(int w, int64_t S, int64_t T) {
   static const int waves = [] {
     const char* e = getenv("BQ_SLIDE_WAVES");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 2;
   }();
-  const int64_t lanes = (int64_t)1024 * waves * 64;
+  // a window on a lane group: 1/G of the items for the same lanes
+  const int64_t lanes = (int64_t)1024 * waves * 64 / slide_group(w);
   const int64_t nseg = lanes / (S > 0 ? S : 1) > 1 ? lanes / (S > 0 ? S : 1) : 1;
   int64_t seg = (T + nseg - 1) / nseg;
   if (seg < 2 * w) seg = 2 * w;
@@ -1421,6 +1578,17 @@ int slide_segment(int w, int64_t S, int64_t T) {
 
 template <int W, int K, bool MED>
 void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
+  if constexpr (W % 4 == 0 && K / (W / 2) == (K + 1) / (W / 2) && K / (W / 4) == (K + 1) / (W / 4) && K + 1 < W) {
+    const int g = slide_group(W);
+    if (g > 1) {   // G lanes per item
+      const unsigned blocks = (unsigned)((g * items + 255) / 256);
+      if (g == 2)
+        hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 2>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+      else
+        hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 4>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+      return;
+    }
+  }
   const unsigned blocks = (unsigned)((items + 255) / 256);
   hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }

@@ -309,28 +309,41 @@ def pump_features(
     volume_lookback: int = 20,
     compression_bars: int = 6,
     stream: torch.cuda.Stream | None = None,
+    trend_score: torch.Tensor | None = None,
 ) -> dict[str, torch.Tensor]:
     """LiquidationSweepPump.compute_pump_score's columns but the two rolling
     quantiles and score_cross (strategies/liquidation_sweep_pump.py:195-268) in
     one pass per row (bq_pump_features): the volume mean, the high / low
     windows and the pad-filled pct_change formed in the kernel. The ewm columns
     (candidate_atr, ema20, ema50) and the benchmark rows ([T]: ffilled close,
-    ewm 20, ewm 50) are inputs."""
+    ewm 20, ewm 50) are inputs; the returned ewm columns ARE those input
+    tensors (the kernel does not write a copy: 24 B per candle less).
+    trend_score: the column already formed with the ewm columns (bq_pump_ewm);
+    then the kernel reads neither ema column back and returns it as given."""
     close = _check_panel(close, "close")
     S, T = close.shape
     ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in
            zip((high, low, close, volume, candidate_atr, ema20, ema50),
                ("high", "low", "close", "volume", "candidate_atr", "ema20", "ema50"))]
+    if trend_score is not None:
+        trend_score = _check_panel(trend_score, "trend_score", (S, T))
     bench = []
     for t, n in zip((bench_ffill, bench_ema20, bench_ema50), ("bench_ffill", "bench_ema20", "bench_ema50")):
         if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float64 or t.numel() != T:
             raise ValueError(f"{n}: expected a float64 CUDA tensor of {T} values")
         bench.append(t.reshape(T).contiguous())
-    out = {n: torch.empty((S, T), dtype=torch.float64, device=close.device) for n in PUMP_COLUMNS}
+    given = {"candidate_atr": ins[4], "ema20": ins[5], "ema50": ins[6]}
+    if trend_score is not None:
+        given["trend_score"] = trend_score
+    out = {n: given[n] if n in given else torch.empty((S, T), dtype=torch.float64, device=close.device)
+           for n in PUMP_COLUMNS}
+    iptr = [t.data_ptr() for t in ins]
+    if trend_score is not None:
+        iptr[5] = iptr[6] = 0   # not read
     st = _lib.load().bq_pump_features(
-        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, _lib.ptr_array([t.data_ptr() for t in bench]),
+        _lib.ptr_array(iptr), S, T, T, _lib.ptr_array([t.data_ptr() for t in bench]),
         int(momentum_bars), int(volume_lookback), int(compression_bars),
-        _lib.ptr_array([out[n].data_ptr() for n in PUMP_COLUMNS]), T, _stream_handle(stream),
+        _lib.ptr_array([0 if n in given else out[n].data_ptr() for n in PUMP_COLUMNS]), T, _stream_handle(stream),
     )
     _lib.check(st, "bq_pump_features")
     return out
@@ -374,17 +387,18 @@ def pump_features_ewm(
 
 @device_entry
 def pump_ewm(high: torch.Tensor, low: torch.Tensor, close: torch.Tensor,
-             stream: torch.cuda.Stream | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+             stream: torch.cuda.Stream | None = None, trend: bool = False) -> tuple[torch.Tensor, ...]:
     """LiquidationSweepPump's candidate_atr (TR.ewm(alpha=1/14, min_periods=14))
-    and ema20 / ema50 of close in panel mode (bq_pump_ewm: the true range
-    formed in the kernel; liquidation_sweep_pump.py:206-217, 252-253)."""
+    and ema20 / ema50 of close in panel mode, one pass per row (bq_pump_ewm:
+    the true range formed in the kernel; liquidation_sweep_pump.py:206-217,
+    252-253); trend=True adds trend_score = (ema20 - ema50) / ema50 (:254)."""
     close = _check_panel(close, "close").contiguous()
     S, T = close.shape
     high = _check_panel(high, "high", (S, T)).contiguous()
     low = _check_panel(low, "low", (S, T)).contiguous()
-    outs = [torch.empty((S, T), dtype=torch.float64, device=close.device) for _ in range(3)]
-    st = _lib.load().bq_pump_ewm(_ptr(high), _ptr(low), _ptr(close), S, T, T, *(_ptr(o) for o in outs), T,
-                                 _stream_handle(stream))
+    outs = [torch.empty((S, T), dtype=torch.float64, device=close.device) for _ in range(4 if trend else 3)]
+    st = _lib.load().bq_pump_ewm(_ptr(high), _ptr(low), _ptr(close), S, T, T, *(_ptr(o) for o in outs[:3]),
+                                 _ptr(outs[3] if trend else None), T, _stream_handle(stream))
     _lib.check(st, "bq_pump_ewm")
     return tuple(outs)
 

@@ -334,9 +334,9 @@ def _pump_score_fused(h, l, c, v, bench, p: PumpParams) -> dict[str, torch.Tenso
         st = engine.pump_features_ewm(h, l, c, v, bf[0], be20[0], be50[0], p.momentum_bars, p.volume_lookback,
                                       p.compression_bars)
     else:
-        atr, e20, e50 = engine.pump_ewm(h, l, c)
+        atr, e20, e50, trend = engine.pump_ewm(h, l, c, trend=True)
         st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
-                                  p.volume_lookback, p.compression_bars)
+                                  p.volume_lookback, p.compression_bars, trend_score=trend)
     thr_s, thr_v = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)
         R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
         R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1), exact=False,

@@ -352,11 +352,12 @@ int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, i
  * within rounding of pandas; strategies/liquidation_sweep_pump.py:206-217,
  * :252-253): atr = TR.ewm(alpha=1/14, adjust=False, min_periods=14).mean() of
  * the true range of (high, low, close) — formed in the kernel, no TR column —
- * and ema20 / ema50 = close.ewm(span=20 / 50, adjust=False).mean(). Inputs
- * [S][ld_in], outputs [S][ld_out] fp64. Feeds bq_pump_features.
+ * and ema20 / ema50 = close.ewm(span=20 / 50, adjust=False).mean(), in one
+ * pass per row; trend_score (NULL = skip) = (ema20 - ema50) / ema50 (:254).
+ * Inputs [S][ld_in], outputs [S][ld_out] fp64. Feeds bq_pump_features.
  */
 int bq_pump_ewm(const double* high, const double* low, const double* close, int64_t S, int64_t T, int64_t ld_in,
-                double* atr, double* ema20, double* ema50, int64_t ld_out, void* stream);
+                double* atr, double* ema20, double* ema50, double* trend_score, int64_t ld_out, void* stream);
 
 /* ---- whole-series order statistics and label cooldown ---------------------- */
 /*
@@ -386,7 +387,8 @@ int bq_cooldown(const uint8_t* label, int64_t S, int64_t T, int64_t ld_in, int32
  * high / low .shift(1).rolling(compression_bars).max() / .min() windows and
  * close.pct_change(momentum_bars) (pad-filled) formed in the kernel.
  * in = {high, low, close, volume, candidate_atr, ema20, ema50} [S][ld_in]
- * fp64 (the three ewm columns from bq_rolling_batch); bench = {ffilled
+ * fp64 (the three ewm columns from bq_pump_ewm; ema20 / ema50 may both be
+ * NULL when out[BQ_PUMP_EMA20 / EMA50 / TREND_SCORE] are NULL); bench = {ffilled
  * benchmark close, its ewm(span=20), ewm(span=50)} [T] fp64 (the benchmark
  * left-merged on the panel's open_time grid); out[BQ_NUM_PUMP_COLS] [S][ld_out]
  * fp64 (NULL = skip). momentum_bars <= 31, volume_lookback and

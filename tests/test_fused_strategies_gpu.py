@@ -281,3 +281,37 @@ def test_pump_ewm_in_pass_against_pandas(cuda, S, T):
                 np.testing.assert_array_equal(x[~fin & ~np.isnan(y)], y[~fin & ~np.isnan(y)], err_msg=name)
                 sc = float(np.max(np.abs(y[fin]))) if fin.any() else 1.0
                 assert np.all(np.abs(x[fin] - y[fin]) <= 1e-12 * np.abs(y[fin]) + 1e-13 * sc), name
+
+
+@pytest.mark.parametrize("S,T", [(9, 3100), (5, 2048), (3, 7)])
+def test_pump_ewm_one_pass_equals_panel_ewm(cuda, S, T):
+    """bq_pump_ewm's one-pass kernel (the three series on the same tiles)
+    against the generic panel ewm (bq_rolling_batch, panel mode) bit for bit
+    — ema20 / ema50 of close and the ATR of the true range — including rows
+    that turn serial in one series only (a NaN high: the true range; an
+    infinite close: both emas; a late listing), and trend_score bit-equal to
+    the staged (ema20 - ema50) / ema50."""
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    E = engine.Ewm
+    p = numpy_panel(S, T, seed0=3 * S + T, edges=False)
+    h, l, c = (p[k].copy() for k in ("high", "low", "close"))
+    if T > 3000:
+        h[0, 700] = np.nan
+        c[1, 2100] = np.inf
+        h[2, :2500] = l[2, :2500] = c[2, :2500] = np.nan
+        c[3, 10:20] = np.nan
+    d = [torch.from_numpy(x).cuda() for x in (h, l, c)]
+    atr, e20, e50, trend = engine.pump_ewm(*d, trend=True)
+    pc = np.concatenate([np.full((S, 1), np.nan), c[:, :-1]], axis=1)
+    tr = np.fmax(np.fmax(h - l, np.abs(h - pc)), np.abs(l - pc))
+    w_atr, w20, w50 = engine.rolling_many(E(torch.from_numpy(tr).cuda(), alpha=1 / 14, min_periods=14),
+                                          E(d[2], span=20), E(d[2], span=50), exact=False)
+    for name, x, y in (("atr", atr, w_atr), ("ema20", e20, w20), ("ema50", e50, w50)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy(), err_msg=name)
+    np.testing.assert_array_equal(trend.cpu().numpy(), ((e20 - e50) / e50).cpu().numpy())
+    a3 = engine.pump_ewm(*d)
+    assert len(a3) == 3
+    for x, y in zip(a3, (atr, e20, e50)):
+        np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())

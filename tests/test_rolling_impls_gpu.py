@@ -1,7 +1,7 @@
 """Both kernel families behind each rolling statistic give the same bits:
 the per-lane sorted window (a run-time and a register-resident compile-time
-window) vs the per-wave sorted union vs the per-output sorting network
-(order statistics),
+window, the latter on one lane or split over a lane pair) vs the per-wave
+sorted union vs the per-output sorting network (order statistics),
 the LDS-ring replay vs the class-specialised re-staging replay (moments, ewm,
 ffill). Each implementation is forced in its own child process
 (BQ_RANK_IMPL / BQ_REPLAY_IMPL) over the same battery — NaN gaps, constant
@@ -33,7 +33,11 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
         "lane_ring": _run(tmp_path, "lane_ring", {"BQ_RANK_IMPL": "lane", "BQ_REPLAY_IMPL": "ring"}),
         "tile_restage": _run(tmp_path, "tile_restage", {"BQ_RANK_IMPL": "tile", "BQ_REPLAY_IMPL": "restage"}),
         "stencil_mixed": _run(tmp_path, "stencil_mixed", {"BQ_RANK_IMPL": "stencil", "BQ_REPLAY_IMPL": "mixed"}),
-        "slide": _run(tmp_path, "slide", {"BQ_RANK_IMPL": "slide"}),
+        "slide": _run(tmp_path, "slide", {"BQ_RANK_IMPL": "slide", "BQ_SLIDE_PAIR_MIN": "0"}),
+        "slide_pair": _run(tmp_path, "slide_pair", {"BQ_RANK_IMPL": "slide", "BQ_SLIDE_PAIR_MIN": "48",
+                                                    "BQ_SLIDE_GROUP": "2"}),
+        "slide_quad": _run(tmp_path, "slide_quad", {"BQ_RANK_IMPL": "slide", "BQ_SLIDE_PAIR_MIN": "48",
+                                                    "BQ_SLIDE_GROUP": "4"}),
         "restage64": _run(tmp_path, "restage64", {"BQ_REPLAY_IMPL": "restage", "BQ_REPLAY_SPW": "64"}),
         "mixed32": _run(tmp_path, "mixed32", {"BQ_REPLAY_IMPL": "mixed", "BQ_REPLAY_SPW": "32"}),
         "auto": _run(tmp_path, "auto", {}),
