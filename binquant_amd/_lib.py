@@ -210,6 +210,8 @@ SIGNATURES: dict[str, tuple] = {
                                      _I32, _I32, _P, ctypes.c_size_t, _P, _P, _P, _I64, _P]),
     "bq_beta_corr": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
     "bq_rolling": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _I32, _I32, _I32, ctypes.c_double, _P, _I64, _P]),
+    "bq_rolling_quantile_cross": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _I32, _I32, ctypes.c_double, _P, _I64,
+                                                 _P, _I64, _P]),
     "bq_ewm": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _I32, _P, _I64, _P]),
     "bq_row_quantile": (ctypes.c_int, [_P, _I64, _I64, _I64, ctypes.c_double, _P, _P]),
     "bq_cooldown": (ctypes.c_int, [_P, _I64, _I64, _I64, _I32, _P, _P, _I64, _P]),
@@ -236,6 +238,8 @@ SIGNATURES: dict[str, tuple] = {
                                                  _P, _P]),
     "bq_store_gather": (ctypes.c_int, [ctypes.POINTER(BqStoreView), _P, _I64, _P, _PP, _I64, _P]),
     "bq_rolling_batch": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _P]),
+    "bq_rolling_batch_cross": (ctypes.c_int, [ctypes.POINTER(BqRollJob), _I32, _I64, _I64, _PP,
+                                              ctypes.POINTER(ctypes.c_int64), _P]),
     "bq_fused_eval": (ctypes.c_int, [ctypes.POINTER(BqFusedProgram), _I64, _I64, _P]),
     "bq_fused_set_native": (ctypes.c_int, [_I32]),
     "bq_fused_set_cache_dir": (ctypes.c_int, [ctypes.c_char_p]),

@@ -71,6 +71,8 @@ struct RollJob {
   int lower;   // BQ_ROLL_QLOWER: the quantile's lower order statistic, no interpolation
   double q, alpha;
   int64_t rows;   // this job's rows (<= the batch's S; a benchmark row beside a panel)
+  uint8_t* cross;    // slide kernel only (bq_rolling_quantile_cross): NULL, or [S][ld_cross]
+  int64_t ld_cross;  // (x[t] >= out[t]) & (x[t-1] < out[t-1])
 };
 
 struct RollBatch {
@@ -702,7 +704,7 @@ __device__ __forceinline__ double max_f64_nn(double a, double b) {
 // 8-byte-aligned pairs of doubles: one 16-byte access (rows are 8-byte aligned)
 typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
 
-template <int W, int K, bool MED>
+template <int W, int K, bool MED, bool XC = false>
 __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
   // steps per chunk: each lane reads / writes 8 * SL_C contiguous bytes
   // (16 for short windows: 0.27 -> 0.22 ms at w = 19; 8 where registers bind)
@@ -716,7 +718,13 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
   double* __restrict__ out = A.out + sym * A.ld_out;
   const int T = B.T, sh = A.shift;
   const int t_begin = seg * A.seg, t_end = min(T, t_begin + A.seg);
-  const int t_start = max(0, t_begin - W + 1);
+  // with the crossing flags the window of step t_begin - 1 is built too (its
+  // oldest value enters the warm-up and leaves at t_begin): the flag at
+  // t_begin needs that step's threshold
+  // the flags: an instantiation of its own (their registers); a job of that
+  // launch without them skips them (block-uniform)
+  const bool xc = XC && A.cross != nullptr;
+  const int t_start = max(0, t_begin - W + (xc ? 0 : 1));
   const double inf = __builtin_inf();
   // values of steps ts .. ts + SL_C - 1 (x[t - shift], NaN outside the row):
   // a lane's whole span at once, so every line it touches is used up
@@ -787,9 +795,31 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
 #pragma unroll
     for (int i = W - 1; i >= 0; --i) s[i] = sh_on ? (i >= bit ? s[i - bit] : -inf) : s[i];
   }
+  // the order statistic of the window in s holding n numbers
+  auto rank_value = [&]() -> double {
+    if (!(n >= A.minp && n > 0)) return qnan();
+    constexpr int K1 = K + 1 < W ? K + 1 : K;
+    const double lo = s[K];
+    if constexpr (MED) {
+      return (n & 1) ? lo : (lo + s[K1]) / 2.0;
+    } else {
+      const double idxf = A.q * (double)(n - 1);
+      const int idx = (int)idxf;
+      return ((double)idx == idxf || A.lower) ? lo : lo + (s[K1] - lo) * (idxf - (double)idx);
+    }
+  };
+  // crossing flags: the previous step's series value and threshold (NaN
+  // before the row: pandas' shift(1), and NaN compares false)
+  double pthr = qnan(), pps = qnan();
+  if (xc && t_begin >= 1) {
+    pthr = rank_value();
+    pps = x[t_begin - 1];
+  }
   for (int tc = t_begin; tc < t_end; tc += SL_C) {
-    double vin[SL_C], vout[SL_C], r[SL_C];
+    double vin[SL_C], vout[SL_C], r[SL_C], xs[XC ? SL_C : 1];
     load_chunk(tc, vin);
+    if constexpr (XC)
+      if (xc) load_chunk(tc + sh, xs);   // x[t] itself
     if (tc + SL_C - 1 - W >= t_start) load_chunk(tc - W, vout);   // else: placeholders below
 #pragma unroll
     for (int j = 0; j < SL_C; ++j) {
@@ -814,17 +844,27 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
         s[i] = max_f64_nn(bp, min_f64_nn(v, b));
         bp = b;
       }
-      r[j] = qnan();
-      if (n >= A.minp && n > 0) {
-        constexpr int K1 = K + 1 < W ? K + 1 : K;
-        const double lo = s[K];
-        if constexpr (MED) {
-          r[j] = (n & 1) ? lo : (lo + s[K1]) / 2.0;
-        } else {
-          const double idxf = A.q * (double)(n - 1);
-          const int idx = (int)idxf;
-          r[j] = ((double)idx == idxf || A.lower) ? lo : lo + (s[K1] - lo) * (idxf - (double)idx);
-        }
+      r[j] = rank_value();
+    }
+    if (XC && xc) {   // (x[t] >= thr[t]) & (x[t - 1] < thr[t - 1]), one byte per candle
+      uint64_t f[SL_C / 8];
+#pragma unroll
+      for (int m = 0; m < SL_C / 8; ++m) f[m] = 0;
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j) {
+        const bool c = xs[j] >= r[j] && pps < pthr;
+        f[j / 8] |= (uint64_t)(c ? 1 : 0) << (8 * (j % 8));
+        pps = xs[j];
+        pthr = r[j];
+      }
+      uint8_t* __restrict__ cr = A.cross + sym * A.ld_cross;
+      if (tc + SL_C <= t_end && (((uintptr_t)(cr + tc)) & 7u) == 0) {
+#pragma unroll
+        for (int m = 0; m < SL_C / 8; ++m) *reinterpret_cast<uint64_t*>(cr + tc + 8 * m) = f[m];
+      } else {
+#pragma unroll
+        for (int j = 0; j < SL_C; ++j)
+          if (tc + j < t_end) cr[tc + j] = (uint8_t)((f[j / 8] >> (8 * (j % 8))) & 1u);
       }
     }
     if (tc >= t_begin && tc + SL_C <= t_end) {
@@ -973,6 +1013,20 @@ __global__ __launch_bounds__(256) void slide_group_kernel(const RollBatch B) {
         if (tc + j < t_end) out[tc + j] = r[j];
     }
   }
+}
+
+// (x[t] >= thr[t]) & (x[t-1] < thr[t-1]) where the slide kernel does not run
+__global__ __launch_bounds__(256) void cross_kernel(const double* __restrict__ x, const double* __restrict__ thr,
+                                                    int64_t S, int T, int64_t ld_in, int64_t ld_out,
+                                                    uint8_t* __restrict__ cross, int64_t ld_cross) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= S * (int64_t)T) return;
+  const int64_t s = i / T;
+  const int t = (int)(i - s * T);
+  const double* xr = x + s * ld_in;
+  const double* tr = thr + s * ld_out;
+  const bool c = xr[t] >= tr[t] && t >= 1 && xr[t - 1] < tr[t - 1];
+  cross[s * ld_cross + t] = c ? 1 : 0;
 }
 
 // ---- tile rank kernel (wave = 64*OPL consecutive outputs of one symbol) --------------
@@ -1562,14 +1616,14 @@ int slide_group(int w) {
   return slide_pair_min() > 0 && w >= slide_pair_min() && w % g == 0 ? g : 1;
 }
 
-int slide_segment(int w, int64_t S, int64_t T) {
+int slide_segment(int w, int64_t S, int64_t T, bool single = false) {
   static const int waves = [] {
     const char* e = getenv("BQ_SLIDE_WAVES");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 2;
   }();
   // a window on a lane group: 1/G of the items for the same lanes
-  const int64_t lanes = (int64_t)1024 * waves * 64 / slide_group(w);
+  const int64_t lanes = (int64_t)1024 * waves * 64 / (single ? 1 : slide_group(w));
   const int64_t nseg = lanes / (S > 0 ? S : 1) > 1 ? lanes / (S > 0 ? S : 1) : 1;
   int64_t seg = (T + nseg - 1) / nseg;
   if (seg < 2 * w) seg = 2 * w;
@@ -1577,7 +1631,12 @@ int slide_segment(int w, int64_t S, int64_t T) {
 }
 
 template <int W, int K, bool MED>
-void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
+void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st, bool single) {
+  if (single) {   // the crossing-flag instantiation
+    const unsigned blocks = (unsigned)((items + 255) / 256);
+    hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED, true>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+    return;
+  }
   if constexpr (W % 4 == 0 && K / (W / 2) == (K + 1) / (W / 2) && K / (W / 4) == (K + 1) / (W / 4) && K + 1 < W) {
     const int g = slide_group(W);
     if (g > 1) {   // G lanes per item
@@ -1593,15 +1652,16 @@ void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st)
   hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
-void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream_t st) {
+// single: the one-lane kernel with the crossing flags (bq_rolling_quantile_cross)
+void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream_t st, bool single = false) {
   switch (v) {
-    case 0: launch_slide1<19, 9, true>(B, n, items, st); break;
-    case 1: launch_slide1<48, 37, false>(B, n, items, st); break;
+    case 0: launch_slide1<19, 9, true>(B, n, items, st, single); break;
+    case 1: launch_slide1<48, 37, false>(B, n, items, st, single); break;
 #if BQ_SLIDE_BIG
-    case 3: launch_slide1<80, 72, false>(B, n, items, st); break;
-    case 4: launch_slide1<96, 76, false>(B, n, items, st); break;
+    case 3: launch_slide1<80, 72, false>(B, n, items, st, single); break;
+    case 4: launch_slide1<96, 76, false>(B, n, items, st, single); break;
 #endif
-    default: launch_slide1<60, 50, false>(B, n, items, st);
+    default: launch_slide1<60, 50, false>(B, n, items, st, single);
   }
 }
 static_assert(kNSlide == 3 + 2 * BQ_SLIDE_BIG, "launch_slide covers every kSlide entry");
@@ -1758,12 +1818,30 @@ int rank_impl(int w, int64_t S, int64_t T, bool slide) {
 extern "C" {
 
 int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream) {
+  return bq_rolling_batch_cross(jobs, n_jobs, S, T, nullptr, nullptr, stream);
+}
+
+int bq_rolling_batch_cross(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, uint8_t* const* cross,
+                           const int64_t* ld_cross, void* stream) {
   using namespace bq;
   if (!jobs || n_jobs < 0 || S < 0 || T < 0 || T > 0x7fffffff) return BQ_EINVAL;
-  for (int i = 0; i < n_jobs; ++i)
+  for (int i = 0; i < n_jobs; ++i) {
     if (!job_ok(jobs[i], S, T)) return BQ_EINVAL;
+    if (cross && cross[i] && (jobs[i].mode != BQ_ROLL_QUANTILE || jobs[i].rows > 0 || !ld_cross || ld_cross[i] < T))
+      return BQ_EINVAL;
+  }
   if (S == 0 || T == 0 || n_jobs == 0) return BQ_OK;
   hipStream_t st = (hipStream_t)stream;
+  // crossing flags: the slide variants that carry a flag job launch the
+  // flag instantiation (one lane per window); elsewhere a flag pass follows
+  bool slide_xc[kNSlide] = {};
+  for (int i = 0; i < n_jobs; ++i)
+    if (cross && cross[i]) {
+      const int sv = slide_variant(jobs[i].window, jobs[i].mode, jobs[i].q);
+      if (sv >= 0 && rank_impl(jobs[i].window, S, T, true) == 3) slide_xc[sv] = true;
+    }
+  int nxp = 0;
+  int xpass[BQ_MAX_ROLL_JOBS];
   // replay jobs (moments, ewm): lane = symbol; rank jobs grouped by window size
   RollBatch rep;
   memset(&rep, 0, sizeof(rep));
@@ -1872,7 +1950,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   }
   auto flush_slide = [&](int v) {
     if (!nslide[v]) return;
-    launch_slide(v, slide[v], nslide[v], slide_items[v], st);
+    launch_slide(v, slide[v], nslide[v], slide_items[v], st, slide_xc[v]);
     nslide[v] = 0;
     slide_items[v] = 0;
   };
@@ -1931,6 +2009,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
     }
     RollJob J;
     memset(&J, 0, sizeof(J));
+    const bool want_x = cross && cross[i];
     J.x = in.x;
     J.out = in.out;
     J.ld_in = in.ld_in;
@@ -1964,8 +2043,12 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       if (nrep == RW_MAXJOBS) flush_rep();
     } else if (const int sv = slide_variant(in.window, J.mode, J.q);
                rank_impl(in.window, S, T, sv >= 0) == 3) {
-      J.seg = slide_segment(in.window, S, T);
+      J.seg = slide_segment(in.window, S, T, slide_xc[sv]);
       J.nseg = (int)((T + J.seg - 1) / J.seg);
+      if (want_x) {
+        J.cross = cross[i];
+        J.ld_cross = ld_cross[i];
+      }
       slide[sv].j[nslide[sv]++] = J;
       const int64_t items = S * (int64_t)J.nseg;
       slide_items[sv] = items > slide_items[sv] ? items : slide_items[sv];
@@ -2001,6 +2084,7 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
       rank_items[b] = items > rank_items[b] ? items : rank_items[b];
       if (nrank[b] == RW_MAXJOBS) flush_rank(b);
     }
+    if (want_x && !J.cross) xpass[nxp++] = i;   // not on the slide kernel: a flag pass after
   }
   flush_pan();
   flush_rep();
@@ -2009,6 +2093,12 @@ int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t
   for (int g = 0; g < 6; ++g) flush_tile(g);
   for (int v = 0; v < kNSlide; ++v) flush_slide(v);
   for (int b = 0; b < 6; ++b) flush_sten(b);
+  for (int u = 0; u < nxp; ++u) {
+    const bq_roll_job& in = jobs[xpass[u]];
+    const int64_t n = S * T;
+    hipLaunchKernelGGL(cross_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in.x, in.out, S, (int)T,
+                       in.ld_in, in.ld_out, cross[xpass[u]], ld_cross[xpass[u]]);
+  }
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
@@ -2028,6 +2118,24 @@ int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t win
   j.mode = mode;
   j.q = q;
   return bq_rolling_batch(&j, 1, S, T, stream);
+}
+
+int bq_rolling_quantile_cross(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window,
+                              int32_t min_periods, int32_t shift, double q, double* out, int64_t ld_out,
+                              uint8_t* cross, int64_t ld_cross, void* stream) {
+  if (!cross) return BQ_EINVAL;
+  bq_roll_job j;
+  memset(&j, 0, sizeof(j));
+  j.x = x;
+  j.out = out;
+  j.ld_in = ld_in;
+  j.ld_out = ld_out;
+  j.window = window;
+  j.min_periods = min_periods;
+  j.shift = shift;
+  j.mode = BQ_ROLL_QUANTILE;
+  j.q = q;
+  return bq_rolling_batch_cross(&j, 1, S, T, &cross, &ld_cross, stream);
 }
 
 int bq_ewm(const double* x, int64_t S, int64_t T, int64_t ld_in, double alpha, int32_t min_periods, double* out,

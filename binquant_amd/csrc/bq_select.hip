@@ -28,6 +28,7 @@
 #include "binquant_amd.h"
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 namespace bq {
@@ -215,6 +216,138 @@ __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __res
   }
 }
 
+// Rows of up to 64 * RQ_KW values: one WAVE per row (4 rows per workgroup),
+// the same radix select with the row's keys in the wave's registers (RQ_KW
+// per lane) and a 256-bin histogram per wave in LDS — no workgroup barrier:
+// the block kernel's passes were ~4 barriers each over 4 waves of one row.
+constexpr int RQ_KW = 32;
+constexpr int RQ_WPB = 4;
+
+// inclusive wave scan of an unsigned (DPP rows + row carries)
+__device__ __forceinline__ unsigned wave_scan_add_u32(unsigned v, int lane) {
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const unsigned y = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += y;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(RQ_WPB * WAVE) void row_quantile_wave_kernel(const double* __restrict__ x, int64_t S,
+                                                                            int T, int64_t ld_in, double q,
+                                                                            double* __restrict__ out) {
+  __shared__ unsigned hist_all[RQ_WPB][256];
+  const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+  const int64_t row = (int64_t)blockIdx.x * RQ_WPB + wv;
+  if (row >= S) return;   // whole wave; no workgroup barrier below
+  unsigned* hist = hist_all[wv];
+  const double* __restrict__ r = x + row * ld_in;
+  // keys (0 marks NaN / padding, as in row_quantile_kernel); lane-contiguous
+  // pairs of values: 16-byte loads
+  uint64_t kr[RQ_KW];
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < RQ_KW; ++i) {
+    const int t = (i >> 1) * (2 * WAVE) + 2 * lane + (i & 1);
+    const double v = t < T ? r[t] : qnan();
+    kr[i] = v == v ? order_key(v) : 0ull;
+    cnt += v == v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  const int n = cnt;
+  if (n == 0) {
+    if (lane == 0) out[row] = qnan();
+    return;
+  }
+  const double vi = (double)(n - 1) * q;
+  const double fl = floor(vi);
+  const int prev = (int)fl;
+  const int next = prev + 1 < n ? prev + 1 : n - 1;
+  const double gamma = vi - fl;
+  uint64_t prefix = 0, mask = 0;
+  int k = prev;
+  for (int sh = 56; sh >= 0; sh -= 8) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) hist[4 * lane + b] = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < RQ_KW; ++i) {
+      const uint64_t key = kr[i];
+      if (key && (key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // lane l owns bins 4l .. 4l + 3: its 4 counts, then the wave's exclusive prefix
+    unsigned h[4], tot = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      h[b] = hist[4 * lane + b];
+      tot += h[b];
+    }
+    const unsigned incl = wave_scan_add_u32(tot, lane);
+    unsigned excl = incl - tot;
+    int found = -1, fk = 0, fh = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (found < 0 && h[b] > 0 && (int)excl <= k && k < (int)(excl + h[b])) {
+        found = 4 * lane + b;
+        fk = k - (int)excl;
+        fh = (int)h[b];
+      }
+      excl += h[b];
+    }
+    // exactly one lane found the bin: broadcast it
+    const uint64_t bal = __ballot(found >= 0);
+    const int src = __builtin_ctzll(bal);
+    const int bin = __shfl(found, src, WAVE);
+    k = __shfl(fk, src, WAVE);
+    const int hb = __shfl(fh, src, WAVE);
+    prefix |= (uint64_t)bin << sh;
+    mask |= 255ull << sh;
+    if (hb == 1 && sh > 0) {   // one key carries the prefix: fetch it
+      uint64_t got = 0;
+#pragma unroll
+      for (int i = 0; i < RQ_KW; ++i) {
+        const uint64_t key = kr[i];
+        if (key && (key & mask) == prefix) got = key;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t p = __shfl_xor(got, o);
+        got = p > got ? p : got;
+      }
+      prefix = got;
+      break;
+    }
+  }
+  const double a = key_value(prefix);
+  double b = a;
+  if (next != prev) {
+    int le = 0;
+    uint64_t above = ~0ull;
+#pragma unroll
+    for (int i = 0; i < RQ_KW; ++i) {
+      const uint64_t key = kr[i];
+      if (key) {
+        le += key <= prefix;
+        if (key > prefix && key < above) above = key;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      le += __shfl_xor(le, o);
+      const uint64_t p = __shfl_xor(above, o);
+      above = p < above ? p : above;
+    }
+    b = le > next ? a : key_value(above);
+  }
+  if (lane == 0) {
+    const double d = b - a;
+    out[row] = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+  }
+}
+
 // One wave per symbol row: 64 candles per step are read as one coalesced
 // 64-byte load, the labels of the step become one ballot mask, and the greedy
 // (keep a label iff it is more than `bars` after the last kept one) walks only
@@ -253,6 +386,17 @@ __global__ __launch_bounds__(256) void cooldown_kernel(const uint8_t* __restrict
 
 }  // namespace bq
 
+namespace {
+// BQ_ROW_QUANTILE_WAVE=0: the workgroup-per-row kernel for every row length
+bool row_quantile_wave() {
+  static const bool on = [] {
+    const char* e = getenv("BQ_ROW_QUANTILE_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 extern "C" {
 
 int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double q, double* out, void* stream) {
@@ -262,7 +406,10 @@ int bq_row_quantile(const double* x, int64_t S, int64_t T, int64_t ld_in, double
   if (S == 0) return BQ_OK;
   const dim3 g((unsigned)S), blk(SQ_NT);
   hipStream_t st = (hipStream_t)stream;
-  if (T <= 8 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<8>, g, blk, 0, st, x, (int)T, ld_in, q, out);
+  if (T <= RQ_KW * WAVE && row_quantile_wave())
+    hipLaunchKernelGGL(row_quantile_wave_kernel, dim3((unsigned)((S + RQ_WPB - 1) / RQ_WPB)), dim3(RQ_WPB * WAVE), 0,
+                       st, x, S, (int)T, ld_in, q, out);
+  else if (T <= 8 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<8>, g, blk, 0, st, x, (int)T, ld_in, q, out);
   else if (T <= 16 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<16>, g, blk, 0, st, x, (int)T, ld_in, q, out);
   else if (T <= 40 * SQ_NT) hipLaunchKernelGGL(row_quantile_kernel<40>, g, blk, 0, st, x, (int)T, ld_in, q, out);
   else hipLaunchKernelGGL(row_quantile_kernel<0>, g, blk, 0, st, x, (int)T, ld_in, q, out);

@@ -814,6 +814,33 @@ def rolling(
 
 
 @device_entry
+def rolling_quantile_cross(
+    x: torch.Tensor,
+    window: int,
+    q: float,
+    min_periods: int | None = None,
+    shift: int = 0,
+    stream: torch.cuda.Stream | None = None,
+) -> tuple[torch.Tensor, torch.Tensor]:
+    """(thr, cross): thr = x.shift(shift).rolling(window, min_periods).quantile(q)
+    and cross = (x >= thr) & (x.shift(1) < thr.shift(1)) (bool) in one pass
+    where the sliding-window kernel runs (bq_rolling_quantile_cross) —
+    LiquidationSweepPump's score_threshold / score_cross
+    (strategies/liquidation_sweep_pump.py:231-239)."""
+    x = _check_panel(x, "x")
+    S, T = x.shape
+    thr = torch.empty((S, T), dtype=torch.float64, device=x.device)
+    cross = torch.empty((S, T), dtype=torch.bool, device=x.device)
+    st = _lib.load().bq_rolling_quantile_cross(
+        ctypes.c_void_p(x.data_ptr()), S, T, _row_stride(x), int(window),
+        int(window if min_periods is None else min_periods), int(shift), float(q),
+        ctypes.c_void_p(thr.data_ptr()), T, ctypes.c_void_p(cross.data_ptr()), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_rolling_quantile_cross")
+    return thr, cross
+
+
+@device_entry
 def ewm(
     x: torch.Tensor,
     alpha: float | None = None,
@@ -872,7 +899,8 @@ class Ffill:
 
 
 @device_entry
-def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = None) -> list[torch.Tensor]:
+def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = None,
+                 cross: tuple[int, ...] = ()):
     """Independent Roll / Ewm / Ffill series over one [S, T] shape in as few
     launches as the kernel families allow (bq_rolling_batch): the
     lane-per-symbol replays of different series run side by side instead of
@@ -884,9 +912,13 @@ def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = 
     (1e-9) instead of the bit-exact sequential replay; order statistics on
     the tile kernels sort packed keys (the union slot in the key's low bits:
     the selected value is an element within 2^-45 relative of the exact
-    order statistic); var / std and the rest are unchanged."""
+    order statistic); var / std and the rest are unchanged.
+    cross: indices of quantile specs that also get their crossing flags,
+    (x >= thr) & (x.shift(1) < thr.shift(1)) as bool [S, T]
+    (bq_rolling_batch_cross; liquidation_sweep_pump.py:237-239's score_cross
+    form) — then the result is (outs, flags), flags in the order of cross."""
     if not specs:
-        return []
+        return ([], []) if cross else []
     xs = [_check_panel(sp.x, "x") for sp in specs]
     S = max(int(x.shape[0]) for x in xs)
     T = int(xs[0].shape[1])
@@ -924,6 +956,12 @@ def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = 
         jobs.append(j)
         outs.append(out)
         keep.append(x)
+    flags = {}
+    for k in cross:
+        if not (isinstance(specs[k], Roll) and specs[k].stat == "quantile" and xs[k].shape[0] == S):
+            raise ValueError(f"cross: spec {k} is not a quantile over the whole panel")
+        flags[k] = torch.empty((S, T), dtype=torch.bool, device=xs[k].device)
+    fptr = {id(jobs[k]): flags[k].data_ptr() for k in flags}
     L = _lib.load()
     # a batch call takes MAX_ROLL_JOBS jobs: the sequential replays (moments,
     # ewm — one latency-bound launch per call, whatever its job count) go
@@ -935,8 +973,14 @@ def rolling_many(*specs, exact: bool = True, stream: torch.cuda.Stream | None = 
     for i in range(0, len(jobs), _lib.MAX_ROLL_JOBS):
         chunk = jobs[i : i + _lib.MAX_ROLL_JOBS]
         arr = (_lib.BqRollJob * len(chunk))(*chunk)
-        _lib.check(L.bq_rolling_batch(arr, len(chunk), S, T, _stream_handle(stream)), "bq_rolling_batch")
-    return outs
+        if fptr:
+            cp = _lib.ptr_array([fptr.get(id(j), 0) for j in chunk])
+            cl = (ctypes.c_int64 * len(chunk))(*([T] * len(chunk)))
+            _lib.check(L.bq_rolling_batch_cross(arr, len(chunk), S, T, cp, cl, _stream_handle(stream)),
+                       "bq_rolling_batch_cross")
+        else:
+            _lib.check(L.bq_rolling_batch(arr, len(chunk), S, T, _stream_handle(stream)), "bq_rolling_batch")
+    return (outs, [flags[k] for k in cross]) if cross else outs
 
 
 @device_entry

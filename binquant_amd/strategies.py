@@ -337,12 +337,11 @@ def _pump_score_fused(h, l, c, v, bench, p: PumpParams) -> dict[str, torch.Tenso
         atr, e20, e50, trend = engine.pump_ewm(h, l, c, trend=True)
         st = engine.pump_features(h, l, c, v, atr, e20, e50, bf[0], be20[0], be50[0], p.momentum_bars,
                                   p.volume_lookback, p.compression_bars, trend_score=trend)
-    thr_s, thr_v = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)
+    # the two quantiles in one launch, score_cross formed in the score's steps
+    (thr_s, thr_v), (cross,) = engine.rolling_many(   # panel mode: packed-key order statistics (within 2^-45)
         R(st["pump_score"], p.score_lookback, "quantile", q=p.score_quantile, shift=1),
-        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1), exact=False,
+        R(st["relative_volume"], p.score_lookback, "quantile", q=p.score_quantile, shift=1), exact=False, cross=(0,),
     )
-    PS, TS = F.inp(st["pump_score"]), F.inp(thr_s)
-    cross = F.run({"score_cross": (PS >= TS) & (F.shift(PS, 1) < F.shift(TS, 1))})["score_cross"]
     out = {k: st[k] for k in ("candidate_atr", "momentum_3", "relative_volume", "pre_breakout_compression",
                               "pump_score")}
     out.update(score_threshold=thr_s, volume_threshold=thr_v, score_cross=cross)

@@ -313,6 +313,19 @@ int bq_rolling(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t win
                int32_t shift, int32_t mode, double q, double* out, int64_t ld_out, void* stream);
 
 /*
+ * out = x.shift(shift).rolling(window, min_periods).quantile(q) as bq_rolling
+ * (BQ_ROLL_QUANTILE), and cross[t] = (x[t] >= out[t]) & (x[t-1] < out[t-1])
+ * as one byte per candle (pandas comparisons: NaN compares false; 0 at t = 0)
+ * — LiquidationSweepPump's score_threshold and score_cross
+ * (strategies/liquidation_sweep_pump.py:231-239) in one pass where the
+ * sliding-window kernel runs (else the quantile, then a flag pass). cross:
+ * uint8 [S][ld_cross] device pointer.
+ */
+int bq_rolling_quantile_cross(const double* x, int64_t S, int64_t T, int64_t ld_in, int32_t window,
+                              int32_t min_periods, int32_t shift, double q, double* out, int64_t ld_out,
+                              uint8_t* cross, int64_t ld_cross, void* stream);
+
+/*
  * Many independent rolling / ewm series over one [S][T] shape in one call
  * (the strategy pipelines issue 5-18 of them per frame batch, e.g.
  * strategies/failed_spike_fade.py:260-357): one launch per kernel family
@@ -337,6 +350,16 @@ typedef struct bq_roll_job {
   int32_t reserved;
 } bq_roll_job;
 int bq_rolling_batch(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, void* stream);
+/*
+ * bq_rolling_batch with crossing flags: for a BQ_ROLL_QUANTILE job i with
+ * cross[i] != NULL (uint8 [S][ld_cross[i]] device pointer; the job on all S
+ * rows), also cross[i][t] = (x[t] >= out[t]) & (x[t-1] < out[t-1]) as
+ * bq_rolling_quantile_cross — formed in the sliding-window kernel's steps
+ * where that kernel runs the job. cross / ld_cross: host arrays of n_jobs
+ * (cross NULL: none).
+ */
+int bq_rolling_batch_cross(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, int64_t T, uint8_t* const* cross,
+                           const int64_t* ld_cross, void* stream);
 
 /*
  * out = x.ewm(alpha=alpha, adjust=False, min_periods=min_periods).mean()

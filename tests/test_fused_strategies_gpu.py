@@ -315,3 +315,41 @@ def test_pump_ewm_one_pass_equals_panel_ewm(cuda, S, T):
     assert len(a3) == 3
     for x, y in zip(a3, (atr, e20, e50)):
         np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+
+
+@pytest.mark.parametrize("S,T,w,q", [(2100, 2000, 48, 0.80), (2100, 2000, 80, 0.92), (40, 700, 48, 0.80),
+                                     (2100, 2000, 30, 0.5)])
+def test_rolling_quantile_cross(cuda, S, T, w, q):
+    """bq_rolling_quantile_cross: the threshold bit-equal to bq_rolling's
+    quantile of x.shift(1) (the sliding-window kernel at large panels, with
+    the flags formed in its steps and the window of each segment's previous
+    step built for the first flag; the tile / stencil kernels + a flag pass
+    elsewhere) and cross = (x >= thr) & (x.shift(1) < thr.shift(1)) bit for
+    bit, on rows with NaN runs, a constant stretch and a late start."""
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    x = numpy_panel(S, T, seed0=S + w, edges=False)["volume"].copy()
+    x[1, 300:340] = np.nan
+    x[2, :500] = np.nan
+    x[3, 100:400] = 5.0
+    x[4, ::7] = np.nan
+    d = torch.from_numpy(x).cuda()
+    thr, cross = engine.rolling_quantile_cross(d, w, q, shift=1)
+    want = engine.rolling(d, w, "quantile", q=q, shift=1)
+    np.testing.assert_array_equal(thr.cpu().numpy(), want.cpu().numpy())
+    t = want.cpu().numpy()
+    with np.errstate(invalid="ignore"):
+        c = (x >= t) & np.concatenate([np.zeros((S, 1), bool), x[:, :-1] < t[:, :-1]], axis=1)
+    got = cross.cpu().numpy()
+    assert got.dtype == bool
+    np.testing.assert_array_equal(got, c)
+    assert c.sum() > 0
+    # in a batch beside a quantile without flags (one launch of the flag
+    # instantiation where the slide kernel runs), flags on the second spec
+    d2 = torch.flip(d, dims=[1]).contiguous()
+    (a, b), (f,) = engine.rolling_many(engine.Roll(d2, w, "quantile", q=q, shift=1),
+                                       engine.Roll(d, w, "quantile", q=q, shift=1), exact=False, cross=(1,))
+    np.testing.assert_array_equal(b.cpu().numpy(), t)
+    np.testing.assert_array_equal(a.cpu().numpy(), engine.rolling(d2, w, "quantile", q=q, shift=1).cpu().numpy())
+    np.testing.assert_array_equal(f.cpu().numpy(), c)

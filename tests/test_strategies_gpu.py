@@ -114,7 +114,8 @@ def test_rolling_signed_series_vs_pandas(cuda, stat, window, minp):
         np.testing.assert_array_equal(got[s], want, err_msg=f"{stat} {s}")
 
 
-@pytest.mark.parametrize("T", [700, 3000, 9000])   # register-resident row forms (8 / 16 / 40 keys per thread)
+# register-resident row forms: a wave per row (T <= 2048), a workgroup per row (8 / 16 / 40 keys per thread)
+@pytest.mark.parametrize("T", [200, 700, 2000, 2048, 3000, 9000])
 def test_row_quantile_is_numpy_bitwise(cuda, T):
     from binquant_amd import engine
 
@@ -258,12 +259,12 @@ def test_plan_cache_hits_are_bit_exact(cuda):
     from binquant_amd import signals, strategies
     from binquant_amd.synth import device_panel
 
-    # (the staged burst pipeline: its fused path, bq_burst_features, runs no
-    # JIT programs)
+    # (the staged burst and pump pipelines: their fused paths, bq_burst_features
+    # and bq_pump_features + bq_rolling_quantile_cross, run no JIT programs)
     calls = {
         "burst": lambda o, h, l, c, v: _staged_burst(strategies, o, h, l, c, v),
         "spike": lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c),
-        "pump": lambda o, h, l, c, v: strategies.pump_score_features(o, h, l, c, v, c[0].clone()),
+        "pump": lambda o, h, l, c, v: _staged_pump(strategies, o, h, l, c, v),
         "gainer": lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c),
     }
     for seed, (name, fn) in enumerate(calls.items()):
@@ -290,6 +291,14 @@ def _staged_burst(strategies, o, h, l, c, v):
         return strategies.activity_burst_features(o, h, l, c, v, v * c)
     finally:
         strategies._BURST_FUSED = True
+
+
+def _staged_pump(strategies, o, h, l, c, v):
+    strategies._PUMP_FUSED = False
+    try:
+        return strategies.pump_score_features(o, h, l, c, v, c[0].clone())
+    finally:
+        strategies._PUMP_FUSED = True
 
 
 def _assert_same_tree(a, b, path):
