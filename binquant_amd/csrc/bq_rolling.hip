@@ -914,7 +914,10 @@ __global__ __launch_bounds__(256) void slide_group_kernel(const RollBatch B) {
   constexpr int H = W / G;
   constexpr int KL = K / H;   // the lane holding the rank slots
   static_assert((G == 2 || G == 4) && W % G == 0 && (K + 1) / H == KL && K + 1 < W, "group layout");
-  constexpr int SL_C = 8;
+#ifndef BQ_SG_C
+#define BQ_SG_C 8
+#endif
+  constexpr int SL_C = BQ_SG_C;
   const RollJob& A = B.j[blockIdx.y];
   const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int q = threadIdx.x & (G - 1);
