@@ -951,14 +951,64 @@ __global__ __launch_bounds__(256) void slide_group_kernel(const RollBatch B) {
   };
   auto b_of = [&](int nn) -> int { return nn >= 1 ? K - a_of(nn) : K + 1; };
   const bool top = q == G - 1, bottom = q == 0;
-  // the empty window: B(0) = K + 1 bottom placeholders, the rest on top
   double s[H];
-#pragma unroll
-  for (int i = 0; i < H; ++i) s[i] = q * H + i < K + 1 ? -inf : inf;
   int n = 0, nb = K + 1;
-  // steps from t_start (the W - 1 before the segment fill the window), in
-  // chunks aligned to t_begin so the output chunks are the single-lane ones
-  const int tw = t_begin - ((t_begin - t_start + SL_C - 1) / SL_C) * SL_C;
+  int tw;   // the first step of the full-step loop
+  if constexpr (G == 2) {
+    // pairs: the window before the segment filled insert-only (the
+    // single-lane kernel's warm-up, 2 VALU per slot instead of 5: every
+    // placeholder +inf on top, the lower lane's old top slot handed up for
+    // the upper lane's bottom clamp), then the split made by shifting the
+    // pair's combined array up by B(n)
+#pragma unroll
+    for (int i = 0; i < H; ++i) s[i] = inf;
+    constexpr int NCH = (W + SL_C - 1) / SL_C;
+    const int t0w = t_begin - NCH * SL_C;   // step of chunk slot 0
+    for (int c = 0; c < NCH; ++c) {
+      if (t0w + (c + 1) * SL_C <= t_start) continue;   // chunk wholly before the window
+      double v[SL_C];
+      load_chunk(t0w + c * SL_C, v);
+#pragma unroll
+      for (int j = 0; j < SL_C; ++j) {
+        const bool num = t0w + c * SL_C + j >= t_start && win_ok(v[j]);
+        n += num ? 1 : 0;
+        const double a = num ? v[j] + 0.0 : inf;
+        const double dn = from_lower<G>(s[H - 1]);
+#pragma unroll
+        for (int i = H - 1; i > 0; --i) s[i] = max_f64_nn(s[i - 1], min_f64_nn(a, s[i]));
+        s[0] = max_f64_nn(bottom ? -inf : dn, min_f64_nn(a, s[0]));
+      }
+    }
+    // log-step shift of the combined array [lower | upper] by nb (-inf
+    // filling): per step b, the upper lane's slots i < b take the lower
+    // lane's slot H + i - b (read by a swap before the step), the lower
+    // lane's take -inf
+    nb = b_of(n);
+#pragma unroll
+    for (int b = 1; b < W; b <<= 1) {
+      const bool sh_on = (nb & b) != 0;
+      double p[H];
+#pragma unroll
+      for (int i = 0; i < H; ++i) {
+        if (i >= b) break;
+        const int j = H + i - b;
+        p[i] = j >= 0 ? from_upper<G>(s[j >= 0 ? j : 0]) : -inf;   // the partner's slot j
+      }
+#pragma unroll
+      for (int i = H - 1; i >= 0; --i) {
+        const double v = i >= b ? s[i >= b ? i - b : 0] : (bottom ? -inf : p[i]);
+        s[i] = sh_on ? v : s[i];
+      }
+    }
+    tw = t_begin;
+  } else {
+    // the empty window: B(0) = K + 1 bottom placeholders, the rest on top;
+    // steps from t_start (the W - 1 before the segment fill the window) are
+    // full steps, in chunks aligned to t_begin (the single-lane output chunks)
+#pragma unroll
+    for (int i = 0; i < H; ++i) s[i] = q * H + i < K + 1 ? -inf : inf;
+    tw = t_begin - ((t_begin - t_start + SL_C - 1) / SL_C) * SL_C;
+  }
   for (int tc = tw; tc < t_end; tc += SL_C) {
     double vin[SL_C], vout[SL_C], r[SL_C];
     load_chunk(tc, vin);
