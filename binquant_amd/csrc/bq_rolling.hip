@@ -1669,52 +1669,99 @@ int slide_group(int w) {
   return slide_pair_min() > 0 && w >= slide_pair_min() && w % g == 0 ? g : 1;
 }
 
-int slide_segment(int w, int64_t S, int64_t T, bool single = false) {
-  static const int waves = [] {
+// Segments of a slide batch (lanes = (symbol, segment) x G lanes per window):
+// enough for one round of the kernel's resident waves over the chip, whose
+// occupancy comes from its registers (hipOccupancy..., per instantiation) —
+// BQ_SLIDE_WAVES rounds (default 1). A second, partial round costs a whole
+// segment's time: at 12.5k x 2k the a17 medians (two w = 19 series, 3 waves
+// per SIMD) ran 0.40 ms over 10 segments (two rounds) against 0.34 over 5.
+// Each segment replays W - 1 warm-up values, so segments stay >= 2 W.
+int device_cus() {
+  static const int cus = [] {
+    int d = 0, c = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+      c = 0;
+    return c > 0 ? c : 256;
+  }();
+  return cus;
+}
+template <typename F>
+int resident_waves(F kern) {   // 256-thread workgroups per CU = waves per SIMD
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb < 1) nb = 1;
+  return nb;
+}
+// ... and no more items in flight than the L2 holds their two streams
+// (the entering chunk and the leaving one, `chunk` values each; a group's
+// lanes share theirs): 32 MiB = 8 XCDs x 4 MiB. The w = 19 medians (16-value
+// chunks) at 7 segments (175k lanes x 256 B > the L2) ran 0.43 ms, at 5
+// (125k lanes) 0.34.
+int64_t slide_segments(bq::RollBatch& B, int n, int w, int g, int occ, int chunk) {
+  static const int rounds = [] {
     const char* e = getenv("BQ_SLIDE_WAVES");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 2;
+    return v > 0 ? v : 1;
   }();
-  // a window on a lane group: 1/G of the items for the same lanes
-  const int64_t lanes = (int64_t)1024 * waves * 64 / (single ? 1 : slide_group(w));
-  const int64_t nseg = lanes / (S > 0 ? S : 1) > 1 ? lanes / (S > 0 ? S : 1) : 1;
+  const int64_t l2_items = ((int64_t)32 << 20) / (2 * chunk * 8);
+  int64_t items = (int64_t)device_cus() * 4 * occ * 64 * rounds / g;
+  items = items < l2_items * rounds ? items : l2_items * rounds;
+  const int64_t per = (B.S > 0 ? B.S : 1) * (int64_t)n;
+  const int64_t nseg = items / per > 1 ? items / per : 1;
+  const int64_t T = B.T;
   int64_t seg = (T + nseg - 1) / nseg;
   if (seg < 2 * w) seg = 2 * w;
-  return (int)(seg < T ? seg : (T > 0 ? T : 1));
+  if (seg > T) seg = T > 0 ? T : 1;
+  const int ns = (int)((T + seg - 1) / seg);
+  for (int i = 0; i < n; ++i) {
+    B.j[i].seg = (int)seg;
+    B.j[i].nseg = ns;
+  }
+  return B.S * (int64_t)ns;
 }
 
 template <int W, int K, bool MED>
-void launch_slide1(const bq::RollBatch& B, int n, int64_t items, hipStream_t st, bool single) {
+void launch_slide1(const bq::RollBatch& B0, int n, hipStream_t st, bool single) {
+  bq::RollBatch B = B0;
   if (single) {   // the crossing-flag instantiation
+    static const int occ = resident_waves(bq::slide_rank_kernel<W, K, MED, true>);
+    const int64_t items = slide_segments(B, n, W, 1, occ, W <= 24 ? 16 : 8);
     const unsigned blocks = (unsigned)((items + 255) / 256);
     hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED, true>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
     return;
   }
   if constexpr (W % 4 == 0 && K / (W / 2) == (K + 1) / (W / 2) && K / (W / 4) == (K + 1) / (W / 4) && K + 1 < W) {
     const int g = slide_group(W);
-    if (g > 1) {   // G lanes per item
-      const unsigned blocks = (unsigned)((g * items + 255) / 256);
-      if (g == 2)
-        hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 2>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
-      else
-        hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 4>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+    if (g == 2) {
+      static const int occ = resident_waves(bq::slide_group_kernel<W, K, MED, 2>);
+      const int64_t items = slide_segments(B, n, W, 2, occ, BQ_SG_C);
+      const unsigned blocks = (unsigned)((2 * items + 255) / 256);
+      hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 2>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
+      return;
+    }
+    if (g == 4) {
+      static const int occ = resident_waves(bq::slide_group_kernel<W, K, MED, 4>);
+      const int64_t items = slide_segments(B, n, W, 4, occ, BQ_SG_C);
+      const unsigned blocks = (unsigned)((4 * items + 255) / 256);
+      hipLaunchKernelGGL((bq::slide_group_kernel<W, K, MED, 4>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
       return;
     }
   }
+  static const int occ = resident_waves(bq::slide_rank_kernel<W, K, MED>);
+  const int64_t items = slide_segments(B, n, W, 1, occ, W <= 24 ? 16 : 8);
   const unsigned blocks = (unsigned)((items + 255) / 256);
   hipLaunchKernelGGL((bq::slide_rank_kernel<W, K, MED>), dim3(blocks, (unsigned)n), dim3(256), 0, st, B);
 }
 
 // single: the one-lane kernel with the crossing flags (bq_rolling_quantile_cross)
-void launch_slide(int v, const bq::RollBatch& B, int n, int64_t items, hipStream_t st, bool single = false) {
+void launch_slide(int v, const bq::RollBatch& B, int n, hipStream_t st, bool single = false) {
   switch (v) {
-    case 0: launch_slide1<19, 9, true>(B, n, items, st, single); break;
-    case 1: launch_slide1<48, 37, false>(B, n, items, st, single); break;
+    case 0: launch_slide1<19, 9, true>(B, n, st, single); break;
+    case 1: launch_slide1<48, 37, false>(B, n, st, single); break;
 #if BQ_SLIDE_BIG
-    case 3: launch_slide1<80, 72, false>(B, n, items, st, single); break;
-    case 4: launch_slide1<96, 76, false>(B, n, items, st, single); break;
+    case 3: launch_slide1<80, 72, false>(B, n, st, single); break;
+    case 4: launch_slide1<96, 76, false>(B, n, st, single); break;
 #endif
-    default: launch_slide1<60, 50, false>(B, n, items, st, single);
+    default: launch_slide1<60, 50, false>(B, n, st, single);
   }
 }
 static_assert(kNSlide == 3 + 2 * BQ_SLIDE_BIG, "launch_slide covers every kSlide entry");
@@ -1995,7 +2042,7 @@ int bq_rolling_batch_cross(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, i
   };
   RollBatch slide[kNSlide];
   int nslide[kNSlide] = {};
-  int64_t slide_items[kNSlide] = {};
+
   for (int v = 0; v < kNSlide; ++v) {
     memset(&slide[v], 0, sizeof(RollBatch));
     slide[v].S = S;
@@ -2003,9 +2050,8 @@ int bq_rolling_batch_cross(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, i
   }
   auto flush_slide = [&](int v) {
     if (!nslide[v]) return;
-    launch_slide(v, slide[v], nslide[v], slide_items[v], st, slide_xc[v]);
+    launch_slide(v, slide[v], nslide[v], st, slide_xc[v]);   // segments set there
     nslide[v] = 0;
-    slide_items[v] = 0;
   };
   RollBatch ff;
   memset(&ff, 0, sizeof(ff));
@@ -2096,15 +2142,11 @@ int bq_rolling_batch_cross(const bq_roll_job* jobs, int32_t n_jobs, int64_t S, i
       if (nrep == RW_MAXJOBS) flush_rep();
     } else if (const int sv = slide_variant(in.window, J.mode, J.q);
                rank_impl(in.window, S, T, sv >= 0) == 3) {
-      J.seg = slide_segment(in.window, S, T, slide_xc[sv]);
-      J.nseg = (int)((T + J.seg - 1) / J.seg);
       if (want_x) {
         J.cross = cross[i];
         J.ld_cross = ld_cross[i];
       }
       slide[sv].j[nslide[sv]++] = J;
-      const int64_t items = S * (int64_t)J.nseg;
-      slide_items[sv] = items > slide_items[sv] ? items : slide_items[sv];
       if (nslide[sv] == RW_MAXJOBS) flush_slide(sv);
     } else if (rank_impl(in.window, S, T, false) == 2 && S * ((T + SR_NT - 1) / SR_NT) <= 0x7fffffff) {
       const int b = stencil_bucket(in.window);
