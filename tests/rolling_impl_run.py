@@ -34,6 +34,20 @@ def main(out):
     rank = engine.rolling_many(*[Roll(x, w, st, q=q, min_periods=mp, shift=sh) for w, st, q, mp, sh in RANK_JOBS])
     for (w, st, q, mp, sh), r in zip(RANK_JOBS, rank):
         res[f"rank_{w}_{st}_{q}_{mp}_{sh}"] = r
+    # rows shorter than two windows (one segment per row at the long windows)
+    short = panel(6, 171)
+    for (w, st, q, mp, sh), r in zip(RANK_JOBS, engine.rolling_many(
+            *[Roll(short, w, st, q=q, min_periods=mp, shift=sh) for w, st, q, mp, sh in RANK_JOBS])):
+        res[f"short_{w}_{st}_{q}_{mp}_{sh}"] = r
+    # crossing flags beside plain quantiles (the flag instantiation of the
+    # slide kernel where it runs, a flag pass after the other kernels)
+    xj = [(48, 0.8, 48, 1), (80, 0.92, 20, 1), (60, 0.85, 20, 1), (19, 0.5, 19, 2)]
+    thr, flags = engine.rolling_many(*[Roll(x, w, "quantile", q=q, min_periods=mp, shift=sh) for w, q, mp, sh in xj],
+                                     cross=(0, 1, 3))
+    for k, t in enumerate(thr):
+        res[f"xthr_{k}"] = t
+    for k, f in enumerate(flags):
+        res[f"xflag_{k}"] = f
     mixed = [Roll(x, 2, "sum"), Roll(x, 12, "mean", shift=1), Roll(x, 20, "std"), Roll(x, 80, "var0", min_periods=5),
              Roll(x, 96, "std0", min_periods=1, shift=3), Ewm(x, alpha=1 / 14, min_periods=14), Ewm(x, span=50),
              Ffill(x)]

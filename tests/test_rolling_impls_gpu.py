@@ -29,6 +29,9 @@ def _run(tmp_path, name, env):
 
 
 def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
+    sys.path.insert(0, str(HERE))
+    from rolling_impl_run import RANK_JOBS, panel
+
     runs = {
         "lane_ring": _run(tmp_path, "lane_ring", {"BQ_RANK_IMPL": "lane", "BQ_REPLAY_IMPL": "ring"}),
         "tile_restage": _run(tmp_path, "tile_restage", {"BQ_RANK_IMPL": "tile", "BQ_REPLAY_IMPL": "restage"}),
@@ -51,12 +54,18 @@ def test_rolling_implementations_agree_bitwise(cuda, tmp_path):
             # signs of zero must agree too, except for order statistics: which of
             # -0.0 / +0.0 a window's rank holds is unspecified (they compare
             # equal; pandas' skiplist keeps insertion order)
-            num = ~np.isnan(b) & ~(k.startswith("rank") & (b == 0))
+            if b.dtype == bool:   # crossing flags
+                continue
+            num = ~np.isnan(b) & ~(k.startswith(("rank", "short", "xthr")) & (b == 0))
             assert np.array_equal(np.signbit(a[num]), np.signbit(b[num])), (name, k)
+    # the flags are those of the thresholds (x >= thr) & (x.shift(1) < thr.shift(1))
+    xv = panel(37, 700).cpu().numpy()
+    for k, (w, q, mp, sh) in zip((0, 1), ((48, 0.8, 48, 1), (80, 0.92, 20, 1))):
+        t = ref[f"xthr_{k}"]
+        with np.errstate(invalid="ignore"):
+            want = (xv >= t) & np.concatenate([np.zeros((37, 1), bool), xv[:, :-1] < t[:, :-1]], axis=1)
+        np.testing.assert_array_equal(ref[f"xflag_{k}"], want)
     # order statistics vs pandas on the same battery
-    sys.path.insert(0, str(HERE))
-    from rolling_impl_run import RANK_JOBS, panel
-
     x = panel(37, 700).cpu().numpy()
     df = pd.DataFrame(x.T)
     for w, st, q, mp, sh in RANK_JOBS:
