@@ -75,6 +75,9 @@ struct CtxArgs {
   uint16_t* gcnt;      // packed counts [ngrp][ld_g]
   int64_t ld_g;
   double* last[BQ_NUM_FEATURES];   // optional features at t = T - 1, [S] each
+  double* feat[BQ_NUM_FEATURES];   // FEAT: the feature columns [S][ld_f] (NULL = skip)
+  int64_t ld_f;
+  int vout;
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -119,7 +122,10 @@ __device__ __forceinline__ double cx_div(double a, double b) {
 // DIV: pandas' EMA divide by (old_wt + new_wt) is needed (not exactly 1.0)
 // RING: span 50's history term from the D ring (long caps); otherwise the
 // lagged chains for every span whose a^(M-1) >= 1e-15 (short caps)
-template <bool DIV, bool RING>
+// FEAT: bq_market_features — the six feature columns written (whole-line
+// stores of each wave's row) instead of reduced: no group records, no
+// workgroup barrier
+template <bool DIV, bool RING, bool FEAT = false>
 __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArgs A) {
   __shared__ double sTr[CX_NW][CX_RS], sC[CX_NW][CX_RS];   // true range / close rings per wave
   __shared__ double sR[2][4][CX_TT];   // reduction slots: 4 sums, index k * 64 + lane
@@ -382,6 +388,21 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
       fap[k] = cl != 0.0 ? cx_div(a, cl) : 0.0;
       fbw[k] = m != 0.0 ? cx_div(up - lo, m < 0.0 ? -m : m) : 0.0;
     }
+    if constexpr (FEAT) {
+      if (live) {   // wave-uniform: store_lines exchanges across the wave
+        const int64_t orow = sym * A.ld_f;
+        const bool vo = A.vout != 0, whole = t0 + CX_TT <= T;
+        const double* const cols[BQ_NUM_FEATURES] = {fr, fe20, fe50, ftr, fap, fbw};
+#pragma unroll
+        for (int f = 0; f < BQ_NUM_FEATURES; ++f)
+          if (A.feat[f]) {
+            double v[CX_K];
+#pragma unroll
+            for (int k = 0; k < CX_K; ++k) v[k] = cols[f][k];
+            store_lines<CX_K>(A.feat[f] + orow, tb, T, vo, v, whole);
+          }
+      }
+    } else {
     // the last timestamp's feature row, when asked (the context's symbol_features)
     if (live && tb <= T - 1 && T - 1 < tb + CX_K) {
 #pragma unroll
@@ -458,6 +479,7 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
           if (tb + k < T) gc[tb + k] = (uint16_t)cn[k];
       }
     }
+    }   // !FEAT
 
     if (t0 + CX_TT >= T) break;
     wave_sync();   // every lane's reads of this tile's rings are done
@@ -607,6 +629,67 @@ static double cx_alpha_from_span(double span) {
   return 1.0 / (1.0 + com);
 }
 
+// the EMA constants and the history-cap correction factors
+static void ctx_consts(CtxArgs& A, int max_bars) {
+  const double spans[2] = {20.0, 50.0};   // live_market_context_accumulator.py:266-267
+  for (int e = 0; e < 2; ++e) {
+    const double al = cx_alpha_from_span(spans[e]);
+    A.alpha[e] = al;
+    A.om[e] = 1.0 - al;
+    A.den[e] = A.om[e] + al;
+    A.lin_a[e] = A.om[e] / A.den[e];
+    A.lin_b[e] = al / A.den[e];
+    double ak = 1.0;
+    for (int k = 0; k < CX_K; ++k) ak *= A.lin_a[e];
+    for (int j = 0; j < 8; ++j) {
+      A.apow[e][j] = ak;
+      ak *= ak;
+    }
+    double cp = 1.0;
+    for (int k = 0; k < max_bars - 1; ++k) cp *= A.lin_a[e];
+    A.corr[e] = cp;
+  }
+  A.lag20 = A.corr[0] >= 1e-15;
+  A.lag50 = A.corr[1] >= 1e-15;
+  if (!A.lag20) A.corr[0] = 0.0;
+  if (!A.lag50) A.corr[1] = 0.0;
+}
+
+// bq_market_features through context_partials_kernel<..., FEAT> (bq_market.hip
+// calls this): the same per-wave feature computation, the columns written
+int context_features(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t max_bars,
+                     double* const* feat, int64_t ld_out, hipStream_t st) {
+  CtxArgs A;
+  memset(&A, 0, sizeof(A));
+  A.h = hlc[0];
+  A.l = hlc[1];
+  A.c = hlc[2];
+  A.S = S;
+  A.ld_in = ld_in;
+  A.T = (int)T;
+  A.M = max_bars;
+  auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
+  A.vin = (ld_in % 2) == 0 && aligned(A.h) && aligned(A.l) && aligned(A.c);
+  int vout = (ld_out % 2) == 0;
+  for (int f = 0; f < BQ_NUM_FEATURES; ++f) {
+    A.feat[f] = feat[f];
+    if (feat[f]) vout &= aligned(feat[f]);
+  }
+  A.ld_f = ld_out;
+  A.vout = vout;
+  ctx_consts(A, max_bars);
+  const unsigned ngrp = (unsigned)((S + CX_NW - 1) / CX_NW);
+  const bool ring = A.corr[1] <= 1e-6 && !A.lag20;
+  if (A.den[0] != 1.0 || A.den[1] != 1.0) {
+    if (ring) hipLaunchKernelGGL((context_partials_kernel<true, true, true>), dim3(ngrp), dim3(CX_NT), 0, st, A);
+    else hipLaunchKernelGGL((context_partials_kernel<true, false, true>), dim3(ngrp), dim3(CX_NT), 0, st, A);
+  } else {
+    if (ring) hipLaunchKernelGGL((context_partials_kernel<false, true, true>), dim3(ngrp), dim3(CX_NT), 0, st, A);
+    else hipLaunchKernelGGL((context_partials_kernel<false, false, true>), dim3(ngrp), dim3(CX_NT), 0, st, A);
+  }
+  return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
 }  // namespace bq
 
 extern "C" {
@@ -641,28 +724,7 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
   A.M = max_bars;
   auto aligned = [](const void* p) { return (((uintptr_t)p) & 15u) == 0; };
   A.vin = (ld_in % 2) == 0 && aligned(A.h) && aligned(A.l) && aligned(A.c);
-  const double spans[2] = {20.0, 50.0};   // live_market_context_accumulator.py:266-267
-  for (int e = 0; e < 2; ++e) {
-    const double al = cx_alpha_from_span(spans[e]);
-    A.alpha[e] = al;
-    A.om[e] = 1.0 - al;
-    A.den[e] = A.om[e] + al;
-    A.lin_a[e] = A.om[e] / A.den[e];
-    A.lin_b[e] = al / A.den[e];
-    double ak = 1.0;
-    for (int k = 0; k < CX_K; ++k) ak *= A.lin_a[e];
-    for (int j = 0; j < 8; ++j) {
-      A.apow[e][j] = ak;
-      ak *= ak;
-    }
-    double cp = 1.0;
-    for (int k = 0; k < max_bars - 1; ++k) cp *= A.lin_a[e];
-    A.corr[e] = cp;
-  }
-  A.lag20 = A.corr[0] >= 1e-15;
-  A.lag50 = A.corr[1] >= 1e-15;
-  if (!A.lag20) A.corr[0] = 0.0;
-  if (!A.lag50) A.corr[1] = 0.0;
+  ctx_consts(A, max_bars);
   char* ws = (char*)workspace;
   for (int f = 0; f < 4; ++f) A.gsum[f] = (double*)(ws + L.off_sum[f]);
   A.gcnt = (uint16_t*)(ws + L.off_cnt);

@@ -24,6 +24,7 @@
 #include "bq_device.h"
 #include "binquant_amd.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace bq {
@@ -513,6 +514,19 @@ static double alpha_from_span(double span) {
   return 1.0 / (1.0 + com);
 }
 
+// bq_context.hip: the features through the one-wave-per-symbol context kernel
+int context_features(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t max_bars,
+                     double* const* feat, int64_t ld_out, hipStream_t st);
+
+// BQ_MARKET_FEATURES_IMPL=block: the workgroup-per-symbol features_kernel below
+bool market_features_block() {
+  static const bool on = [] {
+    const char* e = getenv("BQ_MARKET_FEATURES_IMPL");
+    return e && strcmp(e, "block") == 0;
+  }();
+  return on;
+}
+
 }  // namespace bq
 
 extern "C" {
@@ -524,6 +538,8 @@ int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t l
       max_bars < 15 || max_bars > BQ_MAX_HISTORY + 1 || T > (int64_t)0x7fffffff - MF_TT)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;
+  if (!market_features_block() && T <= (int64_t)0x7fffffff - 256 && S <= (int64_t)0x7fffffff)
+    return context_features(hlc, S, T, ld_in, max_bars, feat, ld_out, (hipStream_t)stream);
   FeatArgs A;
   memset(&A, 0, sizeof(A));
   A.h = hlc[0];

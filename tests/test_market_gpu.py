@@ -224,3 +224,49 @@ def test_c5_features_and_breadth_at_shard_size(cuda):
                     assert dev_ctx[k] == v, (t, k)
                 elif isinstance(v, float):
                     assert dev_ctx[k] == pytest.approx(v, rel=1e-9, abs=1e-12), (t, k)
+
+
+_IMPL_CHILD = """
+import sys, numpy as np, torch
+from binquant_amd import engine
+from binquant_amd.synth import numpy_panel
+out = {}
+for S, T, M in ((7, 1300, 400), (5, 900, 200), (3, 600, 15), (4, 2049, 512)):
+    p = numpy_panel(S, T, seed0=S * T + M)
+    d = {k: torch.from_numpy(v).cuda() for k, v in p.items()}
+    f = engine.market_features(d["high"], d["low"], d["close"], max_bars=M)
+    for k, v in f.items():
+        out[f"{S}_{T}_{M}_{k}"] = v.cpu().numpy()
+np.savez(sys.argv[1], **out)
+"""
+
+
+def test_features_wave_and_block_kernels_agree(cuda, tmp_path):
+    """bq_market_features' two kernels — one wave per symbol (the context
+    kernel's feature pass, default) and one workgroup per symbol
+    (BQ_MARKET_FEATURES_IMPL=block) — on the same panels: NaN positions equal,
+    values within 1e-12 of each row's magnitude (their window sums and EMA
+    history terms are associated differently). Exchange klines carry a price
+    in every candle (the store's input): missing closes are outside this
+    path's domain, and the two kernels' window sums treat them differently."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parent.parent)
+    res = {}
+    for impl in ("wave", "block"):
+        out = tmp_path / f"{impl}.npz"
+        env = dict(os.environ, BQ_MARKET_FEATURES_IMPL=impl, PYTHONPATH=root)
+        subprocess.run([sys.executable, "-c", _IMPL_CHILD, str(out)], env=env, check=True, timeout=240)
+        res[impl] = np.load(out)
+    a, b = res["wave"], res["block"]
+    assert set(a.files) == set(b.files)
+    for k in a.files:
+        x, y = a[k], b[k]
+        np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=k)
+        fin = ~np.isnan(y)
+        sc = np.nanmax(np.abs(np.where(fin, y, np.nan)), axis=1, keepdims=True)
+        sc = np.where(np.isfinite(sc) & (sc > 0), sc, 1.0)
+        assert np.all(np.abs(x - y)[fin] <= (1e-12 * np.broadcast_to(sc, y.shape))[fin]), k
