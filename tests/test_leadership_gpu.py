@@ -56,13 +56,18 @@ def test_leadership_panel_vs_oracle(cuda):
     np.testing.assert_array_equal(out["rs_6h"].cpu().numpy(), want[2])
 
 
-@pytest.mark.parametrize("S,T", [(300, 1500), (7, 2500), (3, 97)])
-def test_leadership_fused_equals_staged(cuda, S, T):
+@pytest.mark.parametrize("S,T,bench_gaps", [(300, 1500, True), (7, 2500, True), (3, 97, True), (64, 2600, False),
+                                             (5, 300, False)])
+def test_leadership_fused_equals_staged(cuda, S, T, bench_gaps):
     """bq_leadership (one counting pass) against the staged pipeline (align, fused
     stages, the order-statistic jobs, the integer rolling sum) bit for bit:
     BTC gaps and a duplicated BTC time, zero / negative closes, a late
     listing, symbols on their own time grids; T = 2500 at 7 symbols runs
-    several 256-candle tiles per row (each with its 95-entry history halo)."""
+    several 256-candle tiles per row (each with its 95-entry history halo).
+    Without BTC gaps every row sits on the benchmark's grid and reads the
+    benchmark's shared strength ratios, but the rows given a gap of their
+    own (a skipped candle, a two-hour hole) divide again in the tiles that
+    hold the gap."""
     from binquant_amd import signals
 
     rng = np.random.default_rng(S * 7 + T)
@@ -74,9 +79,14 @@ def test_leadership_fused_equals_staged(cuda, S, T):
     close[0, 500 % T:520 % T] = 0.0
     close[1 % S, 700 % T] = -1.0
     close[2 % S, : T // 3] = 0.0   # late listing
-    keep = rng.random(T + 40) > 0.03
-    bt = grid[keep]
-    bt = np.sort(np.concatenate([bt, bt[5:6]]))   # a duplicated time: the later row wins
+    if bench_gaps:
+        keep = rng.random(T + 40) > 0.03
+        bt = grid[keep]
+        bt = np.sort(np.concatenate([bt, bt[5:6]]))   # a duplicated time: the later row wins
+    else:
+        bt = np.concatenate([grid, grid[-1] + 900_000 * np.arange(1, 41, dtype=np.int64)])
+        times[3 % S, T // 2:] += 900_000        # a skipped candle
+        times[4 % S, T // 3:] += 8 * 900_000    # a two-hour hole
     bc = 30_000.0 * np.exp(np.cumsum(rng.normal(0, 0.004, bt.size)))
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     for q in (0.80, 0.55):   # the strategy's RS_QUANTILE and another (the count test holds for any q)
