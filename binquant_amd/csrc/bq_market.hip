@@ -518,13 +518,16 @@ static double alpha_from_span(double span) {
 int context_features(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in, int32_t max_bars,
                      double* const* feat, int64_t ld_out, hipStream_t st);
 
-// BQ_MARKET_FEATURES_IMPL=block: the workgroup-per-symbol features_kernel below
-bool market_features_block() {
-  static const bool on = [] {
+// BQ_MARKET_FEATURES_IMPL=block / wave forces the workgroup-per-symbol
+// features_kernel below / the context kernel's feature pass (default: by rows)
+int market_features_impl() {   // 0 auto, 1 block, 2 wave
+  static const int v = [] {
     const char* e = getenv("BQ_MARKET_FEATURES_IMPL");
-    return e && strcmp(e, "block") == 0;
+    if (e && strcmp(e, "block") == 0) return 1;
+    if (e && strcmp(e, "wave") == 0) return 2;
+    return 0;
   }();
-  return on;
+  return v;
 }
 
 }  // namespace bq
@@ -538,7 +541,11 @@ int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t l
       max_bars < 15 || max_bars > BQ_MAX_HISTORY + 1 || T > (int64_t)0x7fffffff - MF_TT)
     return BQ_EINVAL;
   if (S == 0 || T == 0) return BQ_OK;
-  if (!market_features_block() && T <= (int64_t)0x7fffffff - 256 && S <= (int64_t)0x7fffffff)
+  // one wave per row once the rows fill the chip (3 waves per SIMD x 1 024
+  // SIMDs); fewer rows — the C5 step's one benchmark row — walk faster on a
+  // workgroup each (1 x 10 000: 0.10 against 0.18 ms)
+  const int impl = market_features_impl();
+  if (impl != 1 && (impl == 2 || S >= 4096) && T <= (int64_t)0x7fffffff - 256 && S <= (int64_t)0x7fffffff)
     return context_features(hlc, S, T, ld_in, max_bars, feat, ld_out, (hipStream_t)stream);
   FeatArgs A;
   memset(&A, 0, sizeof(A));
