@@ -100,24 +100,26 @@ __device__ __forceinline__ void cx_load(const double* __restrict__ row, int tb, 
   }
 }
 
-// a / b with the hardware reciprocal + CX_NR Newton steps. Measured on gfx950
-// over 4M mantissas x 2^[-60,60] (tools/rcp_probe.hip): 0 steps 4.6e-8 max
-// relative error (fails the 1e-9 contract), 1 step 2.2e-15, 2 steps equal to
-// the IEEE quotient on every sample, so the features match numpy's a / b.
+// 1 / |b| with the hardware reciprocal + CX_NR Newton steps. Measured on
+// gfx950 over 4M mantissas x 2^[-60,60] (tools/rcp_probe.hip): 0 steps 4.6e-8
+// max relative error (fails the 1e-9 contract), 1 step 2.2e-15, 2 steps the
+// correctly rounded reciprocal on every sample — a ratio a * r is then within
+// about an ulp of numpy's a / b (not bit for bit: a * RN(1/b) rounds twice).
 // One step would be 2.5% faster at the shard (1.70 -> 1.66 ms); kept at two.
-// The sign of a / b and a zero numerator are exact either way.
-__device__ __forceinline__ double cx_div(double a, double b) {
+__device__ __forceinline__ double cx_rcp(double b) {
 #if CX_NR == 0
-  const double r = __builtin_amdgcn_rcp(fabs(b));
+  return __builtin_amdgcn_rcp(fabs(b));
 #elif CX_NR == 1
   const double v = fabs(b);
-  double r = __builtin_amdgcn_rcp(v);
-  r = fma(r, fma(-v, r, 1.0), r);
+  const double r = __builtin_amdgcn_rcp(v);
+  return fma(r, fma(-v, r, 1.0), r);
 #else
-  const double r = rcp_nr(fabs(b));
+  return rcp_nr(fabs(b));
 #endif
-  return b < 0.0 ? -(a * r) : a * r;
 }
+// a / b from r = cx_rcp(b): the sign of a / b and a zero numerator exact
+__device__ __forceinline__ double cx_mul_rcp(double a, double b, double r) { return b < 0.0 ? -(a * r) : a * r; }
+__device__ __forceinline__ double cx_div(double a, double b) { return cx_mul_rcp(a, b, cx_rcp(b)); }
 
 // DIV: pandas' EMA divide by (old_wt + new_wt) is needed (not exactly 1.0)
 // RING: span 50's history term from the D ring (long caps); otherwise the
@@ -359,6 +361,12 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
       }
     }
     double fr[CX_K], fe20[CX_K], fe50[CX_K], ftr[CX_K], fap[CX_K], fbw[CX_K];
+    // the closes' reciprocals, each shared by candle k's ATR ratio and candle
+    // k + 1's return (5 per lane instead of 8: the same r, the same bits)
+    double rc[CX_K + 1];
+    rc[0] = cx_rcp(p1);
+#pragma unroll
+    for (int k = 0; k < CX_K; ++k) rc[k + 1] = cx_rcp(c[k]);
 #pragma unroll
     for (int k = 0; k < CX_K; ++k) {
       const int t = tb + k;
@@ -381,11 +389,11 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
         s = 0.0;
       }
       const double up = m + (2.0 * s), lo = m - (2.0 * s);
-      fr[k] = prev == 0.0 ? 0.0 : cx_div(cl - prev, prev);   // safe_pct (shared/utils.py:20-23)
+      fr[k] = prev == 0.0 ? 0.0 : cx_mul_rcp(cl - prev, prev, rc[k]);   // safe_pct (shared/utils.py:20-23)
       fe20[k] = e20;
       fe50[k] = e50;
       ftr[k] = e50 != 0.0 ? cx_div(e20 - e50, e50 < 0.0 ? -e50 : e50) : 0.0;
-      fap[k] = cl != 0.0 ? cx_div(a, cl) : 0.0;
+      fap[k] = cl != 0.0 ? cx_mul_rcp(a, cl, rc[k + 1]) : 0.0;
       fbw[k] = m != 0.0 ? cx_div(up - lo, m < 0.0 ? -m : m) : 0.0;
     }
     if constexpr (FEAT) {
