@@ -883,6 +883,10 @@ __global__ __launch_bounds__(256) void slide_rank_kernel(const RollBatch B) {
   }
 }
 
+#ifndef BQ_SG_C
+#define BQ_SG_C 8   // steps per chunk of slide_group_kernel (4: 0.64 vs 0.61 ms at w = 80)
+#endif
+
 // ---- slide rank kernel, lane groups (w >= 48) -----------------------------------------
 // slide_rank_kernel's sorted window split over G = 2 or 4 adjacent lanes:
 // lane q of a group holds slots q H .. q H + H - 1 (H = W / G), so a lane
@@ -914,9 +918,6 @@ __global__ __launch_bounds__(256) void slide_group_kernel(const RollBatch B) {
   constexpr int H = W / G;
   constexpr int KL = K / H;   // the lane holding the rank slots
   static_assert((G == 2 || G == 4) && W % G == 0 && (K + 1) / H == KL && K + 1 < W, "group layout");
-#ifndef BQ_SG_C
-#define BQ_SG_C 8
-#endif
   constexpr int SL_C = BQ_SG_C;
   const RollJob& A = B.j[blockIdx.y];
   const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
