@@ -643,7 +643,7 @@ def time_enrich(panel, steps: int, warmup: int, world: int):
     ranks) and mean enrich_kernel time (HIP events on the launch stream)."""
     S, T = panel["close"].shape
     dev = panel["close"].device
-    out = {k: torch.empty((S, T), dtype=torch.float64, device=dev) for k in ENRICH_COLUMNS}
+    out = engine.enrich_outputs(S, T, dev)   # padded row pitch (engine.enrich_outputs)
     stream = torch.cuda.current_stream()
 
     def step():
