@@ -178,3 +178,24 @@ def test_c4_shard_size_properties(cuda):
     want = ref.enrich_panel(host["open"], host["high"], host["low"], host["close"], host["volume"])
     got = {k: v[rows].cpu().numpy() for k, v in out.items()}
     compare(got, want, host)
+
+
+def test_padded_output_pitch_is_bit_equal(cuda):
+    """engine.enrich_outputs (views of [S, T + 64] buffers on large panels:
+    the HBM-friendly row pitch the bench uses) gives the same bits as the
+    default contiguous outputs."""
+    import numpy as np
+    import torch
+
+    from binquant_amd import engine
+    from binquant_amd.synth import numpy_panel
+
+    S, T = 1100, 1500
+    p = {k: torch.from_numpy(v).cuda() for k, v in numpy_panel(S, T, seed0=9).items()}
+    args = [p[k] for k in ("open", "high", "low", "close", "volume")]
+    out = engine.enrich_outputs(S, T, "cuda")
+    assert next(iter(out.values())).stride(0) == T + engine.ENRICH_ROW_PAD
+    a = engine.enrich(*args, out=out)
+    b = engine.enrich(*args)
+    for k in b:
+        np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
