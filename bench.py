@@ -18,8 +18,8 @@ Also reported (same JSON line):
   cpu_baseline — the oracle's pandas per-symbol path in the reference's call
                  pattern at C1 (500-candle frame: indicators_enrichment +
                  _compute_symbol_features per symbol) over a
-                 process pool sized to the host's CPU share, rank 0 at N=1,
-                 time-bounded sample;
+                 process pool sized to the host's CPU share, rank 0 at every
+                 N (after the timed legs), time-bounded sample;
   tick         — C3: 10k symbols, one candle per tick, H2D + bq_tick + D2H
                  latency p50/p99;
   breadth      — C5 (configs[4]) end to end: market_context_batch = the fused
@@ -47,6 +47,7 @@ import json
 import os
 import sys
 import time
+from datetime import timedelta
 
 import numpy as np
 import pandas as pd
@@ -96,10 +97,13 @@ def launch_ranks(args) -> int | None:
     """`bench.py --gpus N` run by itself (no WORLD_SIZE in the environment,
     N > 1): start N fresh child interpreters of this script, one per GPU
     (RANK = LOCAL_RANK = i, WORLD_SIZE = N, rendezvous on 127.0.0.1 at a free
-    port), wait for all of them and return the worst exit code; rank 0
-    prints the JSON line. Called before anything touches the GPU in this
-    process (the children are new processes, not an exec of this one).
-    Returns None when this process is itself a rank."""
+    port), poll them and return 0 when all succeed; rank 0 prints the JSON
+    line. The first rank to exit non-zero ends the run: the others (which
+    would otherwise wait in the rendezvous or a collective for the missing
+    rank) are terminated and that rank's code is returned. Called before
+    anything touches the GPU in this process (the children are new
+    processes, not an exec of this one). Returns None when this process is
+    itself a rank."""
     if "WORLD_SIZE" in os.environ or args.gpus <= 1:
         return None
     import socket
@@ -113,9 +117,24 @@ def launch_ranks(args) -> int | None:
         env = dict(os.environ, RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            print(f"bench.py: a rank exited with code {bad[0]}; the other ranks were stopped", file=sys.stderr)
+            return bad[0]
+        if all(rc == 0 for rc in rcs):
+            return 0
+        time.sleep(0.2)
 
 
 def setup_dist(args):
@@ -130,15 +149,21 @@ def setup_dist(args):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s); "
                          "run `bench.py --gpus N` alone (it starts N ranks) or under "
                          "torch.distributed.run --nproc-per-node N")
+    fail = os.environ.get("BQ_BENCH_FAIL_RANK", "")   # test hook: "rank:code" exits that rank at start-up
+    if fail and int(fail.split(":")[0]) == rank:
+        raise SystemExit(int(fail.split(":")[1]))
     backend = os.environ.get("BQ_BENCH_BACKEND", "nccl")
+    timeout = timedelta(seconds=float(os.environ.get("BQ_BENCH_PG_TIMEOUT", "600")))
     if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
+        # rendezvous first: a rank that never arrives leaves the others in
+        # init_process_group, before any device call (launch_ranks stops them)
+        if world > 1:
+            dist.init_process_group("gloo", timeout=timeout)
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        return world, rank, local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        if backend == "gloo":
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     return world, rank, local
 
 
@@ -253,18 +278,25 @@ def cpu_baseline(args):
     }
 
 
-def pmc_traffic(kernel: str, candles: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this
-    workload (profiles/pmc_traffic.json); null when the summary was taken on
-    another panel size."""
+def pmc_entry(kernel: str, candles: int) -> dict:
+    """The committed rocprofv3 PMC summary of this workload
+    (profiles/pmc_traffic.json); empty when it was taken on another panel
+    size (the source tag is kept)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f).get(kernel, {})
     except (OSError, ValueError):
-        return None, None
+        return {}
     if d.get("candles_per_launch") != candles:
-        return None, d.get("source")
+        return {"source": d.get("source")}
+    return d
+
+
+def pmc_traffic(kernel: str, candles: int):
+    """HBM bytes per launch from the committed PMC summary (pmc_entry); null
+    when the summary was taken on another panel size."""
+    d = pmc_entry(kernel, candles)
     return d.get("bytes_per_launch"), d.get("source")
 
 
@@ -373,7 +405,10 @@ def bench_breadth(args, panel, world, dev):
     unfused_ms = _time_call(lambda: (engine.market_features(h, l, c, max_bars=400, out=feats),
                                      engine.breadth_partial(c, feats, out=up)), reps=2)
     del feats, up
-    traffic, traffic_src = pmc_traffic("context_partials", S * T)
+    # traffic / VALU from the committed PMC of all three passes per call at
+    # this shape (tools/row_profile.sh context + tools/context_traffic.py)
+    pe = pmc_entry("context_partials", S * T)
+    traffic, traffic_src = pe.get("bytes_per_launch"), pe.get("source")
     return {
         "value": n_total * T / dt,
         "unit": "symbol-candles/s",
@@ -390,8 +425,14 @@ def bench_breadth(args, panel, world, dev):
                     + "benchmark features, D2H, score_contexts + annotate_market of all T contexts",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "bq_context_partials", "kernel_ms": kern_ms,
-                     "algorithmic_bytes_per_candle": CONTEXT_BYTES_PER_CANDLE, "candles_per_launch": S * T},
+                     "traffic_scope": pe.get("scope"),
+                     "traffic_by_pass": {k: v.get("traffic_bytes") for k, v in (pe.get("kernels") or {}).items()},
+                     "kernel": "bq_context_partials (passes 1 + 2 + 3)", "kernel_ms": kern_ms,
+                     "algorithmic_bytes_per_candle": CONTEXT_BYTES_PER_CANDLE, "candles_per_launch": S * T,
+                     # pass 1 is bound by its instruction stream as much as by HBM
+                     "valu": {k: v for k, v in (pe.get("valu") or {}).items()
+                              if k in ("kernel", "valu_lane_ops_per_candle", "valu_busy_est", "valu_active_share")}
+                     or None},
         "unfused_ms": unfused_ms,
     }
 
@@ -568,7 +609,7 @@ def bench_cohort(args, dev):
     # per symbol, on a bounded sample of the cohort's own frames
     from oracle import indicators_ref, market_ref
 
-    n_sample = 24
+    n_sample = min(24, S)
     h5 = {k: p5[k][:n_sample].cpu().numpy() for k in ("open", "high", "low", "close", "volume")}
     h15 = {k: p15[k][:n_sample].cpu().numpy() for k in ("open", "high", "low", "close", "volume")}
     t0 = time.perf_counter()
@@ -735,17 +776,19 @@ def main():
         }
         del shard
         torch.cuda.empty_cache()
-    if rank == 0 and world == 1 and not args.no_tick:
+    # rank 0 only, after every timed multi-rank leg (the other ranks wait in
+    # the closing barrier): C3 and the store tick are one-GPU latencies, so
+    # they run at every world size; the per-row legs at N = 1 only; the CPU
+    # baseline at every world size (north_star: the reference CPU path beside
+    # the GPU figure at 1, 2, 4 and 8 GPUs)
+    if rank == 0 and not args.no_tick:
         result["tick"] = bench_tick(args, dev)
         result["store"] = bench_store(args, dev)
     if rank == 0 and world == 1 and not args.no_rows:
         result["rows"] = bench_rows(args, dev)
         result["live"] = bench_live(args, dev)
         result["cohort"] = bench_cohort(args, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args)
-    else:
-        result["cpu_baseline"] = None
+    result["cpu_baseline"] = cpu_baseline(args) if rank == 0 and not args.no_cpu_baseline else None
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -201,7 +201,8 @@ def enrich_outputs(S: int, T: int, device, columns=ENRICH_COLUMNS) -> dict[str, 
     exactly T doubles (80 000 B at T = 10 000) the concurrently resident
     workgroups' output streams meet the same HBM channels: the C4 shard
     (12 500 x 10 000) ran at 0.666 of 8 TB/s, at 0.711 with the 512-B pad
-    (tools/shard_pitch.py). Small panels get plain [S, T] tensors."""
+    (tools/shard_pitch.py). Small panels get plain [S, T] tensors.
+    enrich() allocates its own outputs this way too."""
     pad = ENRICH_ROW_PAD if S >= 1024 and T >= 1024 else 0
     return {k: torch.empty((S, T + pad), dtype=torch.float64, device=device)[:, :T] for k in columns}
 
@@ -239,11 +240,20 @@ def enrich(
     if unknown:
         raise ValueError(f"unknown enrich columns: {sorted(unknown)}")
     out = dict(out or {})
-    for name in cols:
-        if name not in out:
-            out[name] = torch.empty((S, T), dtype=torch.float64, device=close.device)
+    given = [n for n in cols if n in out]
+    for name in given:
+        _check_panel(out[name], f"out[{name}]", (S, T))
+    missing = [n for n in cols if n not in out]
+    if missing:
+        # the columns this call allocates share the caller's pitch when some
+        # are given, else enrich_outputs' rule (a padded pitch on large panels:
+        # the layout the bench times is the one every product caller gets)
+        if given:
+            ld = _row_stride(out[given[0]])
+            out.update({n: torch.empty((S, max(ld, T)), dtype=torch.float64, device=close.device)[:, :T]
+                        for n in missing})
         else:
-            _check_panel(out[name], f"out[{name}]", (S, T))
+            out.update(enrich_outputs(S, T, close.device, missing))
     ld_out = T
     if out:
         strides = {_row_stride(out[n]) for n in cols}
@@ -1256,7 +1266,9 @@ def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, 
     host synchronisation), so no row is ever cut. An int capacity (fixed
     geometry, e.g. a captured graph) gives C = max(T, capacity) without the
     synchronisation; a row with more pairs than C is then cut at C, keeping
-    its oldest pairs — size it from the benchmark's repeats."""
+    its oldest pairs — size it from the benchmark's repeats. capacity=None
+    cannot be used under hipGraph capture (it reads the repeat check back to
+    the host): a capturing caller gets a ValueError asking for capacity."""
     ts = _check_ts(ts)
     S, T = ts.shape
     close = _check_panel(close, "close", (S, T)).contiguous()
@@ -1264,6 +1276,9 @@ def join_returns(ts: torch.Tensor, close: torch.Tensor, bench_ts: torch.Tensor, 
     bc = _check_panel(bench_close.reshape(1, -1), "bench_close", (1, bts.numel())).contiguous()
     lens = _check_lens(lens, S, ts.device)
     if capacity is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise ValueError("join_returns: capacity=None synchronises with the host and cannot run under "
+                             "graph capture; pass capacity= (e.g. T when the benchmark repeats no time)")
         capacity = _join_capacity(ts, lens, bts)
     C = max(T, int(capacity))
     x = torch.empty((S, C), dtype=torch.float64, device=ts.device)

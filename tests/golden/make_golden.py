@@ -47,7 +47,19 @@ Fixtures:
                         helpers; outputs recorded at 48 sampled positions per symbol
                         (panel_gen.sample_positions: last rows, tile boundary, random)
 
-Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf,btc_change]
+  headline_twins.npz    per-candle pins of the headline enrich columns from the reference's
+                        own twins, on every prefix of 4 frames (random walk across a
+                        1024-candle tile, a 1e-3-priced walk, constant runs, NaN gaps):
+                        LiveMarketContextAccumulator._compute_symbol_features (ema20, ema50,
+                        atr_pct = rolling-14 TR mean / close, bb_width = ddof-0 rolling-20
+                        (upper - lower) / |mid|, trend_score; :256-272),
+                        BBExtremeReversion._compute_rsi (SMA RSI, windows 14 and 6;
+                        bb_extreme_reversion.py:134-150) and MeanReversionFade._trend_score
+                        with its EMA windows set to 9 / 21 — the expression of
+                        price_tracker.py:204-205 and inverse_price_tracker.py:157-158 —
+                        and at its own 20 / 50 (mean_reversion_fade.py:150-155)
+
+Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf,btc_change,twins]
 """
 
 from __future__ import annotations
@@ -168,6 +180,8 @@ def child(out_dir: Path, only: set[str] | None = None) -> None:
             inf_windows(out_dir)
         if "btc_change" in only:
             btc_change(out_dir)
+        if "twins" in only:
+            headline_twins(out_dir)
         return
     import numpy as np
     import pandas as pd
@@ -967,6 +981,75 @@ def btc_change(out_dir: Path) -> None:
         out[f"{name}__last"] = np.float64(last)
     np.savez_compressed(out_dir / "btc_change.npz", **out)
     print("btc_change.npz", len(cases), "cases, pandas", pd.__version__)
+
+
+def headline_twins(out_dir: Path) -> None:
+    """Per-candle values of the reference's in-repo twins of the headline
+    enrich columns (pybinbot itself is absent), each real function called on
+    every prefix df.iloc[:k] (they read the last row). See the module
+    docstring; tests/test_twins_gpu.py runs bq_enrich with the matching
+    IndicatorParams against them."""
+    import numpy as np
+    import pandas as pd
+
+    from market_regime.live_market_context_accumulator import LiveMarketContextAccumulator
+    from strategies.coinrule.bb_extreme_reversion import BBExtremeReversion
+    from strategies.mean_reversion_fade import MeanReversionFade
+
+    class TrendScore921(MeanReversionFade):   # price_tracker.py:204-205's spans through the real method
+        EMA_FAST_WINDOW = 9
+        EMA_SLOW_WINDOW = 21
+
+    rng = np.random.default_rng(20261019)
+
+    def walk(n, scale, vol):
+        c = scale * np.exp(np.cumsum(rng.normal(0, vol, n)))
+        o = np.r_[c[0], c[:-1]]
+        h = np.maximum(o, c) * (1 + rng.uniform(0, 0.003, n))
+        l = np.minimum(o, c) * (1 - rng.uniform(0, 0.003, n))
+        return o, h, l, c, rng.lognormal(3, 1, n)
+
+    frames = {}
+    frames["walk"] = walk(1100, 100.0, 0.004)
+    frames["tiny"] = walk(400, 1e-3, 0.01)
+    o, h, l, c, v = walk(600, 25.0, 0.006)
+    for a, b in ((100, 140), (300, 330), (500, 505)):   # constant runs: flat candles
+        c[a:b] = c[a - 1]
+        o[a:b] = h[a:b] = l[a:b] = c[a - 1]
+    frames["runs"] = (o, h, l, c, v)
+    o, h, l, c, v = walk(600, 3.0, 0.005)
+    for a, b in ((50, 51), (200, 203), (450, 451), (451, 452)):   # missing candles (close, high, low)
+        c[a:b] = h[a:b] = l[a:b] = np.nan
+    frames["gaps"] = (o, h, l, c, v)
+    feat_cols = ["ema20", "ema50", "atr_pct", "bb_width", "trend_score", "return_pct"]
+    out = {}
+    for name, (o, h, l, c, v) in frames.items():
+        n = len(c)
+        df = pd.DataFrame({"timestamp": 1_700_000_000_000 + 300_000 * np.arange(n), "open": o, "high": h,
+                           "low": l, "close": c, "volume": v})
+        for col in ("open", "high", "low", "close", "volume"):
+            out[f"{name}__{col}"] = df[col].to_numpy(dtype=float)
+        feats = np.full((n, len(feat_cols)), np.nan)
+        for k in range(2, n + 1):
+            f = LiveMarketContextAccumulator._compute_symbol_features("SYMUSDT", df.iloc[:k])
+            if f is not None:
+                feats[k - 1] = [float(getattr(f, col)) for col in feat_cols]
+        out[f"{name}__features"] = feats
+        for w in (14, 6):
+            r = np.full(n, np.nan)
+            for k in range(1, n + 1):
+                val = BBExtremeReversion._compute_rsi(df["close"].iloc[:k], w)
+                if val is not None:
+                    r[k - 1] = val
+            out[f"{name}__sma_rsi{w}"] = r
+        out[f"{name}__trend_9_21"] = np.array([TrendScore921._trend_score(df["close"].iloc[:k])
+                                               for k in range(1, n + 1)])
+        out[f"{name}__trend_20_50"] = np.array([MeanReversionFade._trend_score(df["close"].iloc[:k])
+                                                for k in range(1, n + 1)])
+    out["names"] = np.array(list(frames))
+    out["feature_columns"] = np.array(feat_cols)
+    np.savez_compressed(out_dir / "headline_twins.npz", **out)
+    print("headline_twins.npz", list(frames), "pandas", pd.__version__)
 
 
 def pd_frame(rows):

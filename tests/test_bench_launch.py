@@ -27,15 +27,32 @@ def test_world_mismatch_fails_before_any_gpu_call():
     assert "--gpus 4 but the launcher started 2 rank(s)" in r.stderr
 
 
+def test_failing_rank_ends_the_run():
+    """a rank that exits non-zero at start-up (here rank 1, by the
+    BQ_BENCH_FAIL_RANK test hook) must end the self-launched run with its
+    code; rank 0, left waiting in the gloo rendezvous for it, is stopped by
+    the parent instead of hanging until the process-group timeout."""
+    import time
+
+    t0 = time.perf_counter()
+    r = _bench(["--gpus", "2"], {"BQ_BENCH_BACKEND": "gloo", "BQ_BENCH_FAIL_RANK": "1:7",
+                                 "BQ_BENCH_PG_TIMEOUT": "300"}, 200)
+    assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
+    assert "the other ranks were stopped" in r.stderr
+    assert time.perf_counter() - t0 < 150
+
+
 @pytest.mark.gpu
 def test_bench_gpus_2_self_launch_gloo(cuda):
     """On the one-GPU box: `BQ_BENCH_BACKEND=gloo bench.py --gpus 2` (two
     ranks sharing the GPU, collectives over gloo) reports n_gpus 2, the
-    whole panel's symbols, and the breadth leg's tracked total from the one
-    all-reduce equal to every symbol of both shards."""
+    whole panel's symbols, the breadth leg's tracked total from the one
+    all-reduce equal to every symbol of both shards, and the CPU baseline
+    (rank 0, at every world size) present."""
     S, T = 3000, 512
     r = _bench(["--gpus", "2", "--symbols", str(S), "--candles", str(T), "--steps", "2", "--warmup", "1",
-                "--no-shard", "--no-tick", "--no-rows", "--no-cpu-baseline", "--breadth-steps", "1"],
+                "--no-shard", "--no-tick", "--no-rows", "--breadth-steps", "1",
+                "--cpu-seconds", "1", "--cpu-workers", "2"],
                {"BQ_BENCH_BACKEND": "gloo"}, 240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -45,3 +62,5 @@ def test_bench_gpus_2_self_launch_gloo(cuda):
     assert res["config"]["symbols"] == S and res["config"]["symbols_per_gpu"] == S // 2
     assert res["breadth"]["tracked_symbols"] == S
     assert res["value"] > 0
+    cb = res["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] == "port"
