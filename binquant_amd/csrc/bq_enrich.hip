@@ -356,6 +356,150 @@ __device__ __forceinline__ int win_of(int def, int v) {
   return DEF ? def : __builtin_amdgcn_readfirstlane(v);
 }
 
+// ---- rows holding a missing or non-finite input ------------------------------
+// The tile walk assumes finite candles: a NaN close would poison the close
+// prefix and the EMA scan for the rest of the row, and the sliding window sums
+// for the rest of a lane's block. pandas instead treats a missing value (and,
+// through _prep_values, +-inf) as an absent observation: a rolling window
+// holding one is NaN (min_periods = window), ewm(adjust=False, ignore_na=False)
+// decays its old weight across the gap and resumes (aggregations.pyx ewm).
+// A workgroup whose row held one recomputes the whole row here after the walk
+// — pandas' elementwise series and window definitions candle by candle
+// (oracle/indicators_ref.py: SMA RSI via delta.where, MFI flows via tp.where,
+// skip-NaN true range, the same-value rule of rolling mean / var), the EMA
+// family as pandas' serial recursion (bit for bit) — and overwrites its
+// outputs. Real klines never take this path (Binance candles always carry
+// prices); it exists so that a drop-in frame with gaps gets pandas' answer.
+struct WinAgg {
+  double sum, first;
+  bool ok, same;
+};
+
+template <typename F>
+__device__ __forceinline__ WinAgg win_agg(F val, int t, int w) {
+  WinAgg a = {0.0, 0.0, t >= w - 1, true};
+  if (!a.ok) return a;
+  a.first = val(t - w + 1);
+  for (int j = t - w + 1; j <= t; ++j) {
+    const double x = val(j);
+    if (!__builtin_isfinite(x)) {
+      a.ok = false;
+      return a;
+    }
+    a.same &= x == a.first;
+    a.sum += x;
+  }
+  return a;
+}
+
+// pandas ewm(adjust=False, ignore_na=False) state: weighted (NaN before the
+// first observation), old_wt
+__device__ __forceinline__ double ewm_gap_step(double& wt, double& old, double x, double al, double om) {
+  const bool obs = __builtin_isfinite(x);   // _prep_values: +-inf -> NaN
+  if (wt == wt) {
+    old *= om;
+    if (obs) {
+      if (wt != x) {
+        wt = old * wt + al * x;
+        wt /= (old + al);
+      }
+      old = 1.0;
+    }
+  } else if (obs) {
+    wt = x;
+  }
+  return wt;
+}
+
+__device__ __forceinline__ void enrich_row_missing(const EnrichArgs& P, const EmaConsts& E, int64_t irow, int64_t orow,
+                                                double* bc, double* b0, double* b1, double* b2, double* b3) {
+  const int tid = threadIdx.x, T = P.T;
+  const double* __restrict__ po = P.in[BQ_OPEN] + irow;
+  const double* __restrict__ ph = P.in[BQ_HIGH] + irow;
+  const double* __restrict__ pl = P.in[BQ_LOW] + irow;
+  const double* __restrict__ pc = P.in[BQ_CLOSE] + irow;
+  const double* __restrict__ pv = P.in[BQ_VOLUME] + irow;
+  auto C = [&](int j) { return j >= 0 ? pc[j] : qnan(); };
+  auto TP = [&](int j) { return j >= 0 ? typical_price(ph[j], pl[j], pc[j]) : qnan(); };
+  auto put = [&](int col, int t, double v) {
+    if (P.out[col]) P.out[col][orow + t] = v;
+  };
+  auto mean_of = [&](const WinAgg& a, int w) { return !a.ok ? qnan() : (a.same ? a.first : a.sum / (double)w); };
+  for (int t = tid; t < T; t += EN_NT) {
+    for (int i = 0; i < 3; ++i)
+      if (P.out[BQ_MA_FAST + i]) put(BQ_MA_FAST + i, t, mean_of(win_agg(C, t, P.ma[i]), P.ma[i]));
+    if (P.out[BQ_BB_UPPER] || P.out[BQ_BB_MID] || P.out[BQ_BB_LOWER]) {
+      const int w = P.bb_w;
+      const WinAgg a = win_agg(C, t, w);
+      double m = qnan(), sd = qnan();
+      if (a.ok) {
+        m = mean_of(a, w);
+        double ss = 0.0;
+        if (!a.same)
+          for (int j = t - w + 1; j <= t; ++j) {
+            const double d = pc[j] - m;
+            ss += d * d;
+          }
+        sd = w - P.bb_ddof > 0 ? sqrt(ss / (double)(w - P.bb_ddof)) : qnan();
+      }
+      put(BQ_BB_MID, t, m);
+      put(BQ_BB_UPPER, t, m + (P.bb_k * sd));
+      put(BQ_BB_LOWER, t, m - (P.bb_k * sd));
+    }
+    if (P.out[BQ_TWAP])
+      put(BQ_TWAP, t, mean_of(win_agg([&](int j) { return ohlc4(po[j], ph[j], pl[j], pc[j]); }, t, P.twap_w),
+                              P.twap_w));
+    if (P.out[BQ_ATR])
+      put(BQ_ATR, t, mean_of(win_agg([&](int j) { return true_range(ph[j], pl[j], C(j - 1)); }, t, P.atr_w),
+                             P.atr_w));
+    if (P.out[BQ_RSI]) {   // delta.where(delta > 0, 0.0): a missing delta is a 0 gain and loss
+      const int w = P.rsi_w;
+      const WinAgg g = win_agg([&](int j) { const double d = C(j) - C(j - 1); return d > 0.0 ? d : 0.0; }, t, w);
+      const WinAgg l = win_agg([&](int j) { const double d = C(j) - C(j - 1); return d < 0.0 ? -d : 0.0; }, t, w);
+      const double rs = mean_of(g, w) / mean_of(l, w);
+      put(BQ_RSI, t, 100.0 - (100.0 / (1.0 + rs)));
+    }
+    if (P.out[BQ_MFI]) {   // mf.where(tp > prev, 0.0) / mf.where(tp < prev, 0.0), rolling sums
+      const int w = P.mfi_w;
+      const WinAgg p = win_agg([&](int j) { const double tp = TP(j); return tp > TP(j - 1) ? tp * pv[j] : 0.0; }, t, w);
+      const WinAgg n = win_agg([&](int j) { const double tp = TP(j); return tp < TP(j - 1) ? tp * pv[j] : 0.0; }, t, w);
+      const double ps = p.ok ? p.sum : qnan(), ns = n.ok ? n.sum : qnan();
+      put(BQ_MFI, t, 100.0 - (100.0 / (1.0 + ps / ns)));
+    }
+  }
+  // the EMA family: pandas' recursion, serial, closes staged through LDS
+  const bool ema = P.out[BQ_MACD] || P.out[BQ_MACD_SIGNAL] || P.out[BQ_EMA_FAST] || P.out[BQ_EMA_SLOW];
+  if (!ema) return;
+  double wf = qnan(), of = 1.0, ws = qnan(), os = 1.0, wg = qnan(), og = 1.0, we = qnan(), oe = 1.0;
+  for (int c0 = 0; c0 < T; c0 += EN_TT) {
+    const int n = min(EN_TT, T - c0);
+    __syncthreads();   // the previous chunk's results are stored
+    for (int i = tid; i < n; i += EN_NT) bc[i] = pc[c0 + i];
+    __syncthreads();
+    if (tid == 0) {   // macd fast / slow and the signal EMA of their difference
+      for (int i = 0; i < n; ++i) {
+        const double x = bc[i];
+        const double f = ewm_gap_step(wf, of, x, E.al[E_FAST], E.om[E_FAST]);
+        const double s = ewm_gap_step(ws, os, x, E.al[E_SLOW], E.om[E_SLOW]);
+        const double m = f - s;
+        b0[i] = m;
+        b1[i] = ewm_gap_step(wg, og, m, E.al[E_SIG], E.om[E_SIG]);
+      }
+    } else if (tid == WAVE || tid == 2 * WAVE) {   // ema_spans[0] / [1] on waves 1 / 2
+      const int e = tid == WAVE ? E_0 : E_1;
+      double* dst = tid == WAVE ? b2 : b3;
+      for (int i = 0; i < n; ++i) dst[i] = ewm_gap_step(we, oe, bc[i], E.al[e], E.om[e]);
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += EN_NT) {
+      put(BQ_MACD, c0 + i, b0[i]);
+      put(BQ_MACD_SIGNAL, c0 + i, b1[i]);
+      put(BQ_EMA_FAST, c0 + i, b2[i]);
+      put(BQ_EMA_SLOW, c0 + i, b3[i]);
+    }
+  }
+}
+
 template <bool DIV, bool VOUT, bool DEF>
 __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichArgs A, int vec_in) {
   // LDS ring (positions [0, H) = halo from the previous tile, [H, R) = tile)
@@ -368,7 +512,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   __shared__ double sWe[EN_NW][NE];
   __shared__ int sWlc[EN_NW];
   __shared__ double sEcar[NE];
-  __shared__ int sLcar;
+  __shared__ int sLcar, sMiss;
   __shared__ EmaConsts E;
   __shared__ EnrichArgs sA;   // window sizes / output table, re-read from LDS each
                               // tile so the compiler cannot hoist them into registers
@@ -406,6 +550,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
   if (tid < NE) sEcar[tid] = 0.0;
   if (tid == 0) {
     sLcar = -1;
+    sMiss = 0;
     sA = A;
   }
   if (tid < EN_H) {   // candles before the series start: NaN close, zero sums
@@ -437,6 +582,7 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
     // ---- phase 1: per-candle quantities into the LDS ring --------------------
     int lcl[EN_K];
     {
+      bool miss = false;   // a missing / non-finite input among the lane's candles (enrich_row_missing)
       double pc = cu.pc;
       double tpp = typical_price(cu.ph, cu.pl, cu.pc);
       int run = -1;
@@ -446,15 +592,18 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
         const double c = cu.c[k];
         const double tp = typical_price(cu.h[k], cu.l[k], c);
         const double mf = tp * cu.v[k];
+        const double o4 = ohlc4(cu.o[k], cu.h[k], cu.l[k], c);
+        miss |= !__builtin_isfinite(o4) | !__builtin_isfinite(mf);   // any of o, h, l, c, v (or an overflow)
         sC[RS1(k)] = c;
         sTR[RS1(k)] = true_range(cu.h[k], cu.l[k], pc);
-        sO4[RS1(k)] = ohlc4(cu.o[k], cu.h[k], cu.l[k], c);
+        sO4[RS1(k)] = o4;
         sMF[RS1(k)] = tp > tpp ? mf : (tp < tpp ? -mf : 0.0);
         if (t == 0 || c != pc) run = t;
         lcl[k] = run;
         pc = c;
         tpp = tp;
       }
+      if (__builtin_amdgcn_ballot_w64(miss)) sMiss = 1;   // wave-uniform; read after the walk
     }
     // close prefix (compensated), wave-local
     double Ploc[EN_K];
@@ -815,6 +964,8 @@ __global__ __launch_bounds__(EN_NT, BQ_EN_WPS) void enrich_kernel(const EnrichAr
       }
     }
   }
+  __syncthreads();   // sMiss final; orders the walk's stores before a rewrite's
+  if (sMiss) enrich_row_missing(sA, E, irow, orow, sC, sP, sTR, sO4, sMF);
 }
 
 static bool window_ok(int w) { return w >= 1 && w <= BQ_MAX_WINDOW; }

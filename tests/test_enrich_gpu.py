@@ -182,8 +182,10 @@ def test_c4_shard_size_properties(cuda):
 
 def test_padded_output_pitch_is_bit_equal(cuda):
     """engine.enrich_outputs (views of [S, T + 64] buffers on large panels:
-    the HBM-friendly row pitch the bench uses) gives the same bits as the
-    default contiguous outputs."""
+    the HBM-friendly row pitch the bench uses, and engine.enrich's own
+    default allocation on such panels) gives the same bits as contiguous
+    [S, T] outputs; a partial `out` sets the pitch of the columns enrich
+    allocates."""
     import numpy as np
     import torch
 
@@ -196,6 +198,50 @@ def test_padded_output_pitch_is_bit_equal(cuda):
     out = engine.enrich_outputs(S, T, "cuda")
     assert next(iter(out.values())).stride(0) == T + engine.ENRICH_ROW_PAD
     a = engine.enrich(*args, out=out)
-    b = engine.enrich(*args)
+    flat = {k: torch.empty((S, T), dtype=torch.float64, device="cuda") for k in out}
+    b = engine.enrich(*args, out=flat)
+    c = engine.enrich(*args)   # default allocation: the padded pitch
+    assert all(v.stride(0) == T + engine.ENRICH_ROW_PAD for v in c.values())
+    part = engine.enrich(*args, out={"rsi": flat["rsi"]})
+    assert all(v.stride(0) == T for v in part.values())
     for k in b:
         np.testing.assert_array_equal(a[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
+        np.testing.assert_array_equal(c[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
+        np.testing.assert_array_equal(part[k].cpu().numpy(), b[k].cpu().numpy(), err_msg=k)
+
+
+def test_missing_and_nonfinite_inputs_follow_pandas(cuda):
+    """Rows holding NaN or +-inf inputs (a drop-in frame with gaps) take the
+    kernel's per-row rewrite (bq_enrich.hip enrich_row_missing): every column
+    equals the pandas oracle — windows over a gap NaN, pandas' ewm gap decay
+    (bit for bit), SMA RSI / MFI with their where(..., 0.0) rules — while the
+    clean rows of the same launch stay on the tile walk (bit-equal to a launch
+    of the clean rows alone)."""
+    S, T = 12, 2300
+    panel = numpy_panel(S, T, seed0=5)
+    nan, inf = np.nan, np.inf
+    c, h, l, o, v = (panel[k] for k in ("close", "high", "low", "open", "volume"))
+    c[1, 500] = nan                                   # one missing close
+    for k in (c, h, l, o):
+        k[2, 800:806] = nan                           # a missing candle run
+    for k in (c, h, l, o, v):
+        k[3, :40] = nan                               # a late listing: leading NaN
+    v[4, 1200] = inf                                  # inf volume: MFI windows
+    c[5, 1500] = inf                                  # inf close (pandas: missing in windows and ewm)
+    c[6, 1023:1025] = nan                             # across the 1024-candle tile boundary
+    v[7, 300:320] = nan                               # missing volume only
+    c[8, -3:] = nan                                   # trailing NaN
+    h[9, 100::97] = nan                               # scattered missing highs
+    c[10, 0] = nan                                    # missing first close
+    got = run_gpu(panel)
+    want = ref.enrich_panel(panel["open"], panel["high"], panel["low"], panel["close"], panel["volume"])
+    price = np.nanmean(np.where(np.isfinite(c), np.abs(c), np.nan), axis=1, keepdims=True)
+    for k in COLS:
+        assert_close(got[k], want[k], k, scale=100.0 if k in ("rsi", "mfi") else price)
+    for k in ("macd", "macd_signal", "ema20", "ema50"):   # the rewrite replays pandas' recursion
+        bad = [s for s in range(1, 11) if not np.array_equal(got[k][s], want[k][s], equal_nan=True)]
+        assert not bad, (k, bad)
+    clean = {k: v[[0, 11]] for k, v in panel.items()}
+    alone = run_gpu(clean)
+    for k in COLS:
+        np.testing.assert_array_equal(got[k][[0, 11]], alone[k], err_msg=k)
