@@ -204,6 +204,11 @@ enum bq_partial_col {
  * hlc = {high, low, close} device pointers, each [S][ld_in].
  * feat[BQ_NUM_FEATURES] device pointers [S][ld_out] (NULL = skip). Row t = 0
  * (fewer than 2 bars of history -> reference returns None) is NaN.
+ * Domain: finite high / low / close (a panel of exchange klines). A candle
+ * without a close never reaches the reference's features (MarketStateStore
+ * drops it, market_state_store.py:84); histories holding candles without a
+ * high / low (which the store keeps) go through bq_store_features, the
+ * store path's pandas replay. bq_context_partials has the same domain.
  */
 #define BQ_MAX_HISTORY 512
 int bq_market_features(const double* const* hlc, int64_t S, int64_t T, int64_t ld_in,

@@ -59,7 +59,13 @@ Fixtures:
                         price_tracker.py:204-205 and inverse_price_tracker.py:157-158 —
                         and at its own 20 / 50 (mean_reversion_fade.py:150-155)
 
-Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf,btc_change,twins]
+  store_gaps.json       a second scripted store feed (the store_sequence.json format) whose
+                        candles miss their high and / or low — None, non-numeric strings,
+                        NaN — which MarketStateStore keeps (it drops only a missing close,
+                        market_state_store.py:84): _compute_symbol_features' skip-NaN true
+                        range and min_periods=1 windows over such histories
+
+Usage: python tests/golden/make_golden.py [--only pins,panel,leadership,inf,btc_change,twins,store_gaps]
 """
 
 from __future__ import annotations
@@ -182,6 +188,8 @@ def child(out_dir: Path, only: set[str] | None = None) -> None:
             btc_change(out_dir)
         if "twins" in only:
             headline_twins(out_dir)
+        if "store_gaps" in only:
+            store_gaps(out_dir)
         return
     import numpy as np
     import pandas as pd
@@ -925,6 +933,83 @@ def store_sequence(out_dir: Path, context_dict) -> None:
     with open(out_dir / "store_sequence.json", "w") as f:
         json.dump(dict(max_bars=M, btc="BTCUSDT", ops=ops, contexts=contexts, final=final), f,
                   separators=(",", ":"), default=float)
+
+
+def store_gaps(out_dir: Path) -> None:
+    """store_gaps.json: MarketStateStore + LiveMarketContextAccumulator under a
+    feed whose candles miss high / low (kept by the store: only a missing
+    close is dropped) — the features' true range is a skip-NaN max and its
+    rolling(14, min_periods=1) mean skips missing values
+    (live_market_context_accumulator.py:256-268)."""
+    import numpy as np
+
+    from market_regime.live_market_context_accumulator import LiveMarketContextAccumulator
+    from market_regime.market_state_store import MarketStateStore
+
+    def context_dict(ctx):
+        if ctx is None:
+            return None
+        d = ctx.model_dump()
+        d["symbol_features"] = {k: v for k, v in sorted(d["symbol_features"].items())}
+        d["metadata"] = {k: v for k, v in d["metadata"].items() if k != "fresh_symbols"}
+        return d
+
+    rng = np.random.default_rng(4242)
+    M = 40
+    step = 900_000
+    t0 = 1_760_100_000_000
+    syms = ["BTCUSDT"] + [f"G{i:02d}USDT" for i in range(1, 50)]
+    price = {s: float(10 ** rng.uniform(-2, 3)) for s in syms}
+    missing = [None, "n/a", float("nan"), ""]
+
+    def candle(s, k):
+        p = price[s] * float(np.exp(rng.normal(0.0003, 0.007)))
+        price[s] = p
+        o = p * float(np.exp(rng.normal(0, 0.002)))
+        c = dict(timestamp=t0 + k * step, open=o, high=max(o, p) * (1 + float(rng.uniform(0, 0.003))),
+                 low=min(o, p) * (1 - float(rng.uniform(0, 0.003))), close=p, volume=float(rng.lognormal(3, 1)))
+        r = rng.random()
+        if r < 0.12:
+            c["high"] = missing[int(rng.integers(0, 4))]
+        elif r < 0.24:
+            c["low"] = missing[int(rng.integers(0, 4))]
+        elif r < 0.30:
+            c["high"] = c["low"] = missing[int(rng.integers(0, 4))]
+        return c
+
+    store = MarketStateStore(max_bars_per_symbol=M)
+    acc = LiveMarketContextAccumulator(store, btc_symbol="BTCUSDT")
+    ops, contexts = [], []
+    for s in syms:
+        rows = [candle(s, k) for k in range(50)]
+        if s == "G05USDT":   # a stretch where every candle misses both
+            for r in rows[20:36]:
+                r["high"] = r["low"] = None
+        ops.append(dict(op="update", symbol=s, rows=rows))
+        store.update(s, pd_frame(rows))
+    for k in range(50, 58):
+        ts = t0 + k * step
+        for i in rng.permutation(len(syms)):
+            s = syms[i]
+            c = candle(s, k)
+            ops.append(dict(op="on_closed_candle", symbol=s, rows=[c]))
+            ctx = context_dict(acc.on_closed_candle(s, c))
+            if ctx is not None:   # per-symbol rows are kept for the refresh contexts only
+                ctx.pop("symbol_features")
+            contexts.append(ctx)
+        ops.append(dict(op="refresh", ts=ts))
+        contexts.append(context_dict(acc.refresh_context_for_timestamp(ts)))
+    final = {
+        "histories": {s: store.get_symbol_history(s).to_dict(orient="list") for s in syms},
+        "last_closed": {s: store.get_last_closed_timestamp(s) for s in syms},
+        "fresh": {str(t0 + k * step): sorted(store.get_fresh_symbols(t0 + k * step)) for k in range(45, 58)},
+        "tracked": store.get_tracked_symbols(),
+        "latest_context_ts": (acc.get_latest_context().timestamp if acc.get_latest_context() else None),
+    }
+    with open(out_dir / "store_gaps.json", "w") as f:
+        json.dump(dict(max_bars=M, btc="BTCUSDT", ops=ops, contexts=contexts, final=final), f,
+                  separators=(",", ":"), default=float)
+    print("store_gaps.json", len(ops), "ops,", sum(c is not None for c in contexts), "contexts")
 
 
 def btc_change(out_dir: Path) -> None:

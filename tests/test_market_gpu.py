@@ -237,6 +237,14 @@ for S, T, M in ((7, 1300, 400), (5, 900, 200), (3, 600, 15), (4, 2049, 512)):
     f = engine.market_features(d["high"], d["low"], d["close"], max_bars=M)
     for k, v in f.items():
         out[f"{S}_{T}_{M}_{k}"] = v.cpu().numpy()
+# the reference's golden histories (market_features.npz), one row each
+z = np.load(sys.argv[2])
+for name in z["names"]:
+    name = str(name)
+    h, l, c = (torch.from_numpy(np.ascontiguousarray(z[f"{name}__{k}"]))[None].cuda() for k in ("high", "low", "close"))
+    f = engine.market_features(h, l, c, max_bars=400)
+    for k, v in f.items():
+        out[f"golden_{name}_{k}"] = v[:, -1:].cpu().numpy()
 np.savez(sys.argv[1], **out)
 """
 
@@ -246,9 +254,14 @@ def test_features_wave_and_block_kernels_agree(cuda, tmp_path):
     kernel's feature pass, default) and one workgroup per symbol
     (BQ_MARKET_FEATURES_IMPL=block) — on the same panels: NaN positions equal,
     values within 1e-12 of each row's magnitude (their window sums and EMA
-    history terms are associated differently). Exchange klines carry a price
-    in every candle (the store's input): missing closes are outside this
-    path's domain, and the two kernels' window sums treat them differently."""
+    history terms are associated differently); both against the reference's
+    golden histories (market_features.npz; the panel wave kernel is otherwise
+    never run at S = 1). The panel kernels take finite high / low / close
+    (include/binquant_amd.h bq_market_features): a missing close never reaches
+    _compute_symbol_features (MarketStateStore drops the candle,
+    market_state_store.py:84), and candles missing high / low — which the
+    store keeps — go through the device store's pandas replay
+    (tests/test_store_gpu.py, store_gaps.json)."""
     import os
     import subprocess
     import sys
@@ -259,10 +272,23 @@ def test_features_wave_and_block_kernels_agree(cuda, tmp_path):
     for impl in ("wave", "block"):
         out = tmp_path / f"{impl}.npz"
         env = dict(os.environ, BQ_MARKET_FEATURES_IMPL=impl, PYTHONPATH=root)
-        subprocess.run([sys.executable, "-c", _IMPL_CHILD, str(out)], env=env, check=True, timeout=240)
+        subprocess.run([sys.executable, "-c", _IMPL_CHILD, str(out), str(G / "market_features.npz")], env=env,
+                       check=True, timeout=240)
         res[impl] = np.load(out)
     a, b = res["wave"], res["block"]
     assert set(a.files) == set(b.files)
+    z = np.load(G / "market_features.npz")
+    cols = [str(c) for c in z["feature_columns"]]
+    for r in (a, b):   # the golden histories through each kernel
+        for name in z["names"]:
+            name = str(name)
+            got = {k: float(r[f"golden_{name}_{k}"][0, 0]) for k in FEATURE_COLUMNS}
+            if bool(z[f"{name}__none"]):
+                assert all(np.isnan(v) for v in got.values()), name
+                continue
+            want = dict(zip(cols, z[f"{name}__features"]))
+            for k in FEATURE_COLUMNS:
+                assert_close([got[k]], [want[k]], f"{name}.{k}", scale=[abs(want["close"]) * 1e-2 + 1e-300])
     for k in a.files:
         x, y = a[k], b[k]
         np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=k)

@@ -59,10 +59,14 @@ def compare_context(got, want, where):
                     _num_close(float(gf[k]), float(w), f"{where}.{sym}.{k}")
 
 
-def test_store_and_contexts_follow_the_reference(cuda):
+@pytest.mark.parametrize("fixture", ["store_sequence.json", "store_gaps.json"])
+def test_store_and_contexts_follow_the_reference(cuda, fixture):
+    """store_gaps.json: candles missing high and / or low (None, strings,
+    NaN — kept by the store, which drops only a missing close): the features'
+    skip-NaN true range and min_periods=1 ATR window over such histories."""
     from binquant_amd.market_regime.store import DeviceLiveMarketContextAccumulator, DeviceMarketStateStore
 
-    d = json.loads((G / "store_sequence.json").read_text())
+    d = json.loads((G / fixture).read_text())
     store = DeviceMarketStateStore(max_bars_per_symbol=d["max_bars"], capacity=8)   # forces two regrowths
     acc = DeviceLiveMarketContextAccumulator(store, btc_symbol=d["btc"])
     ctxs = iter(d["contexts"])

@@ -20,7 +20,7 @@ from binquant_amd import engine, signals, strategies  # noqa: E402
 from binquant_amd.synth import device_panel  # noqa: E402
 
 name = sys.argv[1]
-big = name in ("enrich", "context")
+big = name in ("enrich", "enrich_flat", "context")
 S, T = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else ((12_500, 10_000) if big else (12_500, 2_000))
 p = device_panel(S, T, seed=99)
 o, h, l, c, v = (p[k] for k in ("open", "high", "low", "close", "volume"))
@@ -28,8 +28,18 @@ qv = v * c
 btc = c[0].clone()
 ts = (1_700_000_000_000 + 900_000 * torch.arange(T, device=c.device, dtype=torch.int64)).expand(S, T).contiguous()
 agg = {"open": "first", "high": "max", "low": "min", "close": "last", "volume": "sum"}
+_flat = {}
+
+
+def flat_out():
+    if not _flat:
+        _flat.update({k: torch.empty((S, T), dtype=torch.float64, device=c.device) for k in engine.ENRICH_COLUMNS})
+    return _flat
+
+
 calls = {
-    "enrich": lambda: engine.enrich(o, h, l, c, v),
+    "enrich": lambda: engine.enrich(o, h, l, c, v),   # the default outputs: padded pitch on large panels
+    "enrich_flat": lambda: engine.enrich(o, h, l, c, v, out=flat_out()),   # contiguous [S, T] outputs
     "context": lambda: engine.context_partials(h, l, c, max_bars=400),
     "a9_resample_1h": lambda: engine.resample(ts, {"open": o, "high": h, "low": l, "close": c, "volume": v}, agg,
                                               3_600_000),
@@ -47,7 +57,7 @@ calls = {
 }
 # input bytes read per candle; the algorithmic bytes add every returned output
 # at its dtype (bench.py output_bytes)
-IN = {"enrich": 40, "context": 24, "a9_resample_1h": 48, "a11_beta_corr": 8, "a13_market_features": 24,
+IN = {"enrich": 40, "enrich_flat": 40, "context": 24, "a9_resample_1h": 48, "a11_beta_corr": 8, "a13_market_features": 24,
       "a17_activity_burst": 48, "a18_pump_score": 32, "a19_failed_spike": 48, "a20_wilder_rsi": 8, "a20_adx": 24,
       "a20_zscore": 8, "a20_leadership": 16, "supertrend": 24, "f4_btc_join_returns": 16}
 
