@@ -192,17 +192,20 @@ def _row_stride(x: torch.Tensor) -> int:
     return int(x.stride(0)) if x.shape[0] > 1 else int(x.shape[1])
 
 
-ENRICH_ROW_PAD = 64   # doubles added to each output row's pitch by enrich_outputs
+ENRICH_ROW_PAD = 192   # doubles added to each output row's pitch by enrich_outputs (tools/shard_pitch.py)
 
 
 def enrich_outputs(S: int, T: int, device, columns=ENRICH_COLUMNS) -> dict[str, torch.Tensor]:
     """Output columns for enrich(..., out=...) laid out for HBM: [S, T] views
-    into [S, T + 64] buffers when the panel is large. With a row pitch of
-    exactly T doubles (80 000 B at T = 10 000) the concurrently resident
-    workgroups' output streams meet the same HBM channels: the C4 shard
-    (12 500 x 10 000) ran at 0.666 of 8 TB/s, at 0.711 with the 512-B pad
-    (tools/shard_pitch.py). Small panels get plain [S, T] tensors.
-    enrich() allocates its own outputs this way too."""
+    into [S, T + ENRICH_ROW_PAD] buffers when the panel is large. With a row
+    pitch of exactly T doubles (80 000 B at T = 10 000) the concurrently
+    resident workgroups' output streams meet the same HBM channels: the C4
+    shard (12 500 x 10 000) ran at 0.666 of 8 TB/s, at 0.711 with a 512-B pad
+    (round 5). Round 6 swept the pad on two boxes (profiles/r6d_pitch.txt,
+    r6e_pitch.txt): +512 B 0.709 / 0.626, +768 B 0.719 / 0.692, +1 536 B
+    0.713 / 0.702 at the shard, the 100k headline indifferent — 192 doubles.
+    Small panels get plain [S, T] tensors. enrich() allocates its own outputs
+    this way too."""
     pad = ENRICH_ROW_PAD if S >= 1024 and T >= 1024 else 0
     return {k: torch.empty((S, T + pad), dtype=torch.float64, device=device)[:, :T] for k in columns}
 
