@@ -220,6 +220,7 @@ SIGNATURES: dict[str, tuple] = {
     "bq_burst_features": (ctypes.c_int, [_PP, _I64, _I64, _I64, _P, _PP, _PP, _P, _I64, _P]),
     "bq_burst_qualify": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _I64, _I32, _P, _P]),
     "bq_spike_base": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _I32, _PP, _PP, _I64, _P]),
+    "bq_spike_base_std": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, _I32, _PP, _PP, _PP, _I64, _P]),
     "bq_spike_flags": (ctypes.c_int, [_PP, _P, _P, _I64, _I64, _I64, _P, _PP, _PP, _I64, _P]),
     "bq_supertrend": (ctypes.c_int, [_PP, _I64, _I64, _I64, ctypes.c_double, _P, _P, _P, _I64, _P]),
     "bq_supertrend_hlc": (ctypes.c_int, [_PP, _I64, _I64, _I64, _I32, ctypes.c_double, _P, _P, _P, _I64, _P]),

@@ -205,6 +205,149 @@ __device__ __forceinline__ double sp_count(int t, int w, F f) {
   return (double)c;
 }
 
+// x.rolling(w).std() (ddof 1, min_periods = w) at a lane's SP_K consecutive
+// candles from the ring values f(p): sums of d = x - r about a reference r
+// inside every one of the lane's windows (the value at the lane's first
+// candle), shared like sp_window4 (one core over the W - 3 common positions,
+// lead / trail extras per candle): var = (S2 - S1^2 / n) / (n - 1). With r in
+// the window, |mean - r| is at most the window's range, so the cancellation
+// costs O(n eps) relative — the window's variance to rounding, where pandas'
+// online add / remove recurrence over the whole row (roll_var) drifts when the
+// std is small against the values (~1e-8 relative at std / mean ~ 2e-5): the
+// panel result is then the one closer to the exactly computed value
+// (tests/test_spike_std_gpu.py). pandas' rules: a missing value in the window
+// -> NaN (min_periods = w); n <= 1 -> NaN; every observed value equal -> 0.
+struct SpVar {
+  double s1, s2, mn, mx;
+  int n;
+  __device__ __forceinline__ void init() {
+    s1 = s2 = 0.0;
+    mn = __builtin_inf();
+    mx = -__builtin_inf();
+    n = 0;
+  }
+  __device__ __forceinline__ void add(double v, double r) {
+    const bool ok = win_ok(v);
+    const double d = ok ? v - r : 0.0;
+    s1 += d;
+    s2 = fma(d, d, s2);
+    n += ok;
+    mn = ok ? fmin(mn, v) : mn;
+    mx = ok ? fmax(mx, v) : mx;
+  }
+  __device__ __forceinline__ SpVar then(const SpVar& b) const {
+    SpVar x;
+    x.s1 = s1 + b.s1;
+    x.s2 = s2 + b.s2;
+    x.mn = fmin(mn, b.mn);
+    x.mx = fmax(mx, b.mx);
+    x.n = n + b.n;
+    return x;
+  }
+};
+
+template <typename F>
+__device__ __forceinline__ void sp_std4(int tb, int pb, int w, F f, double (&r)[SP_K]) {
+  const double ref = f(pb);
+  auto fin = [&](const SpVar& a, int t) -> double {
+    if (t < w - 1 || w <= 1 || a.n < w) return qnan();
+    if (a.mn == a.mx) return 0.0;
+    const double var = (a.s2 - a.s1 * (a.s1 / (double)a.n)) / (double)(a.n - 1);
+    return sqrt(var > 0.0 ? var : 0.0);
+  };
+  if (w < SP_K) {   // windows shorter than the lane: each about its own newest value
+#pragma unroll
+    for (int k = 0; k < SP_K; ++k) {
+      SpVar a;
+      a.init();
+      const double rk = f(pb + k);
+      for (int p = pb + k - w + 1; p <= pb + k; ++p) a.add(f(p), rk);
+      r[k] = fin(a, tb + k);
+    }
+    return;
+  }
+  SpVar core;
+  core.init();
+  for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p), ref);
+  SpVar lead[SP_K], trail;
+  trail.init();
+  lead[SP_K - 1].init();
+#pragma unroll
+  for (int k = SP_K - 2; k >= 0; --k) {
+    SpVar one;
+    one.init();
+    one.add(f(pb + k + 1 - w), ref);
+    lead[k] = one.then(lead[k + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < SP_K; ++k) {
+    if (k > 0) trail.add(f(pb + k), ref);
+    r[k] = fin(lead[k].then(core).then(trail), tb + k);
+  }
+}
+
+// sp_window4<true> and sp_std4 over the same window in ONE walk of the ring:
+// the mean's aggregate (SpAgg: sum, count, min / max, signs) and the std's
+// reference-shifted sums advance together (the count and min / max serve
+// both). Same values as the two separate calls.
+struct SpAggV {
+  SpAgg a;
+  double s1, s2;
+  __device__ __forceinline__ void init() {
+    a.init();
+    s1 = s2 = 0.0;
+  }
+  __device__ __forceinline__ void add(double v, double r) {
+    a.add(v);
+    const double d = win_ok(v) ? v - r : 0.0;
+    s1 += d;
+    s2 = fma(d, d, s2);
+  }
+  __device__ __forceinline__ SpAggV then(const SpAggV& b) const {
+    SpAggV x;
+    x.a = a.then(b.a);
+    x.s1 = s1 + b.s1;
+    x.s2 = s2 + b.s2;
+    return x;
+  }
+};
+
+template <typename F>
+__device__ __forceinline__ void sp_mean_std4(int tb, int pb, int w, F f, double (&ma)[SP_K], double (&sd)[SP_K]) {
+  if (w < SP_K) {   // short windows: the separate forms (per-candle references)
+    sp_window4<true>(tb, pb, w, f, ma);
+    sp_std4(tb, pb, w, f, sd);
+    return;
+  }
+  const double ref = f(pb);
+  auto fin_sd = [&](const SpAggV& x, int t) -> double {
+    if (t < w - 1 || w <= 1 || x.a.n < w) return qnan();
+    if (x.a.mn == x.a.mx) return 0.0;
+    const double var = (x.s2 - x.s1 * (x.s1 / (double)x.a.n)) / (double)(x.a.n - 1);
+    return sqrt(var > 0.0 ? var : 0.0);
+  };
+  SpAggV core;
+  core.init();
+  for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p), ref);
+  SpAggV lead[SP_K], trail;
+  trail.init();
+  lead[SP_K - 1].init();
+#pragma unroll
+  for (int k = SP_K - 2; k >= 0; --k) {
+    SpAggV one;
+    one.init();
+    one.add(f(pb + k + 1 - w), ref);
+    lead[k] = one.then(lead[k + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < SP_K; ++k) {
+    if (k > 0) trail.add(f(pb + k), ref);
+    const SpAggV x = lead[k].then(core).then(trail);
+    ma[k] = sp_finish<true>(x.a, tb + k, w);
+    sd[k] = fin_sd(x, tb + k);
+  }
+}
+
 // ---- pass 1: base features ------------------------------------------------------------
 enum { SB_O = 0, SB_H, SB_L, SB_C, SB_V, SB_Q, SB_CF, SB_PSTD, SB_VSTD, SB_S8, SB_S20, SB_BSD, SB_NIN };
 
@@ -212,13 +355,21 @@ struct SpikeBaseArgs {
   const double* in[SB_NIN];
   double* out[BQ_NUM_SPIKE_BASE_F];
   uint8_t* flag[BQ_NUM_SPIKE_BASE_B];
+  double* sd[BQ_NUM_SPIKE_STD];   // TP: the std columns the kernel forms (NULL = not written)
   int64_t S, ld_in, ld_out;
   int T, w, n, pad;
 };
 
 // 3 workgroups per CU (168 VGPRs, 12 B of spill) instead of 2 at 178 VGPRs:
 // a19 4.10 -> 3.99 ms (A/B, same box)
-__global__ __launch_bounds__(SP_NT, 3) void spike_base_kernel(const SpikeBaseArgs A, int vin, int vout, int vb) {
+// TP: the five std columns formed here (sp_std over the rings, written to
+// A.sd) instead of read from the replay's columns (A.in[SB_PSTD ..])
+#ifndef BQ_SP_TP_WGS
+#define BQ_SP_TP_WGS 3   // workgroups per CU of the TP instantiation
+#endif
+template <bool TP>
+__global__ __launch_bounds__(SP_NT, TP ? BQ_SP_TP_WGS : 3) void spike_base_kernel(const SpikeBaseArgs A, int vin, int vout,
+                                                                                int vb) {
   // rings: close, ffilled close, volume, quote volume, body size pct, pct
   // change (formed once per candle, read by every window), candle colour
   __shared__ double sC[SP_R], sF[SP_R], sV[SP_R], sQ[SP_R], sB[SP_R], sP[SP_R];
@@ -307,19 +458,39 @@ __global__ __launch_bounds__(SP_NT, 3) void spike_base_kernel(const SpikeBaseArg
     put(BQ_SPIKE_CLOSE_OPEN_RATIO, r);
     // price: mean over the base window, z-score against the replayed std
     double ma[SP_K], sd[SP_K];
-    sp_window4<true>(tb, pb, W, [&](int p) { return sC[sp_slot(p)]; }, ma);
+    // the std columns (TP): formed from the rings, written once
+    auto std4 = [&](int wc, int slot_col, auto fr, double (&x)[SP_K]) {
+      sp_std4(tb, pb, wc, fr, x);
+      if (A.sd[slot_col]) store_lines<SP_K>(A.sd[slot_col] + orow, tb, T, vo, x, whole);
+    };
+    auto c_at = [&](int p) { return sC[sp_slot(p)]; };
+    auto v_at = [&](int p) { return sV[sp_slot(p)]; };
+    auto put_sd = [&](int col, const double (&x)[SP_K]) {
+      if (A.sd[col]) store_lines<SP_K>(A.sd[col] + orow, tb, T, vo, x, whole);
+    };
+    if constexpr (TP) {
+      sp_mean_std4(tb, pb, W, c_at, ma, sd);
+      put_sd(BQ_SPIKE_STD_PRICE, sd);
+    } else {
+      sp_window4<true>(tb, pb, W, c_at, ma);
+      sp_load(A.in[SB_PSTD] + irow, tb, T, vin, sd);
+    }
     put(BQ_SPIKE_PRICE_MA, ma);
-    sp_load(A.in[SB_PSTD] + irow, tb, T, vin, sd);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = (c[k] - ma[k]) / (sd[k] + SP_EPS);
     put(BQ_SPIKE_PRICE_ZSCORE, r);
     // volume
-    sp_window4<true>(tb, pb, W, [&](int p) { return sV[sp_slot(p)]; }, ma);
+    if constexpr (TP) {
+      sp_mean_std4(tb, pb, W, v_at, ma, sd);
+      put_sd(BQ_SPIKE_STD_VOLUME, sd);
+    } else {
+      sp_window4<true>(tb, pb, W, v_at, ma);
+    }
     put(BQ_SPIKE_VOLUME_MA, ma);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = v[k] / (ma[k] + SP_EPS);
     put(BQ_SPIKE_VOLUME_RATIO, r);
-    sp_load(A.in[SB_VSTD] + irow, tb, T, vin, sd);
+    if constexpr (!TP) sp_load(A.in[SB_VSTD] + irow, tb, T, vin, sd);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = (v[k] - ma[k]) / (sd[k] + SP_EPS);
     put(BQ_SPIKE_VOLUME_ZSCORE, r);
@@ -345,8 +516,13 @@ __global__ __launch_bounds__(SP_NT, 3) void spike_base_kernel(const SpikeBaseArg
     // the 8 / 20-bar std ratio and the compression flag
     {
       double s8[SP_K], s20[SP_K];
-      sp_load(A.in[SB_S8] + irow, tb, T, vin, s8);
-      sp_load(A.in[SB_S20] + irow, tb, T, vin, s20);
+      if constexpr (TP) {
+        std4(8, BQ_SPIKE_STD_8, c_at, s8);
+        std4(20, BQ_SPIKE_STD_20, c_at, s20);
+      } else {
+        sp_load(A.in[SB_S8] + irow, tb, T, vin, s8);
+        sp_load(A.in[SB_S20] + irow, tb, T, vin, s20);
+      }
 #pragma unroll
       for (int k = 0; k < SP_K; ++k) {
         r[k] = s8[k] / (s20[k] + SP_EPS);
@@ -368,9 +544,14 @@ __global__ __launch_bounds__(SP_NT, 3) void spike_base_kernel(const SpikeBaseArg
     sp_window4<false>(tb, pb, 5, [&](int p) { return fabs(pc_at(p)); }, r);
     put(BQ_SPIKE_PC_ABS_SUM_5, r);
     // body size: 10-bar mean, z-score against the replayed std
-    sp_window4<true>(tb, pb, 10, [&](int p) { return bsp_at(p); }, ma);
+    if constexpr (TP) {
+      sp_mean_std4(tb, pb, 10, bsp_at, ma, sd);
+      put_sd(BQ_SPIKE_STD_BODY_PCT_10, sd);
+    } else {
+      sp_window4<true>(tb, pb, 10, bsp_at, ma);
+    }
     put(BQ_SPIKE_BODY_SIZE_PCT_MA_10, ma);
-    sp_load(A.in[SB_BSD] + irow, tb, T, vin, sd);
+    if constexpr (!TP) sp_load(A.in[SB_BSD] + irow, tb, T, vin, sd);
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) r[k] = (bsp[k] - ma[k]) / (sd[k] + SP_EPS);
     put(BQ_SPIKE_BODY_SIZE_PCT_Z, r);
@@ -603,19 +784,22 @@ namespace {
 bool sp_aligned(const void* p, unsigned a) { return (((uintptr_t)p) & (a - 1)) == 0; }
 }
 
-extern "C" int bq_spike_base(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
-                             int32_t streak_length, double* const* out_f, uint8_t* const* out_b, int64_t ld_out,
-                             void* stream) {
+static int spike_base_launch(const double* const* in, int nin, int64_t S, int64_t T, int64_t ld_in,
+                             int32_t base_window, int32_t streak_length, double* const* out_f, uint8_t* const* out_b,
+                             double* const* out_sd, int64_t ld_out, void* stream) {
   using namespace bq;
   if (!in || !out_f || !out_b || S < 0 || T < 0 || ld_in < T || ld_out < T || T > 0x7fffffff - SP_TT ||
       S > 0x7fffffff || base_window < 1 || base_window > SP_H - 2 || streak_length < 1 || streak_length > SP_H - 2)
     return BQ_EINVAL;
   SpikeBaseArgs A;
   memset(&A, 0, sizeof(A));
-  for (int f = 0; f < SB_NIN; ++f) {
+  for (int f = 0; f < nin; ++f) {
     if (!in[f]) return BQ_EINVAL;
     A.in[f] = in[f];
   }
+  const bool tp = out_sd != nullptr;
+  if (tp)
+    for (int c = 0; c < BQ_NUM_SPIKE_STD; ++c) A.sd[c] = out_sd[c];
   for (int c = 0; c < BQ_NUM_SPIKE_BASE_F; ++c) A.out[c] = out_f[c];
   for (int c = 0; c < BQ_NUM_SPIKE_BASE_B; ++c) A.flag[c] = out_b[c];
   if (S == 0 || T == 0) return BQ_OK;
@@ -626,13 +810,35 @@ extern "C" int bq_spike_base(const double* const* in, int64_t S, int64_t T, int6
   A.w = base_window;
   A.n = streak_length;
   int vin = (ld_in % 2) == 0, vout = (ld_out % 2) == 0, vb = (ld_out % 4) == 0;
-  for (int f = 0; f < SB_NIN; ++f) vin &= sp_aligned(in[f], 16);
+  for (int f = 0; f < nin; ++f) vin &= sp_aligned(in[f], 16);
   for (int c = 0; c < BQ_NUM_SPIKE_BASE_F; ++c)
     if (out_f[c]) vout &= sp_aligned(out_f[c], 16);
+  for (int c = 0; c < BQ_NUM_SPIKE_STD; ++c)
+    if (A.sd[c]) vout &= sp_aligned(A.sd[c], 16);
   for (int c = 0; c < BQ_NUM_SPIKE_BASE_B; ++c)
     if (out_b[c]) vb &= sp_aligned(out_b[c], 4);
-  hipLaunchKernelGGL(spike_base_kernel, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout, vb);
+  if (tp)
+    hipLaunchKernelGGL(spike_base_kernel<true>, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout,
+                       vb);
+  else
+    hipLaunchKernelGGL(spike_base_kernel<false>, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout,
+                       vb);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
+}
+
+extern "C" int bq_spike_base(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
+                             int32_t streak_length, double* const* out_f, uint8_t* const* out_b, int64_t ld_out,
+                             void* stream) {
+  return spike_base_launch(in, bq::SB_NIN, S, T, ld_in, base_window, streak_length, out_f, out_b, nullptr, ld_out,
+                           stream);
+}
+
+extern "C" int bq_spike_base_std(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
+                                 int32_t streak_length, double* const* out_f, uint8_t* const* out_b,
+                                 double* const* out_sd, int64_t ld_out, void* stream) {
+  if (!out_sd) return BQ_EINVAL;
+  return spike_base_launch(in, bq::SB_PSTD, S, T, ld_in, base_window, streak_length, out_f, out_b, out_sd, ld_out,
+                           stream);
 }
 
 extern "C" int bq_spike_flags(const double* const* in, const double* vcmr, const double* pbbt, int64_t S, int64_t T,

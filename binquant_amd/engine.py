@@ -545,6 +545,41 @@ def spike_base(o, h, l, c, v, qv, close_ffill, price_std, volume_std, std8, std2
     return out
 
 
+# bq_spike_base_std's std columns (enum bq_spike_std_col), under their
+# FailedSpikeFade.detect names
+SPIKE_STD = ("price_std", "volume_std", "rolling_price_std_8", "rolling_price_std_20", "body_size_pct_std_10")
+
+
+@device_entry
+def spike_base_std(o, h, l, c, v, qv, close_ffill, base_window: int = 12, streak_length: int = 3,
+                   body_size_pct: torch.Tensor | None = None,
+                   stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
+    """spike_base in panel mode (bq_spike_base_std): the five rolling std
+    columns (failed_spike_fade.py:293-339) formed in the same pass as two-pass
+    window sums — the window's variance to rounding, where pandas' online
+    recurrence (and its bit-exact replay, spike_base's inputs) drifts — and
+    returned beside the base columns under their detect() names."""
+    c = _check_panel(c, "c")
+    S, T = c.shape
+    ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip(
+        (o, h, l, c, v, qv, close_ffill), ("o", "h", "l", "c", "v", "qv", "close_ffill"))]
+    out = _cols(S, T, c.device, SPIKE_BASE_FLOAT, torch.float64,
+                {"body_size_pct": body_size_pct} if body_size_pct is not None else None)
+    flags = _cols(S, T, c.device, SPIKE_BASE_BOOL, torch.bool)
+    sd = _cols(S, T, c.device, SPIKE_STD, torch.float64)
+    st = _lib.load().bq_spike_base_std(
+        _lib.ptr_array([t.data_ptr() for t in ins]), S, T, T, int(base_window), int(streak_length),
+        _lib.ptr_array([0 if (n == "body_size_pct" and body_size_pct is not None) else out[n].data_ptr()
+                        for n in SPIKE_BASE_FLOAT]),
+        _lib.ptr_array([flags[n].data_ptr() for n in SPIKE_BASE_BOOL]),
+        _lib.ptr_array([sd[n].data_ptr() for n in SPIKE_STD]), T, _stream_handle(stream),
+    )
+    _lib.check(st, "bq_spike_base_std")
+    out.update(flags)
+    out.update(sd)
+    return out
+
+
 _SPIKE_MODES = {"last": 0, "first": 1, "all": 2}
 
 

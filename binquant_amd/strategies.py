@@ -21,6 +21,8 @@ the reference's name; booleans are returned as torch.bool.
 
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
@@ -176,10 +178,16 @@ def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Te
     eps = 1e-6
     w, n = p.base_window, p.streak_length
     O, C = F.inp(o), F.inp(c)
-    bsp = F.run({"bsp": (C - O).abs() / (O + eps)})["bsp"]
-    cf, price_std, volume_std, s8, s20, bsp_sd = engine.rolling_many(
-        FF(c), R(c, w, "std"), R(v, w, "std"), R(c, 8, "std"), R(c, 20, "std"), R(bsp, 10, "std"))
-    b = engine.spike_base(o, h, l, c, v, qv, cf, price_std, volume_std, s8, s20, bsp_sd, w, n, body_size_pct=bsp)
+    if _SPIKE_STD_IN_PASS:   # the five std columns formed in the base pass (reference-shifted window sums)
+        (cf,) = engine.rolling_many(FF(c))
+        b = engine.spike_base_std(o, h, l, c, v, qv, cf, w, n)   # body_size_pct formed in the pass too
+        price_std, volume_std, s8, s20, bsp_sd = (b[k] for k in engine.SPIKE_STD)
+    else:                    # the five std columns as the bit-exact replays of pandas' online variance
+        bsp = F.run({"bsp": (C - O).abs() / (O + eps)})["bsp"]
+        cf, price_std, volume_std, s8, s20, bsp_sd = engine.rolling_many(
+            FF(c), R(c, w, "std"), R(v, w, "std"), R(c, 8, "std"), R(c, 20, "std"), R(bsp, 10, "std"))
+        b = engine.spike_base(o, h, l, c, v, qv, cf, price_std, volume_std, s8, s20, bsp_sd, w, n,
+                              body_size_pct=bsp)
     pca = b["price_change_abs"]
     (dyn,) = engine.rolling_many(R(pca, 60, "quantile", q=p.price_break_dynamic_q, min_periods=20), exact=False)
     vr = b["volume_ratio"]
@@ -239,6 +247,11 @@ def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Te
 # failed_spike_features (panel mode) through bq_spike_base / bq_spike_flags
 # (False: the staged pipeline; tests compare the two)
 _SPIKE_FUSED = True
+# the fused spike path forms its five rolling std columns inside the base pass
+# (bq_spike_base_std: two-pass window sums, panel mode) instead of replaying
+# pandas' online variance (bq_rolling_batch) ahead of it. exact=True and the
+# staged pipeline keep the replays; tests compare the two within pandas' drift.
+_SPIKE_STD_IN_PASS = os.environ.get("BQ_SPIKE_STD_IN_PASS", "1") != "0"
 
 # panel mode of pump_score_features through bq_pump_features (False: the staged
 # panel pipeline; tests compare the two)

@@ -520,6 +520,23 @@ enum bq_spike_flag_bcol {
 };
 int bq_spike_base(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
                   int32_t streak_length, double* const* out_f, uint8_t* const* out_b, int64_t ld_out, void* stream);
+/*
+ * bq_spike_base_std: the same pass in panel mode with the five rolling std
+ * columns (FailedSpikeFade.compute_base_features' price_std, volume_std,
+ * rolling_price_std_8 / _20 and compute_early_features' body_size_pct std 10,
+ * failed_spike_fade.py:293-339) formed in the pass — two-pass window sums
+ * (the window's variance to rounding) instead of the bit-exact replay of
+ * pandas' online recurrence. in = the first 7 inputs of bq_spike_base
+ * {open, high, low, close, volume, quote_volume, ffilled close}; out_sd
+ * [BQ_NUM_SPIKE_STD] fp64 [S][ld_out] (NULL entries = not written).
+ */
+enum bq_spike_std_col {
+  BQ_SPIKE_STD_PRICE = 0, BQ_SPIKE_STD_VOLUME, BQ_SPIKE_STD_8, BQ_SPIKE_STD_20, BQ_SPIKE_STD_BODY_PCT_10,
+  BQ_NUM_SPIKE_STD
+};
+int bq_spike_base_std(const double* const* in, int64_t S, int64_t T, int64_t ld_in, int32_t base_window,
+                      int32_t streak_length, double* const* out_f, uint8_t* const* out_b, double* const* out_sd,
+                      int64_t ld_out, void* stream);
 int bq_spike_flags(const double* const* in, const double* vcmr, const double* pbbt, int64_t S, int64_t T,
                    int64_t ld_in, const bq_spike_params* p, double* const* out_f, uint8_t* const* out_b,
                    int64_t ld_out, void* stream);

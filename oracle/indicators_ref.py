@@ -340,6 +340,23 @@ def exact_zscore(window_closes) -> float:
     return float(w[-1] - m) / sqrt(float(var))
 
 
+def exact_std(window, ddof: int = 1) -> float:
+    """x.rolling(w).std(ddof) of a full window in exact rational arithmetic
+    (mean and variance exact, one sqrt in float64). pandas' online roll_var
+    drifts from this where the std is small against the values; the spike
+    pass's two-pass std (bq_spike_base_std) is held to it there
+    (tests/util.assert_close_or_exact)."""
+    from fractions import Fraction
+    from math import sqrt
+
+    w = [Fraction(float(v)) for v in np.asarray(window, dtype=np.float64)]
+    if len(w) <= ddof:
+        return float("nan")
+    m = sum(w) / len(w)
+    var = sum((v - m) ** 2 for v in w) / (len(w) - ddof)
+    return sqrt(float(var))
+
+
 def gradual_gainer_leadership(open_time, close, btc_time, btc_close, q: float = 0.80, lookback: int = 96,
                               min_history: int = 100, min_count: int = 20, short: int = 8, long: int = 24):
     """GradualGainerRetest._leadership_allows (strategies/gradual_gainer_retest.py:131-196)

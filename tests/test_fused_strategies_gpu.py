@@ -104,13 +104,16 @@ def test_burst_fused_equals_staged(cuda, with_q):
 
 
 def test_spike_fused_equals_staged(cuda):
-    """bq_spike_base / bq_spike_flags against the staged failed-spike pipeline
-    (panel mode): the rolling std columns and everything computed from raw
-    values (geometry, pct changes, momentum, integer counts, streak flags)
-    equal bit for bit; the rolling means / sums (direct window sums here,
-    sliding in the staged panel kernel) and their dependants within 1e-12 of
-    each row's magnitude; flags equal away from near-ties of their
-    thresholds (a handful at most)."""
+    """bq_spike_base(_std) / bq_spike_flags against the staged failed-spike
+    pipeline (panel mode): everything computed from raw values (geometry, pct
+    changes, momentum, integer counts, streak flags) equal bit for bit; the
+    rolling means / sums (direct window sums here, sliding in the staged panel
+    kernel) and their dependants within 1e-12 of each row's magnitude; the five
+    std columns (formed in the base pass by default, the staged pipeline's
+    replays of pandas' online variance) and their descendants by
+    tests/spike_std.py's rule (1e-9, or closer to the exact window std where
+    pandas drifts); flags equal away from near-ties of their thresholds (a
+    handful at most)."""
     from binquant_amd import strategies
     from binquant_amd.synth import numpy_panel
 
@@ -135,29 +138,22 @@ def test_spike_fused_equals_staged(cuda):
     assert list(fused) == list(staged)
     exact = {"price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
              "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "is_bullish", "close_open_ratio",
-             "price_std", "momentum_3", "momentum_5", "close_to_high", "close_to_low", "rolling_price_std_8",
-             "rolling_price_std_20", "std_ratio_8_20", "pc_1", "pc_pos_count_5", "body_size_pct_std_10",
-             "vol_compression_flag", "upward", "downward", "early_spike_proba", "early_proba_aug_flag"}
-    # z-scores: (x - mean) / (std + eps) cancels where x ~ its mean, so the
-    # means' rounding difference (~1e-16 of x) is amplified by |x| / std
-    from binquant_amd import engine
+             "momentum_3", "momentum_5", "close_to_high", "close_to_low", "pc_1", "pc_pos_count_5",
+             "upward", "downward", "early_spike_proba", "early_proba_aug_flag"}
+    from tests import spike_std
 
-    vstd = engine.rolling(d["volume"], 12, "std").cpu().numpy()
-    zbase = {"price_zscore": (staged["price_std"].cpu().numpy(), p["close"]), "volume_zscore": (vstd, p["volume"]),
-             "body_size_pct_z": (staged["body_size_pct_std_10"].cpu().numpy(), staged["body_size_pct"].cpu().numpy())}
+    fn_, sn_ = ({k: v.cpu().numpy() for k, v in m.items()} for m in (fused, staged))
+    spike_std.check(fn_, sn_, {"close": p["close"], "volume": p["volume"], "body_size_pct": sn_["body_size_pct"]})
+    if not strategies._SPIKE_STD_IN_PASS:   # the replays on both sides: bit for bit
+        exact |= set(spike_std.STD_COLS) | {"std_ratio_8_20", "vol_compression_flag"}
     flips = 0
     for k in staged:
         x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
         assert x.dtype == y.dtype and x.shape == y.shape, k
         if k in exact:
             np.testing.assert_array_equal(x, y, err_msg=k)
-        elif k in zbase:
-            sd, base = zbase[k]
-            np.testing.assert_array_equal(np.isnan(x), np.isnan(y), err_msg=k)
-            with np.errstate(all="ignore"):
-                lim = 1e-12 * np.abs(y) + 1e-13 * np.abs(base) / (sd + 1e-6)
-                ok = np.isnan(y) | (np.abs(x - y) <= lim)
-            assert ok.all(), (k, int((~ok).sum()))
+        elif k in spike_std.STD_COLS or k in spike_std.DESC:
+            continue   # checked by spike_std.check (1e-9, or explained by pandas' drift)
         elif y.dtype == bool:
             flips += int((x != y).sum())
         else:
@@ -211,15 +207,16 @@ def test_fused_odd_shapes_equal_staged(cuda, S, T):
         finally:
             setattr(strategies, flag, True)
         assert list(fused) == list(staged), name
-        if name == "spike":
-            vstd = engine.rolling(d["volume"], 12, "std").cpu().numpy()
-            zb = {"price_zscore": (staged["price_std"].cpu().numpy(), p["close"]),
-                  "volume_zscore": (vstd, p["volume"]),
-                  "body_size_pct_z": (staged["body_size_pct_std_10"].cpu().numpy(),
-                                      staged["body_size_pct"].cpu().numpy())}
+        if name == "spike":   # the std columns and their descendants: tests/spike_std.py's rule
+            from tests import spike_std
+
+            fn_, sn_ = ({k: v.cpu().numpy() for k, v in m.items()} for m in (fused, staged))
+            spike_std.check(fn_, sn_, {"close": p["close"], "volume": p["volume"], "body_size_pct": sn_["body_size_pct"]})
         for k in staged:
             x, y = fused[k].cpu().numpy(), staged[k].cpu().numpy()
             assert x.dtype == y.dtype and x.shape == y.shape, (name, k)
+            if name == "spike" and (k in spike_std.STD_COLS or k in spike_std.DESC):
+                continue   # spike_std.check (1e-9, or explained by pandas' drift)
             if y.dtype == bool or name == "burst":
                 np.testing.assert_array_equal(x, y, err_msg=f"{name}.{k}")
                 continue
@@ -232,9 +229,6 @@ def test_fused_odd_shapes_equal_staged(cuda, S, T):
                 lim = 1e-12 * np.abs(y) + 1e-13 * (sc[:, None] if y.ndim == 2 else sc)
                 if name == "pump" and k == "trend_score":   # the emas' rounding relative to 1 (cancellation)
                     lim = lim + 1e-13
-                if name == "spike" and k in zb:   # the cancellation bound of test_spike_fused_equals_staged
-                    sd, base = zb[k]
-                    lim = lim + 1e-13 * np.abs(base) / (sd + 1e-6)
                 ok = np.isnan(y) | (x == y) | (np.abs(x - y) <= lim)   # x == y: equal infinities (v / 0)
             assert ok.all(), (name, k, int((~ok).sum()))
 

@@ -259,11 +259,12 @@ def test_plan_cache_hits_are_bit_exact(cuda):
     from binquant_amd import signals, strategies
     from binquant_amd.synth import device_panel
 
-    # (the staged burst and pump pipelines: their fused paths, bq_burst_features
-    # and bq_pump_features + bq_rolling_quantile_cross, run no JIT programs)
+    # (the staged burst, pump and spike pipelines: their fused paths,
+    # bq_burst_features, bq_pump_features + bq_rolling_quantile_cross and
+    # bq_spike_base_std + bq_spike_flags, run no JIT programs)
     calls = {
         "burst": lambda o, h, l, c, v: _staged_burst(strategies, o, h, l, c, v),
-        "spike": lambda o, h, l, c, v: strategies.failed_spike_features(o, h, l, c, v, v * c),
+        "spike": lambda o, h, l, c, v: _staged_spike(strategies, o, h, l, c, v),
         "pump": lambda o, h, l, c, v: _staged_pump(strategies, o, h, l, c, v),
         "gainer": lambda o, h, l, c, v: signals.top_gainer_features(o, h, l, c, v, v * c),
     }
@@ -283,6 +284,14 @@ def test_plan_cache_hits_are_bit_exact(cuda):
         finally:
             F._PLAN_CACHE_ON = True
         _assert_same_tree(hot, cold, name)
+
+
+def _staged_spike(strategies, o, h, l, c, v):
+    strategies._SPIKE_FUSED = False
+    try:
+        return strategies.failed_spike_features(o, h, l, c, v, v * c)
+    finally:
+        strategies._SPIKE_FUSED = True
 
 
 def _staged_burst(strategies, o, h, l, c, v):
