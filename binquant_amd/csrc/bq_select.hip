@@ -218,10 +218,20 @@ __global__ __launch_bounds__(SQ_NT) void row_quantile_kernel(const double* __res
 
 // Rows of up to 64 * RQ_KW values: one WAVE per row (4 rows per workgroup),
 // the same radix select with the row's keys in the wave's registers (RQ_KW
-// per lane) and a 256-bin histogram per wave in LDS — no workgroup barrier:
-// the block kernel's passes were ~4 barriers each over 4 waves of one row.
+// per lane) and the 256-bin histogram in LDS — no workgroup barrier: the
+// block kernel's passes were ~4 barriers each over 4 waves of one row.
+// The top digits of real rows fall in a handful of bins (sign + exponent: a
+// row of ratios around 1.0 puts every key in 2 bins), and same-address LDS
+// atomics of one instruction serialise (r6k PMC: 80 % of the kernel's LDS
+// cycles were bank-conflict cycles), so each wave keeps RQ_NCOPY copies of
+// the bins, lane l adding into copy l % RQ_NCOPY; the copies sit RQ_CSTRIDE
+// dwords apart (8 banks of skew), and the owner lane of a bin sums them.
+// NaN maps to the all-ones key: above every number (order_key never yields
+// it), so it is never the k-th (k < n) and needs no test in the passes.
 constexpr int RQ_KW = 32;
 constexpr int RQ_WPB = 4;
+constexpr int RQ_NCOPY = 8;
+constexpr int RQ_CSTRIDE = 256 + 8;
 
 // inclusive wave scan of an unsigned (DPP rows + row carries)
 __device__ __forceinline__ unsigned wave_scan_add_u32(unsigned v, int lane) {
@@ -236,21 +246,21 @@ __device__ __forceinline__ unsigned wave_scan_add_u32(unsigned v, int lane) {
 __global__ __launch_bounds__(RQ_WPB * WAVE) void row_quantile_wave_kernel(const double* __restrict__ x, int64_t S,
                                                                             int T, int64_t ld_in, double q,
                                                                             double* __restrict__ out) {
-  __shared__ unsigned hist_all[RQ_WPB][256];
+  __shared__ __attribute__((aligned(16))) unsigned hist_all[RQ_WPB][RQ_NCOPY * RQ_CSTRIDE];
   const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
   const int64_t row = (int64_t)blockIdx.x * RQ_WPB + wv;
   if (row >= S) return;   // whole wave; no workgroup barrier below
   unsigned* hist = hist_all[wv];
+  unsigned* mine = hist + (lane & (RQ_NCOPY - 1)) * RQ_CSTRIDE;
   const double* __restrict__ r = x + row * ld_in;
-  // keys (0 marks NaN / padding, as in row_quantile_kernel); lane-contiguous
-  // pairs of values: 16-byte loads
+  // lane-contiguous pairs of values: 16-byte loads
   uint64_t kr[RQ_KW];
   int cnt = 0;
 #pragma unroll
   for (int i = 0; i < RQ_KW; ++i) {
     const int t = (i >> 1) * (2 * WAVE) + 2 * lane + (i & 1);
     const double v = t < T ? r[t] : qnan();
-    kr[i] = v == v ? order_key(v) : 0ull;
+    kr[i] = v == v ? order_key(v) : ~0ull;
     cnt += v == v;
   }
 #pragma unroll
@@ -269,22 +279,29 @@ __global__ __launch_bounds__(RQ_WPB * WAVE) void row_quantile_wave_kernel(const 
   int k = prev;
   for (int sh = 56; sh >= 0; sh -= 8) {
 #pragma unroll
-    for (int b = 0; b < 4; ++b) hist[4 * lane + b] = 0;
+    for (int c = 0; c < RQ_NCOPY; ++c)
+      *reinterpret_cast<uint4*>(hist + c * RQ_CSTRIDE + 4 * lane) = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < RQ_KW; ++i) {
       const uint64_t key = kr[i];
-      if (key && (key & mask) == prefix) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+      if ((key & mask) == prefix) atomicAdd(&mine[(unsigned)(key >> sh) & 255u], 1u);
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // lane l owns bins 4l .. 4l + 3: its 4 counts, then the wave's exclusive prefix
-    unsigned h[4], tot = 0;
+    // lane l owns bins 4l .. 4l + 3: its 4 counts over the copies, then the
+    // wave's exclusive prefix
+    unsigned h[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      h[b] = hist[4 * lane + b];
-      tot += h[b];
+    for (int c = 0; c < RQ_NCOPY; ++c) {
+      const uint4 w = *reinterpret_cast<const uint4*>(hist + c * RQ_CSTRIDE + 4 * lane);
+      h[0] += w.x;
+      h[1] += w.y;
+      h[2] += w.z;
+      h[3] += w.w;
     }
+    const unsigned tot = h[0] + h[1] + h[2] + h[3];
     const unsigned incl = wave_scan_add_u32(tot, lane);
     unsigned excl = incl - tot;
     int found = -1, fk = 0, fh = 0;
@@ -310,7 +327,7 @@ __global__ __launch_bounds__(RQ_WPB * WAVE) void row_quantile_wave_kernel(const 
 #pragma unroll
       for (int i = 0; i < RQ_KW; ++i) {
         const uint64_t key = kr[i];
-        if (key && (key & mask) == prefix) got = key;
+        if ((key & mask) == prefix) got = key;
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
@@ -320,19 +337,21 @@ __global__ __launch_bounds__(RQ_WPB * WAVE) void row_quantile_wave_kernel(const 
       prefix = got;
       break;
     }
+    // the next pass clears the bins other lanes are still reading
+    __builtin_amdgcn_wave_barrier();
   }
   const double a = key_value(prefix);
   double b = a;
   if (next != prev) {
+    // NaN keys (all ones) are above a and never the minimum above it while a
+    // number is; with none above, le == n > next
     int le = 0;
     uint64_t above = ~0ull;
 #pragma unroll
     for (int i = 0; i < RQ_KW; ++i) {
       const uint64_t key = kr[i];
-      if (key) {
-        le += key <= prefix;
-        if (key > prefix && key < above) above = key;
-      }
+      le += key <= prefix;
+      if (key > prefix && key < above) above = key;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {

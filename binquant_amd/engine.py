@@ -585,11 +585,13 @@ _SPIKE_MODES = {"last": 0, "first": 1, "all": 2}
 
 @device_entry
 def spike_flags(o, c, close_ffill, volume_ratio, dyn_threshold, vcmr, pbbt, params,
-                stream: torch.cuda.Stream | None = None) -> dict[str, torch.Tensor]:
+                stream: torch.cuda.Stream | None = None, labels: torch.Tensor | None = None) -> dict[str, torch.Tensor]:
     """FailedSpikeFade's flag columns and preliminary labels
     (strategies/failed_spike_fade.py:360-488) in one pass per row
     (bq_spike_flags): vcmr / pbbt [S] the calibrated thresholds, dyn_threshold
-    the |pct change| rolling quantile."""
+    the |pct change| rolling quantile. labels: an optional bool [2, S, T]
+    that receives label_pre / label_short_pre (so one cooldown launch can
+    take both as [2S, T] rows)."""
     c = _check_panel(c, "c")
     S, T = c.shape
     ins = [_check_panel(t, n, (S, T)).contiguous() for t, n in zip(
@@ -603,7 +605,13 @@ def spike_flags(o, c, close_ffill, volume_ratio, dyn_threshold, vcmr, pbbt, para
                             float(params.accel_volume_deriv_min), float(params.accel_price_change_min),
                             float(params.body_size_pct_min))
     out = _cols(S, T, c.device, SPIKE_FLAG_FLOAT, torch.float64)
-    flags = _cols(S, T, c.device, SPIKE_FLAG_BOOL, torch.bool)
+    given = None
+    if labels is not None:
+        if labels.shape != (2, S, T) or labels.dtype != torch.bool or not labels.is_contiguous() \
+                or labels.device != c.device:
+            raise ValueError("labels: expected a contiguous bool [2, S, T] tensor on the panel's device")
+        given = {"label_pre": labels[0], "label_short_pre": labels[1]}
+    flags = _cols(S, T, c.device, SPIKE_FLAG_BOOL, torch.bool, given)
     st = _lib.load().bq_spike_flags(
         _lib.ptr_array([t.data_ptr() for t in ins]), ctypes.c_void_p(vc.data_ptr()), ctypes.c_void_p(pb.data_ptr()),
         S, T, T, ctypes.byref(pr), _lib.ptr_array([out[n].data_ptr() for n in SPIKE_FLAG_FLOAT]),

@@ -170,11 +170,12 @@ def _activity_burst_fused(o, h, l, c, v, qv, p: BurstParams) -> dict[str, torch.
 _BURST_FUSED = True
 
 def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Tensor]:
-    """failed_spike_features (panel mode) through bq_spike_base / bq_spike_flags:
-    the ffill and the five rolling std columns (the bit-exact Welford replays)
-    in ONE bq_rolling_batch call, the base / early features in one pass, the
+    """failed_spike_features (panel mode) through bq_spike_base(_std) /
+    bq_spike_flags: the close ffill, the base / early features and the five
+    rolling std columns in one pass (BQ_SPIKE_STD_IN_PASS=0: the stds as the
+    bit-exact replays of pandas' online variance, batched with the ffill), the
     |pct change| quantile and the whole-series calibration, the flags and
-    labels in a second pass, then the cooldowns."""
+    labels in a second pass, then both cooldowns in one launch."""
     eps = 1e-6
     w, n = p.base_window, p.streak_length
     O, C = F.inp(o), F.inp(c)
@@ -200,7 +201,9 @@ def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Te
     new_base = torch.where(new_floor > base0, new_floor, torch.full_like(new_floor, base0))
     vcmr = torch.where(skip, torch.full_like(new_vol, p.volume_cluster_min_ratio), new_vol).contiguous()
     pbbt = torch.where(skip, torch.full_like(new_base, base0), new_base).contiguous()
-    f = engine.spike_flags(o, c, cf, vr, dyn, vcmr, pbbt, p)
+    S, T = c.shape
+    labels = torch.empty((2, S, T), dtype=torch.bool, device=c.device)   # label_pre / label_short_pre
+    f = engine.spike_flags(o, c, cf, vr, dyn, vcmr, pbbt, p, labels=labels)
     out: dict[str, torch.Tensor] = {}
     for key in ("price_change", "price_change_abs", "body_size", "body_size_pct", "upper_wick", "lower_wick",
                 "upper_wick_ratio", "lower_wick_ratio", "total_range", "range_pct", "is_bullish", "close_open_ratio"):
@@ -237,8 +240,10 @@ def _failed_spike_fused(o, h, l, c, v, qv, p: SpikeParams) -> dict[str, torch.Te
         out["label"], out["suppressed_label"] = label_pre_t.clone(), torch.zeros_like(label_pre_t)
         out["label_short"], out["suppressed_label_short"] = label_short_t.clone(), torch.zeros_like(label_pre_t)
     else:
-        out["label"], out["suppressed_label"] = engine.cooldown(label_pre_t, p.post_spike_cooldown_bars)
-        out["label_short"], out["suppressed_label_short"] = engine.cooldown(label_short_t, p.post_spike_cooldown_bars)
+        kept, sup = engine.cooldown(labels.view(2 * S, T), p.post_spike_cooldown_bars)   # both in one launch
+        kept, sup = kept.view(2, S, T), sup.view(2, S, T)
+        out["label"], out["suppressed_label"] = kept[0], sup[0]
+        out["label_short"], out["suppressed_label_short"] = kept[1], sup[1]
     out["upward"] = b["upward"]
     out["downward"] = b["downward"]
     return out

@@ -132,12 +132,20 @@ def test_row_quantile_is_numpy_bitwise(cuda, T):
     x[7, :] = 7.0                                 # constant
     x[8, :11] = np.nan                            # leading NaNs (rolling warm-up)
     x[9] = -x[9]
+    zeros = np.abs(rng.normal(0, 1e-3, (2, T)))                   # |pct change|: halted candles' exact zeros
+    zeros[0, rng.random(T) < 0.4] = 0.0
+    zeros[1, rng.random(T) < 0.2] = -0.0
+    infs = rng.lognormal(0, 1, (1, T))
+    infs[0, rng.random(T) < 0.05] = np.inf
+    infs[0, rng.random(T) < 0.05] = -np.inf
+    x = np.vstack([x, zeros, infs])
     xt = torch.from_numpy(x).cuda()
     for q in (0.0, 0.25, 0.5, 0.75, 0.85, 0.97, 1.0, 0.333):
         got = engine.row_quantile(xt, q).cpu().numpy()
-        for s in range(10):
+        for s in range(x.shape[0]):
             v = x[s][~np.isnan(x[s])]
-            want = np.quantile(v, q) if v.size else np.nan
+            with np.errstate(invalid="ignore"):
+                want = np.quantile(v, q) if v.size else np.nan
             np.testing.assert_array_equal(got[s], want, err_msg=f"q={q} row {s}")
 
 
