@@ -72,95 +72,71 @@ __device__ __forceinline__ void sp_put_bytes(uint8_t* __restrict__ row, int tb, 
   }
 }
 
-// x.rolling(w).sum() / .mean() at candle t over values f(j), j = -w+1 .. 0
-// (time order), min_periods = w: pandas' NaN skip, same-value rule (every
-// observed value equal: the newest one, times nobs for a sum) and calc_mean's
-// sign rule. Branch-free (selects): the observed values' min / max decide
-// "all equal", sign-bit OR / AND decide "none / all negative".
-template <bool MEAN, typename F>
-__device__ __forceinline__ double sp_window(int t, int w, F f) {
-  if (t < w - 1) return qnan();
-  double s = 0.0, mn = __builtin_inf(), mx = -__builtin_inf(), last = qnan();
-  int n = 0;
-  unsigned sor = 0u, sand = 1u;
-  for (int j = -w + 1; j <= 0; ++j) {
-    const double v = f(j);
-    const bool ok = win_ok(v);   // NaN and +-inf are missing (pandas' window ops)
-    const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
-    s += ok ? v : 0.0;
-    n += ok;
-    sor |= ok ? sg : 0u;
-    sand &= ok ? sg : 1u;
-    mn = ok ? fmin(mn, v) : mn;
-    mx = ok ? fmax(mx, v) : mx;
-    last = ok ? v : last;
-  }
-  if (n < w || n <= 0) return qnan();
-  const bool same = mn == mx;
-  if (!MEAN) return same ? last * (double)n : s;
-  double r = s / (double)n;
-  if (same) r = last;
-  else if (sor == 0u && r < 0.0) r = 0.0;
-  else if (sand == 1u && r > 0.0) r = 0.0;
-  return r;
-}
-
-// The same statistic at a lane's SP_K consecutive candles tb .. tb + 3 (ring
-// positions pb .. pb + 3): their windows share the W - 3 positions
-// pb + 4 - W .. pb, aggregated once; each candle adds its own older (lead) and
-// newer (trail) extras — W + 3 values read instead of 4 W. The observed
-// count, min / max, sign OR / AND and the newest value combine exactly; the
-// sum is (lead + core) + trail instead of strictly time-ordered (rounding).
+// Every window of the two passes has min_periods = w: a window holding a
+// missing value (NaN / +-inf: pandas' window ops) is NaN whatever else it
+// holds. So the aggregates add raw values and count the observed ones only to
+// detect that, and pandas' rules apply to complete windows only, where they
+// reduce to sums: calc_mean's sign rule to the sign-bit count (its neg_ct,
+// signbit as pandas counts it) and the same-value rule to sum |v - ref| about
+// a value of the window (zero iff every value equals it; the result is then
+// the newest value, times the count for a sum). No min / max, no selects per
+// value; a complete window's sum is the same sum in the same order as before.
 struct SpAgg {
-  double s, mn, mx, last;
-  int n;
-  unsigned sor, sand;
+  double s, sa;
+  int n, neg;
   __device__ __forceinline__ void init() {
-    s = 0.0;
-    mn = __builtin_inf();
-    mx = -__builtin_inf();
-    last = qnan();
-    n = 0;
-    sor = 0u;
-    sand = 1u;
+    s = sa = 0.0;
+    n = neg = 0;
   }
-  __device__ __forceinline__ void add(double v) {
-    const bool ok = win_ok(v);   // NaN and +-inf are missing (pandas' window ops); v only under ok
-    const unsigned sg = (unsigned)((unsigned long long)__double_as_longlong(v) >> 63);
-    s += ok ? v : 0.0;
-    n += ok;
-    sor |= ok ? sg : 0u;
-    sand &= ok ? sg : 1u;
-    mn = ok ? fmin(mn, v) : mn;
-    mx = ok ? fmax(mx, v) : mx;
-    last = ok ? v : last;
+  __device__ __forceinline__ void add(double v, double ref) {
+    n += win_ok(v);
+    neg += (int)((unsigned long long)__double_as_longlong(v) >> 63);
+    s += v;
+    sa += fabs(v - ref);
   }
   // this (older) followed by b (newer)
   __device__ __forceinline__ SpAgg then(const SpAgg& b) const {
     SpAgg r;
     r.s = s + b.s;
+    r.sa = sa + b.sa;
     r.n = n + b.n;
-    r.sor = sor | b.sor;
-    r.sand = sand & b.sand;
-    r.mn = fmin(mn, b.mn);
-    r.mx = fmax(mx, b.mx);
-    r.last = b.n > 0 ? b.last : last;
+    r.neg = neg + b.neg;
     return r;
   }
 };
 
+// last: the window's newest value
 template <bool MEAN>
-__device__ __forceinline__ double sp_finish(const SpAgg& a, int t, int w) {
-  if (t < w - 1 || a.n < w || a.n <= 0) return qnan();
-  const bool same = a.mn == a.mx;
-  if (!MEAN) return same ? a.last * (double)a.n : a.s;
+__device__ __forceinline__ double sp_finish(const SpAgg& a, int t, int w, double last) {
+  if (t < w - 1 || a.n < w) return qnan();
+  const bool same = a.sa == 0.0;
+  if (!MEAN) return same ? last * (double)a.n : a.s;
   double r = a.s / (double)a.n;
-  if (same) r = a.last;
-  else if (a.sor == 0u && r < 0.0) r = 0.0;
-  else if (a.sand == 1u && r > 0.0) r = 0.0;
+  if (same) r = last;
+  else if (a.neg == 0 && r < 0.0) r = 0.0;
+  else if (a.neg == a.n && r > 0.0) r = 0.0;
   return r;
 }
 
+// x.rolling(w).sum() / .mean() at candle t over values f(j), j = -w+1 .. 0
+// (time order)
+template <bool MEAN, typename F>
+__device__ __forceinline__ double sp_window(int t, int w, F f) {
+  if (t < w - 1) return qnan();
+  const double last = f(0);
+  SpAgg a;
+  a.init();
+  for (int j = -w + 1; j <= 0; ++j) a.add(f(j), last);
+  return sp_finish<MEAN>(a, t, w, last);
+}
+
+// The same statistic at a lane's SP_K consecutive candles tb .. tb + 3 (ring
+// positions pb .. pb + 3): their windows share the W - 3 positions
+// pb + 4 - W .. pb, aggregated once; each candle adds its own older (lead) and
+// newer (trail) extras — W + 3 values read instead of 4 W. The sum is
+// (lead + core) + trail instead of strictly time-ordered (rounding). The
+// reference of the same-value test: the value at pb, inside every one of the
+// lane's windows.
 // F(p): the value at ring position p (windows shorter than SP_K: one
 // aggregate per candle)
 template <bool MEAN, typename F>
@@ -168,16 +144,18 @@ __device__ __forceinline__ void sp_window4(int tb, int pb, int w, F f, double (&
   if (w < SP_K) {
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
+      const double last = f(pb + k);
       SpAgg a;
       a.init();
-      for (int p = pb + k - w + 1; p <= pb + k; ++p) a.add(f(p));
-      r[k] = sp_finish<MEAN>(a, tb + k, w);
+      for (int p = pb + k - w + 1; p <= pb + k; ++p) a.add(f(p), last);
+      r[k] = sp_finish<MEAN>(a, tb + k, w, last);
     }
     return;
   }
+  const double ref = f(pb);
   SpAgg core;
   core.init();
-  for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p));
+  for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p), ref);
   SpAgg trail;
   trail.init();
   SpAgg lead[SP_K];
@@ -186,13 +164,14 @@ __device__ __forceinline__ void sp_window4(int tb, int pb, int w, F f, double (&
   for (int k = SP_K - 2; k >= 0; --k) {   // lead_k = value at pb + k + 1 - w, then lead_{k+1}
     SpAgg one;
     one.init();
-    one.add(f(pb + k + 1 - w));
+    one.add(f(pb + k + 1 - w), ref);
     lead[k] = one.then(lead[k + 1]);
   }
 #pragma unroll
   for (int k = 0; k < SP_K; ++k) {
-    if (k > 0) trail.add(f(pb + k));
-    r[k] = sp_finish<MEAN>(lead[k].then(core).then(trail), tb + k, w);
+    const double last = f(pb + k);
+    if (k > 0) trail.add(last, ref);
+    r[k] = sp_finish<MEAN>(lead[k].then(core).then(trail), tb + k, w, last);
   }
 }
 
@@ -216,45 +195,41 @@ __device__ __forceinline__ double sp_count(int t, int w, F f) {
 // std is small against the values (~1e-8 relative at std / mean ~ 2e-5): the
 // panel result is then the one closer to the exactly computed value
 // (tests/test_spike_std_gpu.py). pandas' rules: a missing value in the window
-// -> NaN (min_periods = w); n <= 1 -> NaN; every observed value equal -> 0.
+// -> NaN (min_periods = w); n <= 1 -> NaN; every value equal (sum |d| == 0)
+// -> 0.
 struct SpVar {
-  double s1, s2, mn, mx;
+  double s1, s2, sa;
   int n;
   __device__ __forceinline__ void init() {
-    s1 = s2 = 0.0;
-    mn = __builtin_inf();
-    mx = -__builtin_inf();
+    s1 = s2 = sa = 0.0;
     n = 0;
   }
   __device__ __forceinline__ void add(double v, double r) {
-    const bool ok = win_ok(v);
-    const double d = ok ? v - r : 0.0;
+    n += win_ok(v);
+    const double d = v - r;
     s1 += d;
     s2 = fma(d, d, s2);
-    n += ok;
-    mn = ok ? fmin(mn, v) : mn;
-    mx = ok ? fmax(mx, v) : mx;
+    sa += fabs(d);
   }
   __device__ __forceinline__ SpVar then(const SpVar& b) const {
     SpVar x;
     x.s1 = s1 + b.s1;
     x.s2 = s2 + b.s2;
-    x.mn = fmin(mn, b.mn);
-    x.mx = fmax(mx, b.mx);
+    x.sa = sa + b.sa;
     x.n = n + b.n;
     return x;
   }
 };
 
+__device__ __forceinline__ double sp_var_finish(double s1, double s2, double sa, int n, int t, int w) {
+  if (t < w - 1 || w <= 1 || n < w) return qnan();
+  if (sa == 0.0) return 0.0;
+  const double var = (s2 - s1 * (s1 / (double)n)) / (double)(n - 1);
+  return sqrt(var > 0.0 ? var : 0.0);
+}
+
 template <typename F>
 __device__ __forceinline__ void sp_std4(int tb, int pb, int w, F f, double (&r)[SP_K]) {
-  const double ref = f(pb);
-  auto fin = [&](const SpVar& a, int t) -> double {
-    if (t < w - 1 || w <= 1 || a.n < w) return qnan();
-    if (a.mn == a.mx) return 0.0;
-    const double var = (a.s2 - a.s1 * (a.s1 / (double)a.n)) / (double)(a.n - 1);
-    return sqrt(var > 0.0 ? var : 0.0);
-  };
   if (w < SP_K) {   // windows shorter than the lane: each about its own newest value
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
@@ -262,10 +237,11 @@ __device__ __forceinline__ void sp_std4(int tb, int pb, int w, F f, double (&r)[
       a.init();
       const double rk = f(pb + k);
       for (int p = pb + k - w + 1; p <= pb + k; ++p) a.add(f(p), rk);
-      r[k] = fin(a, tb + k);
+      r[k] = sp_var_finish(a.s1, a.s2, a.sa, a.n, tb + k, w);
     }
     return;
   }
+  const double ref = f(pb);
   SpVar core;
   core.init();
   for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p), ref);
@@ -282,14 +258,13 @@ __device__ __forceinline__ void sp_std4(int tb, int pb, int w, F f, double (&r)[
 #pragma unroll
   for (int k = 0; k < SP_K; ++k) {
     if (k > 0) trail.add(f(pb + k), ref);
-    r[k] = fin(lead[k].then(core).then(trail), tb + k);
+    const SpVar x = lead[k].then(core).then(trail);
+    r[k] = sp_var_finish(x.s1, x.s2, x.sa, x.n, tb + k, w);
   }
 }
 
-// sp_window4<true> and sp_std4 over the same window in ONE walk of the ring:
-// the mean's aggregate (SpAgg: sum, count, min / max, signs) and the std's
-// reference-shifted sums advance together (the count and min / max serve
-// both). Same values as the two separate calls.
+// sp_window4<true> and sp_std4 over the same window in ONE walk of the ring
+// (the count and sum |d| serve both). Same values as the two separate calls.
 struct SpAggV {
   SpAgg a;
   double s1, s2;
@@ -298,8 +273,8 @@ struct SpAggV {
     s1 = s2 = 0.0;
   }
   __device__ __forceinline__ void add(double v, double r) {
-    a.add(v);
-    const double d = win_ok(v) ? v - r : 0.0;
+    a.add(v, r);
+    const double d = v - r;
     s1 += d;
     s2 = fma(d, d, s2);
   }
@@ -320,12 +295,6 @@ __device__ __forceinline__ void sp_mean_std4(int tb, int pb, int w, F f, double 
     return;
   }
   const double ref = f(pb);
-  auto fin_sd = [&](const SpAggV& x, int t) -> double {
-    if (t < w - 1 || w <= 1 || x.a.n < w) return qnan();
-    if (x.a.mn == x.a.mx) return 0.0;
-    const double var = (x.s2 - x.s1 * (x.s1 / (double)x.a.n)) / (double)(x.a.n - 1);
-    return sqrt(var > 0.0 ? var : 0.0);
-  };
   SpAggV core;
   core.init();
   for (int p = pb + SP_K - w; p <= pb; ++p) core.add(f(p), ref);
@@ -341,10 +310,11 @@ __device__ __forceinline__ void sp_mean_std4(int tb, int pb, int w, F f, double 
   }
 #pragma unroll
   for (int k = 0; k < SP_K; ++k) {
-    if (k > 0) trail.add(f(pb + k), ref);
+    const double last = f(pb + k);
+    if (k > 0) trail.add(last, ref);
     const SpAggV x = lead[k].then(core).then(trail);
-    ma[k] = sp_finish<true>(x.a, tb + k, w);
-    sd[k] = fin_sd(x, tb + k);
+    ma[k] = sp_finish<true>(x.a, tb + k, w, last);
+    sd[k] = sp_var_finish(x.s1, x.s2, x.a.sa, x.a.n, tb + k, w);
   }
 }
 
