@@ -574,6 +574,10 @@ struct SpikeFlagArgs {
 // 4 workgroups per CU (120 VGPRs, no spill): a19 -0.06 ms (A/B, same box)
 __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagArgs A, int vin, int vout, int vb) {
   __shared__ double sF[SP_R], sP[SP_R], sVR[SP_R], sTP[SP_R];
+  // the cluster conditions per candle, one byte each in time order (bit 0:
+  // VR >= VC, bit 1: VR >= 0.8 VC; 0 before the row and for a missing ratio),
+  // so a lane's 36-candle condition masks are 9 dword reads, not 36 compares
+  __shared__ uint32_t sCB[SP_R / 4];
   __shared__ int sW[SP_NW];
   __shared__ int sCar;
   __shared__ double sTV;   // threshold carried across tiles (the ffill)
@@ -583,6 +587,8 @@ __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagAr
   const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
   const double VC = A.vcmr[sym], PB = A.pbbt[sym];
   if (tid < SP_H) sF[sp_slot(tid)] = sP[sp_slot(tid)] = sVR[sp_slot(tid)] = sTP[sp_slot(tid)] = qnan();
+  if (tid < SP_H / 4) sCB[tid] = 0u;
+  const double vc8 = VC * 0.8;
   if (tid == 0) {
     sCar = -1;
     sTV = qnan();
@@ -599,9 +605,11 @@ __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagAr
     const double vr_next = tb + SP_K < T ? A.in[SF_VR][irow + tb + SP_K] : qnan();
     int lv[SP_K];
     int last = -1;
+    uint32_t cb = 0u;
 #pragma unroll
     for (int k = 0; k < SP_K; ++k) {
       const int t = tb + k;
+      cb |= ((vr[k] >= VC ? 1u : 0u) | (vr[k] >= vc8 ? 2u : 0u)) << (8 * k);
       // where(isnan(D), D, maximum(PB, D)): NaN stays, else the larger
       const double d = dy[k];
       const double tp = d != d ? d : (PB != PB ? qnan() : (PB > d ? PB : d));
@@ -611,6 +619,7 @@ __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagAr
       sVR[sp_slot(pb + k)] = vr[k];
       sTP[sp_slot(pb + k)] = tp;
     }
+    sCB[pb / 4] = cb;
     {
       const int inc = wave_scan_max_dpp(lv[SP_K - 1] + 1, lane);
       if (lane == WAVE - 1) sW[w] = inc - 1;
@@ -640,13 +649,19 @@ __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagAr
     // before the row and missing ratios: 0): VR >= VC and VR >= 0.8 VC
     uint64_t m1 = 0, m8 = 0;
     {
-      const double vc8 = VC * 0.8;
-#pragma unroll 4
-      for (int u = 0; u < 36; ++u) {
-        const double x = u < 35 ? sVR[sp_slot(pb - 31 + u)] : vr_next;
-        m1 |= (uint64_t)(x >= VC) << u;
-        m8 |= (uint64_t)(x >= vc8) << u;
+      // candles pb - 32 .. pb + 3 from 9 dwords of bytes: the low bit of each
+      // byte gathered into a nibble by one multiply (the 4 partial products'
+      // bits never meet), bit j <-> candle pb - 32 + j
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const uint32_t wd = sCB[(pb - SP_H) / 4 + i];
+        const uint32_t n1 = (((wd & 0x01010101u) * 0x204081u) >> 21) & 0xFu;
+        const uint32_t n8 = ((((wd >> 1) & 0x01010101u) * 0x204081u) >> 21) & 0xFu;
+        m1 |= (uint64_t)n1 << (4 * i);
+        m8 |= (uint64_t)n8 << (4 * i);
       }
+      m1 = (m1 >> 1) | ((uint64_t)(vr_next >= VC) << 35);
+      m8 = (m8 >> 1) | ((uint64_t)(vr_next >= vc8) << 35);
     }
     // bits of the window of w candles ending at candle tb + e (e <= 4)
     auto win_bits = [&](uint64_t m, int e, int w) { return (m >> (31 + e - w + 1)) & ((1ull << w) - 1ull); };
@@ -739,6 +754,7 @@ __global__ __launch_bounds__(SP_NT, 4) void spike_flags_kernel(const SpikeFlagAr
         sVR[d] = sVR[a];
         sTP[d] = sTP[a];
       }
+      sCB[(pb - SP_TT) / 4] = sCB[pb / 4];
     }
     if (tid == SP_NT - 1) {
       sCar = lv[SP_K - 1];
