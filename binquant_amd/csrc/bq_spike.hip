@@ -337,7 +337,10 @@ struct SpikeBaseArgs {
 #ifndef BQ_SP_TP_WGS
 #define BQ_SP_TP_WGS 3   // workgroups per CU of the TP instantiation
 #endif
-template <bool TP>
+// WC > 0: the base window (and streak length SN) as compile-time constants
+// (the strategy's defaults): the window walks unroll and their ring slots
+// become lane-base + immediate offsets instead of per-element index math
+template <bool TP, int WC = 0, int SN = 0>
 __global__ __launch_bounds__(SP_NT, TP ? BQ_SP_TP_WGS : 3) void spike_base_kernel(const SpikeBaseArgs A, int vin, int vout,
                                                                                 int vb) {
   // rings: close, ffilled close, volume, quote volume, body size pct, pct
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(SP_NT, TP ? BQ_SP_TP_WGS : 3) void spike_base_kerne
   __shared__ signed char sG[SP_R];   // +1 close > open, -1 close < open, 0 otherwise
   const int tid = threadIdx.x;
   const int64_t sym = blockIdx.x;
-  const int T = A.T, W = A.w, N = A.n;
+  const int T = A.T, W = WC > 0 ? WC : A.w, N = SN > 0 ? SN : A.n;
   const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
   if (tid < SP_H) {
     sC[sp_slot(tid)] = sF[sp_slot(tid)] = sV[sp_slot(tid)] = sQ[sp_slot(tid)] = qnan();
@@ -803,7 +806,10 @@ static int spike_base_launch(const double* const* in, int nin, int64_t S, int64_
     if (A.sd[c]) vout &= sp_aligned(A.sd[c], 16);
   for (int c = 0; c < BQ_NUM_SPIKE_BASE_B; ++c)
     if (out_b[c]) vb &= sp_aligned(out_b[c], 4);
-  if (tp)
+  if (tp && base_window == 12 && streak_length == 3)   // SpikeParams' defaults
+    hipLaunchKernelGGL((spike_base_kernel<true, 12, 3>), dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin,
+                       vout, vb);
+  else if (tp)
     hipLaunchKernelGGL(spike_base_kernel<true>, dim3((unsigned)S), dim3(SP_NT), 0, (hipStream_t)stream, A, vin, vout,
                        vb);
   else
