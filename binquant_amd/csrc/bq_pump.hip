@@ -94,10 +94,13 @@ __device__ __forceinline__ void pf_load(const double* __restrict__ row, int tb, 
 __device__ __forceinline__ double clip0(double x) { return x < 0.0 ? 0.0 : x; }
 __device__ __forceinline__ double rep0(double x) { return x == 0.0 ? qnan() : x; }
 
-template <bool EWM_IN>
 // 3 workgroups per CU for the default pass (168 VGPRs, 8 B of spill): its
 // inputs are loaded at the tile start instead of a tile ahead (the prefetch's
-// 32 registers cost a workgroup per CU) — a18 1.91-2.01 -> 1.86-1.87 ms (A/B)
+// 32 registers cost a workgroup per CU) — a18 1.91-2.01 -> 1.86-1.87 ms (A/B).
+// MC / VWC / CWC > 0: the momentum lag, volume lookback and compression
+// window as compile-time constants (PumpParams' defaults 3 / 20 / 6): the
+// window walks unroll, their ring slots become immediate offsets
+template <bool EWM_IN, int MC = 0, int VWC = 0, int CWC = 0>
 __global__ __launch_bounds__(PF_NT, EWM_IN ? 2 : 3) void pump_features_kernel(const PumpArgs A, int vin, int vout) {
   __shared__ double sH[PF_R], sL[PF_R], sC[PF_R], sV[PF_R], sF[PF_R];
   __shared__ double sEB[EWM_IN ? 3 : 1][PF_NW];   // the waves' scan totals
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(PF_NT, EWM_IN ? 2 : 3) void pump_features_kernel(co
   __shared__ double sFV;      // ffilled close at the end of the previous tile
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), w = tid / WAVE;
   const int64_t sym = blockIdx.x;
-  const int T = A.T, M = A.mom, VW = A.vol_w, CW = A.comp_w;
+  const int T = A.T, M = MC > 0 ? MC : A.mom, VW = VWC > 0 ? VWC : A.vol_w, CW = CWC > 0 ? CWC : A.comp_w;
   const int64_t irow = sym * A.ld_in, orow = sym * A.ld_out;
   if (tid < PF_H) {   // before the row: missing values
     sH[pf_slot(tid)] = sL[pf_slot(tid)] = sC[pf_slot(tid)] = sV[pf_slot(tid)] = sF[pf_slot(tid)] = qnan();
@@ -486,8 +489,12 @@ extern "C" int bq_pump_features(const double* const* in, int64_t S, int64_t T, i
     if (in[f]) vin &= aligned(in[f]);
   for (int c = 0; c < BQ_NUM_PUMP_COLS; ++c)
     if (out[c]) vout &= aligned(out[c]);
-  hipLaunchKernelGGL(pump_features_kernel<false>, dim3((unsigned)S), dim3(PF_NT), 0, (hipStream_t)stream, A, vin,
-                     vout);
+  if (momentum_bars == 3 && volume_lookback == 20 && compression_bars == 6)   // PumpParams' defaults
+    hipLaunchKernelGGL((pump_features_kernel<false, 3, 20, 6>), dim3((unsigned)S), dim3(PF_NT), 0, (hipStream_t)stream, A,
+                       vin, vout);
+  else
+    hipLaunchKernelGGL(pump_features_kernel<false>, dim3((unsigned)S), dim3(PF_NT), 0, (hipStream_t)stream, A, vin,
+                       vout);
   return hipGetLastError() == hipSuccess ? BQ_OK : BQ_EHIP;
 }
 
