@@ -362,16 +362,18 @@ __global__ __launch_bounds__(PF_NT, EWM_IN ? 2 : 3) void pump_features_kernel(co
           else if (neg == 0 && vmean < 0.0) vmean = 0.0;
           else if (neg == nobs && vmean > 0.0) vmean = 0.0;
         }
-        // high.shift(1).rolling(CW).max(), low ... .min() (min_periods = window)
+        // high.shift(1).rolling(CW).max(), low ... .min() (min_periods = window:
+        // a window with a missing value is NaN whatever else it holds, so the
+        // extremes take every value unmasked — v_max / v_min skip a NaN — and
+        // the observed counts decide; NaN and +-inf are missing, window op)
         double hm = -__builtin_inf(), lm = __builtin_inf();
         int nh = 0, nl = 0;
         for (int j = -CW; j <= -1; ++j) {
           const double hv = sH[pf_slot(p + j)], lv = sL[pf_slot(p + j)];
-          const bool oh = win_ok(hv), ol = win_ok(lv);   // NaN and +-inf are missing (window op)
-          nh += oh;
-          nl += ol;
-          hm = oh && hv > hm ? hv : hm;
-          lm = ol && lv < lm ? lv : lm;
+          nh += win_ok(hv);
+          nl += win_ok(lv);
+          hm = fmax(hm, hv);
+          lm = fmin(lm, lv);
         }
         hmax[k] = nh >= CW ? hm : qnan();
         const double lmin = nl >= CW ? lm : qnan();
