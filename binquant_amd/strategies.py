@@ -405,9 +405,11 @@ def failed_spike_features(o, h, l, c, v, qv, p: SpikeParams | None = None,
     RangeIndex). Integer columns come back as torch.bool (label_pre /
     label_short_pre likewise); 'volume_cluster_min_ratio' and
     'price_break_base_threshold' hold the per-symbol auto-calibrated values.
-    exact=True: the rolling sums / means by the bit-exact replay (the live
-    path); default: time-parallel within rounding of pandas (panel mode; the
-    rolling std / var stay the replay of pandas' online variance)."""
+    exact=True: the rolling sums / means / stds by the bit-exact replay (the
+    live path); default: panel mode, within rounding of pandas — the fused
+    passes form the five rolling std columns from window sums about an
+    in-window reference (the exact window std to rounding, where pandas'
+    online variance may drift; BQ_SPIKE_STD_IN_PASS=0 keeps the replay)."""
     p = p or SpikeParams()
     eps = 1e-6
     S, T = c.shape
