@@ -127,7 +127,8 @@ __device__ __forceinline__ double cx_div(double a, double b) { return cx_mul_rcp
 // FEAT: bq_market_features — the six feature columns written (whole-line
 // stores of each wave's row) instead of reduced: no group records, no
 // workgroup barrier
-template <bool DIV, bool RING, bool FEAT = false>
+// MC > 0: the history cap as a compile-time constant (the store's 400 bars)
+template <bool DIV, bool RING, bool FEAT = false, int MC = 0>
 __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArgs A) {
   __shared__ double sTr[CX_NW][CX_RS], sC[CX_NW][CX_RS];   // true range / close rings per wave
   __shared__ double sR[2][4][CX_TT];   // reduction slots: 4 sums, index k * 64 + lane
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(CX_NT, 3) void context_partials_kernel(const CtxArg
   const int64_t sym = grp * CX_NW + w;
   const bool live = sym < A.S;                  // wave-uniform
   const int64_t row = live ? sym : A.S - 1;     // idle waves walk a valid row, contribute nothing
-  const int T = A.T, M = A.M;
+  const int T = A.T, M = MC > 0 ? MC : A.M;
   const double* __restrict__ rH = A.h + row * A.ld_in;
   const double* __restrict__ rL = A.l + row * A.ld_in;
   const double* __restrict__ rC = A.c + row * A.ld_in;
@@ -744,10 +745,14 @@ int bq_context_partials(const double* const* hlc, int64_t S, int64_t T, int64_t 
   // then below 1e-15 and skipped
   const bool ring = A.corr[1] <= 1e-6 && !A.lag20;
   if (A.den[0] != 1.0 || A.den[1] != 1.0) {
-    if (ring) hipLaunchKernelGGL((context_partials_kernel<true, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    if (ring && max_bars == 400)   // MarketStateStore's default cap
+      hipLaunchKernelGGL((context_partials_kernel<true, true, false, 400>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    else if (ring) hipLaunchKernelGGL((context_partials_kernel<true, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
     else hipLaunchKernelGGL((context_partials_kernel<true, false>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
   } else {
-    if (ring) hipLaunchKernelGGL((context_partials_kernel<false, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    if (ring && max_bars == 400)
+      hipLaunchKernelGGL((context_partials_kernel<false, true, false, 400>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
+    else if (ring) hipLaunchKernelGGL((context_partials_kernel<false, true>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
     else hipLaunchKernelGGL((context_partials_kernel<false, false>), dim3((unsigned)L.ngrp), dim3(CX_NT), 0, st, A);
   }
   GroupReduceArgs G;
