@@ -149,6 +149,23 @@ def test_row_quantile_is_numpy_bitwise(cuda, T):
             np.testing.assert_array_equal(got[s], want, err_msg=f"q={q} row {s}")
 
 
+def test_row_quantile_strided_rows(cuda):
+    """Rows of a padded buffer (row stride > T, as enrich_outputs lays them
+    out) give the contiguous rows' quantiles bit for bit."""
+    from binquant_amd import engine
+
+    rng = np.random.default_rng(13)
+    for T in (700, 2000):
+        x = rng.lognormal(0, 1, (37, T))
+        x[rng.random(x.shape) < 0.05] = np.nan
+        buf = torch.full((37, T + 40), 1e300, dtype=torch.float64, device="cuda")
+        buf[:, :T] = torch.from_numpy(x).cuda()
+        for q in (0.75, 0.97):
+            got = engine.row_quantile(buf[:, :T], q).cpu().numpy()
+            want = engine.row_quantile(torch.from_numpy(x).cuda(), q).cpu().numpy()
+            np.testing.assert_array_equal(got, want)
+
+
 def test_row_quantile_large_rows(cuda):
     from binquant_amd import engine
 
